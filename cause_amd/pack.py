@@ -1,0 +1,171 @@
+"""Host-side marshalling for the weave C-ABI: site interning and id packing.
+
+The GPU path works on order-preserving packed 64-bit ids:
+
+    key = ts << (site_bits + tx_bits) | site_rank << tx_bits | tx
+
+so that ``key(a) < key(b)`` iff ``(compare a b) < 0`` for ids ``[ts site tx]``
+(util.cljc:4-10; ids are ``::s/id`` tuples, shared.cljc:31-40).  Site-ids are
+ranked per document in Java ``String.compareTo`` order (UTF-16 code units), over
+every site that appears in a node id *or* a cause id of that document, so a
+cause pointing at an absent node still packs to a distinct, correctly ordered
+key (it is then reported as an orphan by the GPU, never matched by accident).
+
+Kinds (shared.cljc:21): 0 normal value, 1 ``:causal/hide``, 2 ``:causal/h.hide``,
+3 ``:causal/h.show``; bit 2 flags the root node ``[[0 "0" 0] nil nil]``.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+NIL = (1 << 64) - 1          # Clojure nil as a cause (root), CW_NIL in causeweave.h
+NON_ID_CAUSE = NIL - 1       # a list node whose cause is not an id (never matches)
+
+KIND_NORMAL, KIND_HIDE, KIND_HHIDE, KIND_HSHOW, KIND_ROOT = 0, 1, 2, 3, 4
+
+
+def _special_names():
+    return {("causal", "hide"): KIND_HIDE, ("causal", "h.hide"): KIND_HHIDE,
+            ("causal", "h.show"): KIND_HSHOW}
+
+
+_SPECIAL = _special_names()
+ROOT_ID = (0, "0", 0)
+
+
+def kind_of(value) -> int:
+    """Value class of a node value: keywords with ns/name attributes
+    (``causal/hide`` ...) are special (shared.cljc:21); anything else is normal."""
+    ns = getattr(value, "ns", None)
+    name = getattr(value, "name", None)
+    if ns is not None and name is not None:
+        return _SPECIAL.get((ns, name), KIND_NORMAL)
+    return KIND_NORMAL
+
+
+def java_str_key(s: str) -> bytes:
+    """String.compareTo order: compare UTF-16 code units."""
+    return s.encode("utf-16-be")
+
+
+def is_id(x) -> bool:
+    return isinstance(x, tuple) and len(x) == 3 and isinstance(x[1], str)
+
+
+@dataclass(frozen=True)
+class KeyLayout:
+    """Bit layout of packed ids (shared by every document of a batch)."""
+
+    ts_bits: int
+    site_bits: int
+    tx_bits: int
+
+    @property
+    def tx_shift(self) -> int:
+        return 0
+
+    @property
+    def site_shift(self) -> int:
+        return self.tx_bits
+
+    @property
+    def ts_shift(self) -> int:
+        return self.tx_bits + self.site_bits
+
+    @property
+    def key_bits(self) -> int:
+        return self.ts_bits + self.site_bits + self.tx_bits
+
+    def pack(self, ts: int, site_rank: int, tx: int) -> int:
+        return (ts << self.ts_shift) | (site_rank << self.site_shift) | tx
+
+
+class KeyRangeError(ValueError):
+    """Ids do not fit a 64-bit key (CW_STATUS_KEY_RANGE)."""
+
+
+def _bits(v: int) -> int:
+    return max(int(v).bit_length(), 0)
+
+
+def intern_sites(ids) -> dict:
+    """Order-preserving site ranks for one document (String.compareTo order)."""
+    sites = sorted({i[1] for i in ids}, key=java_str_key)
+    return {s: r for r, s in enumerate(sites)}
+
+
+@dataclass
+class PackedDoc:
+    id_key: np.ndarray     # uint64 [n]
+    cause_key: np.ndarray  # uint64 [n]
+    kind: np.ndarray       # uint8  [n]
+    nodes: list            # the input nodes, in the packed order
+    site_rank: dict
+
+
+def layout_for(docs) -> KeyLayout:
+    """Smallest layout that holds every id and id-cause of ``docs``
+    (each doc: iterable of nodes ``(id, cause, value)``)."""
+    mts = msite = mtx = 0
+    for nodes in docs:
+        ids = [n[0] for n in nodes] + [n[1] for n in nodes if is_id(n[1])]
+        sites = {i[1] for i in ids}
+        msite = max(msite, len(sites) - 1 if sites else 0)
+        for ts, _, tx in ids:
+            if ts < 0 or tx < 0:
+                raise KeyRangeError("negative ts/tx-index")
+            mts = max(mts, ts)
+            mtx = max(mtx, tx)
+    lay = KeyLayout(_bits(mts), _bits(msite), _bits(mtx))
+    if lay.key_bits > 63:
+        raise KeyRangeError(f"ids need {lay.key_bits} bits (> 63)")
+    return lay
+
+
+def pack_doc(nodes, layout: KeyLayout) -> PackedDoc:
+    """Pack one document's nodes (``(id, cause, value)`` tuples, any order)."""
+    nodes = list(nodes)
+    ids = [n[0] for n in nodes] + [n[1] for n in nodes if is_id(n[1])]
+    rank = intern_sites(ids)
+    n = len(nodes)
+    idk = np.empty(n, np.uint64)
+    ck = np.empty(n, np.uint64)
+    kd = np.empty(n, np.uint8)
+    for i, (nid, cause, value) in enumerate(nodes):
+        idk[i] = layout.pack(nid[0], rank[nid[1]], nid[2])
+        if cause is None:
+            ck[i] = NIL
+        elif is_id(cause):
+            ck[i] = layout.pack(cause[0], rank[cause[1]], cause[2])
+        else:
+            ck[i] = NON_ID_CAUSE
+        k = kind_of(value)
+        if nid == ROOT_ID and cause is None and value is None:
+            k |= KIND_ROOT
+        kd[i] = k
+    return PackedDoc(idk, ck, kd, nodes, rank)
+
+
+@dataclass
+class PackedBatch:
+    offsets: np.ndarray    # uint64 [D+1]
+    id_key: np.ndarray     # uint64 [N]
+    cause_key: np.ndarray  # uint64 [N]
+    kind: np.ndarray       # uint8  [N]
+    layout: KeyLayout
+    docs: list             # PackedDoc per document
+
+
+def pack_lists(docs) -> PackedBatch:
+    """Pack a batch of list documents (each an iterable of nodes incl. root)."""
+    docs = [list(d) for d in docs]
+    lay = layout_for(docs)
+    packed = [pack_doc(d, lay) for d in docs]
+    off = np.zeros(len(docs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(d) for d in docs], dtype=np.uint64)
+    cat = lambda f, dt: (np.concatenate([getattr(p, f) for p in packed]) if packed
+                         else np.zeros(0, dt))
+    return PackedBatch(off, cat("id_key", np.uint64), cat("cause_key", np.uint64),
+                       cat("kind", np.uint8), lay, packed)
