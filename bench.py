@@ -1,0 +1,187 @@
+"""Benchmark: nodes woven/s for BASELINE.json configs[1] on MI355X.
+
+Workload (per GPU, weak scaling): 10,000 independent CausalLists of 50,001
+nodes each (root + 50,000 nodes from 8 sites: 10% hides, 2% h.shows, 5%
+conj-style causes), node order shuffled inside each
+document.  One step = one full reweave of the GPU's whole batch through the C
+ABI (cw_weave_lists, device memory): sorted ids, parents, weave order, rendered
+bits and counts per document.  Inputs are resident in HBM before timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--docs", type=int, default=10_000, help="documents per GPU")
+    ap.add_argument("--nodes", type=int, default=50_000, help="non-root nodes per document")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="budget of the cpu_baseline sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(spec, budget_s):
+    """The reference algorithm (literal weave-node fold, oracle/weave_oracle.c,
+    one core) on the first documents of this same workload, until ~budget_s."""
+    import oracle
+
+    done_nodes, t_total, ndocs = 0, 0.0, 0
+    from cause_amd import gen
+
+    while t_total < budget_s and ndocs < 64:
+        off, idk, ck, kd = gen.generate(spec, ndocs, ndocs + 1, nthreads=1)
+        t0 = time.perf_counter()
+        _, st = oracle.list_weave(idk, ck, kd, oracle.METHOD_LITERAL)
+        t_total += time.perf_counter() - t0
+        done_nodes += len(idk)
+        ndocs += 1
+    return {"value": done_nodes / t_total, "unit": "nodes/s", "cores": 1, "kind": "port",
+            "sample": f"{ndocs} documents x {spec.doc_size} nodes of the same workload, "
+                      f"literal weave-node fold (shared.cljc:194-241, list.cljc:26-28) "
+                      f"in C, {t_total:.1f} s"}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from cause_amd import abi, gen
+    import dataclasses
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
+    layout = spec.layout()
+    D = a.docs
+    d0 = rank * D  # weak scaling: each rank owns its own contiguous documents
+    t0 = time.time()
+    off, idk, ck, kd = gen.generate(spec, d0, d0 + D, nthreads=16)
+    N = len(idk)
+    t_gen = time.time() - t0
+    g_id = torch.from_numpy(idk.view(np.int64)).to(dev)
+    g_ca = torch.from_numpy(ck.view(np.int64)).to(dev)
+    g_kd = torch.from_numpy(kd).to(dev)
+    perm = torch.empty(N, dtype=torch.int32, device=dev)
+    bits = torch.empty((N + 31) // 32, dtype=torch.int32, device=dev)
+    vcount = torch.empty(D, dtype=torch.int32, device=dev)
+    max_ts = torch.empty(D, dtype=torch.int64, device=dev)
+    status = torch.empty(D, dtype=torch.int32, device=dev)
+    outs = {"weave_perm": perm.data_ptr(), "visible_bits": bits.data_ptr(),
+            "visible_count": vcount.data_ptr(), "max_ts": max_ts.data_ptr(),
+            "status": status.data_ptr()}
+    torch.cuda.synchronize()
+
+    w = abi.Weaver(local)
+    w.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    w.set_async(True)
+
+    def step():
+        w.weave_lists_device(off, g_id.data_ptr(), g_ca.data_ptr(), g_kd.data_ptr(), layout, outs)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if int(status.max().item()) != 0:
+        raise SystemExit(f"rank {rank}: documents out of domain: status max {status.max().item()}")
+
+    # timed region: per-kernel HIP events on the launch stream
+    w.reset_kernel_stats()
+    w.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    w.set_profiling(False)
+    stats = w.kernel_stats()
+
+    dt_max = dt
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt_max = float(t.item())
+    total_nodes = N * world * a.steps
+    value = total_nodes / dt_max
+
+    # dominant kernel = largest share of the measured kernel time
+    name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
+    achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    kernel_ms_total = sum(v[1] for v in stats.values())
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get(name)
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu:
+            cpu = cpu_baseline(spec, a.cpu_seconds)
+        line = {
+            "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
+            "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt_max / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "config2: independent CausalLists, full reweave",
+                       "docs_per_gpu": D, "nodes_per_doc": spec.doc_size,
+                       "nodes_per_gpu": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
+                       "p_show": spec.p_show, "p_conj": spec.p_conj,
+                       "key_bits": layout.key_bits, "parallelism": f"docs sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic,
+                         "launches_per_step": launches / a.steps,
+                         "kernel_ms_per_step": ms / a.steps},
+            "cpu_baseline": cpu,
+            "kernels_ms_per_step": {k: round(v[1] / a.steps, 4) for k, v in
+                                    sorted(stats.items(), key=lambda kv: -kv[1][1])},
+            "kernel_gbs": {k: round(v[2] / (v[1] / 1e3) / 1e9, 1) for k, v in stats.items()
+                           if v[1] > 0},
+            "kernel_sum_ms_per_step": kernel_ms_total / a.steps,
+            "gen_s": t_gen,
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    w.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

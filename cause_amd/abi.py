@@ -1,0 +1,196 @@
+"""ctypes binding of include/causeweave.h (libcauseweave.so).
+
+This is the Python side of the drop-in boundary: the same C entry points a JVM
+shim binds through Panama/JNA.  There is no fallback: if the
+HIP library is missing or fails, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcauseweave.so")
+HEADER = os.path.join(os.path.dirname(_HERE), "include", "causeweave.h")
+
+CW_MEM_HOST, CW_MEM_DEVICE = 0, 1
+STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1, 2, 4, 8, 32
+
+
+class CwListBatch(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("doc_offsets", C.POINTER(C.c_uint64)),
+                ("id_key", C.c_void_p), ("cause_key", C.c_void_p), ("kind", C.c_void_p),
+                ("key_bits", C.c_uint32), ("ts_shift", C.c_uint32), ("site_shift", C.c_uint32),
+                ("site_bits", C.c_uint32)]
+
+
+class CwListResult(C.Structure):
+    _fields_ = [("weave_perm", C.c_void_p), ("visible_bits", C.c_void_p),
+                ("visible_count", C.c_void_p), ("max_ts", C.c_void_p), ("status", C.c_void_p),
+                ("yarn_perm", C.c_void_p)]
+
+
+class CwKernelStat(C.Structure):
+    _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double),
+                ("bytes_alg", C.c_double)]
+
+
+_LIB = None
+
+
+class WeaveError(RuntimeError):
+    pass
+
+
+def header_functions():
+    """Names of every function declared in include/causeweave.h."""
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(cw_\w+)\s*\(", src, re.M)))
+
+
+def lib():
+    """Load libcauseweave.so (raises if it was not built)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise WeaveError(f"{LIB_PATH} is missing: build it (python -c "
+                             "'import __graft_entry__ as g; g.build()' or `make`)")
+        L = C.CDLL(LIB_PATH)
+        L.cw_abi_version.restype = C.c_int
+        L.cw_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.cw_ctx_create.restype = C.c_int
+        L.cw_ctx_destroy.argtypes = [C.c_void_p]
+        L.cw_ctx_destroy.restype = None
+        L.cw_last_error.argtypes = [C.c_void_p]
+        L.cw_last_error.restype = C.c_char_p
+        L.cw_ctx_set_stream.argtypes = [C.c_void_p, C.c_void_p]
+        L.cw_ctx_set_async.argtypes = [C.c_void_p, C.c_int]
+        L.cw_ctx_set_profiling.argtypes = [C.c_void_p, C.c_int]
+        L.cw_get_kernel_stats.argtypes = [C.c_void_p, C.POINTER(CwKernelStat), C.c_int]
+        L.cw_reset_kernel_stats.argtypes = [C.c_void_p]
+        L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
+                                     C.c_int]
+        L.cw_weave_lists.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+@dataclass
+class ListResult:
+    weave_perm: np.ndarray     # uint32[N] doc-local input index per weave position
+    visible_bits: np.ndarray   # uint32[(N+31)//32]
+    visible_count: np.ndarray  # uint32[D]
+    max_ts: np.ndarray         # uint64[D]
+    status: np.ndarray         # uint32[D]
+    yarn_perm: np.ndarray | None
+
+    def visible(self) -> np.ndarray:
+        """uint8[N]: 1 where the global weave position renders."""
+        n = len(self.weave_perm)
+        b = np.unpackbits(self.visible_bits.view(np.uint8), bitorder="little")
+        return b[:n]
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None else None
+
+
+class Weaver:
+    """A weave context on one HIP device (cw_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self._L = lib()
+        h = C.c_void_p()
+        rc = self._L.cw_ctx_create(device, C.byref(h))
+        if rc != 0 or not h:
+            raise WeaveError(f"cw_ctx_create(device={device}) failed: no usable HIP device")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.cw_ctx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise WeaveError(f"{what}: {self._L.cw_last_error(self._h).decode()}")
+
+    def set_stream(self, stream_ptr):
+        self._check(self._L.cw_ctx_set_stream(self._h, C.c_void_p(stream_ptr)), "set_stream")
+
+    def set_async(self, on: bool):
+        self._check(self._L.cw_ctx_set_async(self._h, int(on)), "set_async")
+
+    def set_profiling(self, on: bool):
+        self._check(self._L.cw_ctx_set_profiling(self._h, int(on)), "set_profiling")
+
+    def kernel_stats(self):
+        n = self._L.cw_get_kernel_stats(self._h, None, 0)
+        arr = (CwKernelStat * max(n, 1))()
+        self._L.cw_get_kernel_stats(self._h, arr, n)
+        return {a.name.decode(): (a.launches, a.total_ms, a.bytes_alg) for a in arr[:n]}
+
+    def reset_kernel_stats(self):
+        self._L.cw_reset_kernel_stats(self._h)
+
+    @staticmethod
+    def _batch(offsets, id_ptr, cause_ptr, kind_ptr, layout, key_bits=None):
+        off = np.ascontiguousarray(offsets, np.uint64)
+        b = CwListBatch()
+        b.n_docs = len(off) - 1
+        b.doc_offsets = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        b.id_key, b.cause_key, b.kind = id_ptr, cause_ptr, kind_ptr
+        b.key_bits = layout.key_bits if key_bits is None else key_bits
+        b.ts_shift = layout.ts_shift
+        b.site_shift = layout.site_shift
+        b.site_bits = layout.site_bits
+        return b, off
+
+    def weave_lists(self, offsets, id_key, cause_key, kind, layout, yarns=True,
+                    key_bits=None) -> ListResult:
+        """Host-memory call: numpy in, numpy out."""
+        i = np.ascontiguousarray(id_key, np.uint64)
+        c = np.ascontiguousarray(cause_key, np.uint64)
+        k = np.ascontiguousarray(kind, np.uint8)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        D, N = len(off) - 1, len(i)
+        if int(off[-1]) != N:
+            raise ValueError("offsets[-1] != number of nodes")
+        b, off = self._batch(off, _ptr(i), _ptr(c), _ptr(k), layout, key_bits)
+        out = ListResult(np.zeros(N, np.uint32), np.zeros((N + 31) // 32, np.uint32),
+                         np.zeros(D, np.uint32), np.zeros(D, np.uint64), np.zeros(D, np.uint32),
+                         np.zeros(N, np.uint32) if (yarns and layout.site_bits) else None)
+        r = CwListResult(_ptr(out.weave_perm), _ptr(out.visible_bits), _ptr(out.visible_count),
+                         _ptr(out.max_ts), _ptr(out.status), _ptr(out.yarn_perm))
+        self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_HOST),
+                    "cw_weave_lists")
+        return out
+
+    def weave_lists_device(self, offsets, id_ptr, cause_ptr, kind_ptr, layout, out_ptrs,
+                           key_bits=None):
+        """Device-memory call: raw device pointers (e.g. torch tensor data_ptr()).
+        out_ptrs: dict with weave_perm, visible_bits, visible_count, max_ts,
+        status, yarn_perm (None allowed where the header allows NULL)."""
+        b, off = self._batch(offsets, C.c_void_p(id_ptr), C.c_void_p(cause_ptr),
+                             C.c_void_p(kind_ptr), layout, key_bits)
+        g = lambda n: C.c_void_p(out_ptrs[n]) if out_ptrs.get(n) else None
+        r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), g("max_ts"),
+                         g("status"), g("yarn_perm"))
+        self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
+                    "cw_weave_lists")

@@ -1,0 +1,1089 @@
+// causeweave.hip -- MI355X (gfx950) weave for Cause: kernels + the C ABI of
+// include/causeweave.h.
+//
+// Pipeline for a batch of independent CausalLists (DESIGN.md has the byte
+// accounting and the reference lines each stage replaces):
+//
+//   1. id sort      segmented LSD radix sort of (id_key, input index) per doc
+//                   -- (sort (::s/nodes ct)), list.cljc:28
+//   2. join         cause -> parent rank by binary search in the sorted ids,
+//                   domain checks (root, dup, orphan, lamport) -- shared.cljc:163-178
+//   3. eff parent   non-specials climb through special causes
+//   4. child sort   segmented radix sort by (eff parent, class): siblings
+//                   specials-first, then by id -- weave-later?, shared.cljc:202-223
+//   5. links        first child / next sibling / parent per node, visibility
+//                   (hide?, list.cljc:48-55 via SURVEY F6), splitter flags
+//   6. Euler walk   each splitter arc walks its sublist of the Euler tour
+//   7. rank         per-document list ranking of the sublists in LDS
+//   8. emit         weave position -> weave_perm, visibility, counts
+//   9. pack         visibility bytes -> bitmap
+//  (10. yarns       stable radix partition of the id order by site, spin 1-arity)
+//
+// Everything is integer work bounded by HBM/L2 traffic; MFMA is not used.
+// Launch grids map documents contiguously so the blocks that touch one
+// document run close together in time and share its lines in L2.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "causeweave.h"
+#include "cw_internal.h"
+
+using namespace cw;
+
+// ============================================================================
+// Device kernels
+// ============================================================================
+
+// Block-wide exclusive scan of one value per thread (blockDim.x = 64*W).
+template <int NT>
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wtot[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    uint32_t t = wtot[i];
+    before += (i < (int)w) ? t : 0u;
+    all += t;
+  }
+  if (total) *total = all;
+  __syncthreads();
+  return before + x - v;
+}
+
+// --- segmented LSD radix sort ------------------------------------------------
+template <typename K>
+__global__ __launch_bounds__(256) void k_radix_hist(const K *__restrict__ keys,
+                                                    const uint32_t *__restrict__ tile_start,
+                                                    uint32_t shift, uint32_t dmask,
+                                                    uint32_t *__restrict__ hist) {
+  __shared__ uint32_t h[4][RADIX];
+  const uint32_t t = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  for (uint32_t i = tid; i < 4 * RADIX; i += 256) (&h[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  for (uint32_t i = s + tid; i < e; i += 256)
+    atomicAdd(&h[w][(uint32_t)(keys[i] >> shift) & dmask], 1u);
+  __syncthreads();
+  hist[(size_t)t * RADIX + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+// Per document: turn the (tile, digit) counts into global output offsets,
+// digit-major then tile order (stable).
+__global__ __launch_bounds__(256) void k_radix_scan(uint32_t *__restrict__ hist,
+                                                    const uint32_t *__restrict__ tile_first,
+                                                    const uint32_t *__restrict__ doc_off) {
+  __shared__ uint32_t wtot[4];
+  const uint32_t d = blockIdx.x, b = threadIdx.x;
+  const uint32_t t0 = tile_first[d], t1 = tile_first[d + 1];
+  if (t0 == t1) return;  // empty document (uniform per block)
+  uint32_t tot = 0;
+  for (uint32_t t = t0; t < t1; t++) tot += hist[(size_t)t * RADIX + b];
+  uint32_t run = doc_off[d] + block_exscan<256>(tot, wtot, nullptr);
+  for (uint32_t t = t0; t < t1; t++) {
+    uint32_t c = hist[(size_t)t * RADIX + b];
+    hist[(size_t)t * RADIX + b] = run;
+    run += c;
+  }
+}
+
+// Stable scatter of one tile.  vals_in == nullptr means "value = doc-local
+// index of the element" (first pass).  Ranks inside the tile come from
+// wave-level digit matching (8 ballots) and per-wave digit counters in LDS;
+// the tile is reordered in LDS so the global writes are digit runs.
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ offs, uint32_t shift, uint32_t dmask) {
+  __shared__ K skey[TILE];
+  __shared__ uint32_t sval[TILE];
+  __shared__ uint32_t wcnt[2][SORT_WAVES][RADIX];
+  __shared__ uint32_t run[RADIX], bstart[RADIX], soff[RADIX];
+  __shared__ uint32_t wtot[SORT_WAVES];
+
+  const uint32_t t = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  const uint32_t len = e - s;
+  const uint32_t lbase = s - doc_off[tile_doc[t]];
+
+  if (tid < RADIX) {
+    run[tid] = 0;
+    soff[tid] = offs[(size_t)t * RADIX + tid];
+  }
+  for (uint32_t i = tid; i < SORT_WAVES * RADIX; i += SORT_THREADS) (&wcnt[0][0][0])[i] = 0;
+  __syncthreads();
+
+  K key[SORT_ITEMS];
+  uint32_t val[SORT_ITEMS], rk[SORT_ITEMS];
+#pragma unroll
+  for (uint32_t k = 0; k < SORT_ITEMS; k++) {
+    const uint32_t j = k * SORT_THREADS + tid;
+    const bool valid = j < len;
+    key[k] = valid ? keys_in[s + j] : (K)0;
+    val[k] = valid ? (vals_in ? vals_in[s + j] : lbase + j) : 0u;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (uint32_t bit = 0; bit < RADIX_BITS; bit++) {
+      const bool on = (d >> bit) & 1u;
+      const uint64_t b = __ballot(on);
+      m &= on ? b : ~b;
+    }
+    const uint32_t lr = lanes_below(m);
+    const uint32_t buf = k & 1;
+    if (valid && lr == 0) wcnt[buf][w][d] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (tid < RADIX) {
+      uint32_t r = run[tid];
+#pragma unroll
+      for (uint32_t ww = 0; ww < SORT_WAVES; ww++) {
+        const uint32_t c = wcnt[buf][ww][tid];
+        wcnt[buf][ww][tid] = r;
+        r += c;
+        wcnt[buf ^ 1][ww][tid] = 0;
+      }
+      run[tid] = r;
+    }
+    __syncthreads();
+    rk[k] = valid ? wcnt[buf][w][d] + lr : 0u;
+  }
+  uint32_t cnt = tid < RADIX ? run[tid] : 0u;
+  uint32_t ex = block_exscan<SORT_THREADS>(cnt, wtot, nullptr);
+  if (tid < RADIX) bstart[tid] = ex;
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < SORT_ITEMS; k++) {
+    const uint32_t j = k * SORT_THREADS + tid;
+    if (j < len) {
+      const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
+      const uint32_t p = bstart[d] + rk[k];
+      skey[p] = key[k];
+      sval[p] = val[k];
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < len; j += SORT_THREADS) {
+    const K kk = skey[j];
+    const uint32_t d = (uint32_t)(kk >> shift) & dmask;
+    const uint32_t dst = soff[d] + j - bstart[d];
+    keys_out[dst] = kk;
+    vals_out[dst] = sval[j];
+  }
+}
+
+// --- join: cause -> parent rank ---------------------------------------------
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__ a, uint32_t n,
+                                                    uint64_t x) {
+  uint32_t lo = 0, len = n;
+  while (len > 0) {
+    const uint32_t half = len >> 1;
+    if (a[lo + half] < x) {
+      lo += half + 1;
+      len -= half + 1;
+    } else {
+      len = half;
+    }
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_join(
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, uint32_t *__restrict__ par,
+    uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
+  __shared__ uint32_t bst;
+  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  if (threadIdx.x == 0) bst = 0;
+  __syncthreads();
+  uint32_t st = 0;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base;
+    const uint32_t gi = base + sval[i];
+    const uint8_t kd = kind[gi];
+    uint32_t p = 0;
+    if (r == 0) {
+      if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
+    } else {
+      if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
+      const uint64_t my = skey[i];
+      if (my == skey[i - 1]) st |= CW_STATUS_DUP;
+      const uint64_t ck = cause_key[gi];
+      const uint32_t c = lower_bound_u64(skey + base, n, ck);
+      if (c == n || skey[base + c] != ck) st |= CW_STATUS_ORPHAN;
+      else if (c >= r) st |= CW_STATUS_NON_LAMPORT;
+      else p = c;
+    }
+    par[i] = p;
+    skind[i] = kd;
+  }
+  if (st) atomicOr(&bst, st);
+  __syncthreads();
+  if (threadIdx.x == 0 && bst) atomicOr(&status[d], bst);
+}
+
+// --- effective parent + child-sort key ---------------------------------------
+// child key = ((eff+1) << 1) | (special ? 0 : 1); the root gets 0 (sorts first).
+__global__ __launch_bounds__(256) void k_eff(const uint32_t *__restrict__ par,
+                                             const uint8_t *__restrict__ skind,
+                                             const uint32_t *__restrict__ tile_start,
+                                             const uint32_t *__restrict__ tile_doc,
+                                             const uint32_t *__restrict__ doc_off,
+                                             uint32_t *__restrict__ epar,
+                                             uint32_t *__restrict__ ckey) {
+  const uint32_t t = blockIdx.x, base = doc_off[tile_doc[t]];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base;
+    if (r == 0) {
+      epar[i] = 0;
+      ckey[i] = 0;
+      continue;
+    }
+    const uint8_t k = skind[i];
+    uint32_t c = par[i];
+    const bool sp = is_special(k);
+    if (!sp)
+      while (c != 0 && is_special(skind[base + c])) c = par[base + c];
+    epar[i] = c;
+    ckey[i] = ((c + 1) << 1) | (sp ? 0u : 1u);
+  }
+}
+
+// --- links --------------------------------------------------------------------
+// Over the child-sorted array: groups (eff parent, class) in ascending rank.
+// Sibling order is specials by descending id, then non-specials by descending
+// id, so the next sibling inside a class is the previous group element and the
+// first child of a class is the group's last element.
+__global__ __launch_bounds__(256) void k_links(const uint32_t *__restrict__ ckey_s,
+                                               const uint32_t *__restrict__ cval_s,
+                                               const uint32_t *__restrict__ tile_start,
+                                               const uint32_t *__restrict__ tile_doc,
+                                               const uint32_t *__restrict__ doc_off,
+                                               uint32_t *__restrict__ nsc,
+                                               uint32_t *__restrict__ fcS,
+                                               uint32_t *__restrict__ fcN) {
+  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t key = ckey_s[i];
+    if (key == 0) continue;  // the root
+    const uint32_t j = i - base, r = cval_s[i];
+    const uint32_t e = (key >> 1) - 1;
+    const bool prev_same = j > 0 && ckey_s[i - 1] == key;
+    const bool next_same = j + 1 < n && ckey_s[i + 1] == key;
+    nsc[base + r] = prev_same ? cval_s[i - 1] : 0u;
+    if (!next_same) ((key & 1) ? fcN : fcS)[base + e] = r;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_link_final(
+    const uint32_t *__restrict__ nsc, const uint32_t *__restrict__ fcS,
+    const uint32_t *__restrict__ fcN, const uint32_t *__restrict__ epar,
+    const uint8_t *__restrict__ skind, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ doc_log2k, uint64_t *__restrict__ link) {
+  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base;
+    const uint8_t k = skind[i];
+    const bool sp = is_special(k);
+    const uint32_t fs = fcS[i], fn = fcN[i];
+    const uint32_t fc = fs ? fs : fn;
+    uint32_t nx;
+    if (r == 0) {
+      nx = NX_END;
+    } else {
+      uint32_t ns = nsc[i];
+      if (!ns && sp) ns = fcN[base + epar[i]];  // last special -> newest non-special
+      nx = ns ? ns : (NX_UP | epar[i]);
+    }
+    // the next weave node after a non-special is its first child,
+    // which is its newest special child when it has one.
+    const bool vis = !sp && r != 0 && !(fs && is_hide(skind[base + fs]));
+    const bool split = r == split_node(d, r >> log2k, log2k, n);
+    const uint32_t lo = fc | (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
+    link[i] = (uint64_t)lo | ((uint64_t)nx << 32);
+  }
+}
+
+// --- Euler walk ----------------------------------------------------------------
+// Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
+// splitter block lw/2's splitter node and follows the tour until the next
+// splitter arc.  Every down arc it crosses gets (walker, local count).
+__global__ __launch_bounds__(WALK_THREADS) void k_walk(
+    const uint64_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
+    const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_W,
+    const uint32_t *__restrict__ walk_first, uint64_t *__restrict__ loc,
+    uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext, uint32_t *__restrict__ status) {
+  const uint32_t b = blockIdx.x, d = wblk_doc[b];
+  const uint32_t lw = wblk_w0[b] + threadIdx.x;
+  if (lw >= doc_W[d]) return;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  uint32_t v = split_node(d, lw >> 1, log2k, n);
+  uint32_t dir = lw & 1;  // 0 = down, 1 = up
+  uint32_t cnt = 0, nextsub = NX_END;
+  if (dir == 0) {
+    loc[base + v] = (uint64_t)lw << 32;
+    cnt = 1;
+  }
+  uint64_t L = link[base + v];
+  const uint32_t max_steps = 2 * n + 2;
+  for (uint32_t steps = 0;; steps++) {
+    uint32_t u, ndir;
+    if (dir == 0) {
+      const uint32_t fc = (uint32_t)L & LINK_IDX;
+      if (fc) { u = fc; ndir = 0; }
+      else { u = v; ndir = 1; }
+    } else {
+      const uint32_t nx = (uint32_t)(L >> 32);
+      if (nx == NX_END) break;
+      if (nx & NX_UP) { u = nx & ~NX_UP; ndir = 1; }
+      else { u = nx; ndir = 0; }
+    }
+    const uint64_t Lu = (u == v) ? L : link[base + u];
+    if ((uint32_t)Lu & LINK_SPLIT) {
+      nextsub = ((u >> log2k) << 1) | ndir;
+      break;
+    }
+    if (ndir == 0) {
+      loc[base + u] = ((uint64_t)lw << 32) | cnt;
+      cnt++;
+    }
+    v = u;
+    dir = ndir;
+    L = Lu;
+    if (steps > max_steps) {
+      atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+      break;
+    }
+  }
+  wcnt[walk_first[d] + lw] = cnt;
+  wnext[walk_first[d] + lw] = nextsub;
+}
+
+// --- sublist ranking (one workgroup per document, Wyllie pointer jumping in LDS)
+__global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
+                                              const uint32_t *__restrict__ wnext,
+                                              const uint32_t *__restrict__ walk_first,
+                                              const uint32_t *__restrict__ doc_W,
+                                              const uint32_t *__restrict__ doc_off,
+                                              const uint64_t *__restrict__ skey, uint32_t ts_shift,
+                                              uint32_t *__restrict__ sbase,
+                                              uint64_t *__restrict__ max_ts,
+                                              uint32_t *__restrict__ status) {
+  __shared__ uint32_t val[2][MAX_SUBLISTS];
+  __shared__ uint32_t nx[2][MAX_SUBLISTS];
+  const uint32_t d = blockIdx.x, W = doc_W[d], f = walk_first[d];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  if (threadIdx.x == 0 && max_ts) max_ts[d] = n ? (skey[base + n - 1] >> ts_shift) : 0ull;
+  if (W == 0) return;
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
+    val[0][i] = wcnt[f + i];
+    nx[0][i] = wnext[f + i];
+  }
+  __syncthreads();
+  uint32_t cur = 0;
+  for (uint32_t span = 1; span < W; span <<= 1) {
+    for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
+      const uint32_t x = nx[cur][i];
+      if (x != NX_END) {
+        val[cur ^ 1][i] = val[cur][i] + val[cur][x];
+        nx[cur ^ 1][i] = nx[cur][x];
+      } else {
+        val[cur ^ 1][i] = val[cur][i];
+        nx[cur ^ 1][i] = NX_END;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  const uint32_t total = val[cur][0];  // sublist 0 = down(root) heads the tour
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) sbase[f + i] = total - val[cur][i];
+  if (threadIdx.x == 0 && total != n) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+}
+
+// --- emit: rank order -> weave order -------------------------------------------
+__global__ __launch_bounds__(256) void k_emit(
+    const uint64_t *__restrict__ loc, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ link, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ walk_first, const uint32_t *__restrict__ doc_W,
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, uint32_t *__restrict__ perm,
+    uint8_t *__restrict__ vis8, uint32_t *__restrict__ vcount, uint32_t *__restrict__ status) {
+  __shared__ uint32_t wtot[4];
+  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d], W = doc_W[d];
+  uint32_t nvis = 0;
+  bool bad = false;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint64_t L = loc[i];
+    const uint32_t lw = (uint32_t)(L >> 32);
+    if (lw >= W) { bad = true; continue; }
+    const uint32_t pos = sbase[f + lw] + (uint32_t)L;
+    if (pos >= n) { bad = true; continue; }
+    const uint32_t v = ((uint32_t)link[i] & LINK_VIS) ? 1u : 0u;
+    perm[base + pos] = sval[i];
+    vis8[base + pos] = (uint8_t)v;
+    nvis += v;
+  }
+  if (bad) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+  uint32_t total;
+  block_exscan<256>(nvis, wtot, &total);
+  if (threadIdx.x == 0 && total) atomicAdd(&vcount[d], total);
+}
+
+__global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
+                                                   uint32_t *__restrict__ bits) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g0 = w * 32;
+  if (g0 >= N) return;
+  uint32_t m = 0;
+  if (g0 + 32 <= N) {
+    const uint4 a = *reinterpret_cast<const uint4 *>(vis8 + g0);
+    const uint4 b = *reinterpret_cast<const uint4 *>(vis8 + g0 + 16);
+    const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int q = 0; q < 8; q++)
+#pragma unroll
+      for (int y = 0; y < 4; y++) m |= ((x[q] >> (8 * y)) & 1u) << (4 * q + y);
+  } else {
+    for (uint32_t g = g0; g < N; g++) m |= (uint32_t)(vis8[g] & 1u) << (g - g0);
+  }
+  bits[w] = m;
+}
+
+__global__ void k_or_reduce(const uint64_t *__restrict__ keys, uint32_t N,
+                            unsigned long long *__restrict__ out) {
+  uint64_t acc = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    acc |= keys[i];
+  for (int o = 32; o > 0; o >>= 1) acc |= __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, (unsigned long long)acc);
+}
+
+// ============================================================================
+// Host side
+// ============================================================================
+
+namespace {
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+};
+
+struct KStat {
+  uint64_t launches = 0;
+  double ms = 0, bytes = 0;
+};
+
+struct PendingEvt {
+  std::string name;
+  hipEvent_t a, b;
+  double bytes;
+};
+
+}  // namespace
+
+struct cw_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  bool async = false;
+  bool prof = false;
+  std::string err;
+  std::map<std::string, DevBuf> bufs;
+  void *pinned = nullptr;
+  size_t pinned_bytes = 0;
+  std::map<std::string, KStat> stats;
+  std::vector<PendingEvt> pending;
+  std::vector<hipEvent_t> evt_pool;
+  // cached host tables (reused when the document layout repeats)
+  std::vector<uint64_t> last_off;
+  struct Tables {
+    std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
+        wblk_doc, wblk_w0;
+    uint32_t T = 0, Wtot = 0, Bw = 0, nmax = 0;
+  } tab;
+  bool tab_on_device = false;
+};
+
+namespace {
+
+int fail(cw_ctx *c, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return -1;
+}
+
+#define HIPCHK(c, x)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) return fail((c), "%s: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                                      __FILE__, __LINE__);                                \
+  } while (0)
+
+void *scratch(cw_ctx *c, const char *name, size_t bytes) {
+  DevBuf &b = c->bufs[name];
+  if (bytes == 0) bytes = 16;
+  if (b.bytes < bytes) {
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = bytes + bytes / 8;  // headroom for slightly larger batches
+    if (hipMalloc(&b.p, want) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    b.bytes = want;
+  }
+  return b.p;
+}
+
+template <typename T>
+T *scratch_t(cw_ctx *c, const char *name, size_t count) {
+  return reinterpret_cast<T *>(scratch(c, name, count * sizeof(T)));
+}
+
+hipEvent_t get_event(cw_ctx *c) {
+  if (!c->evt_pool.empty()) {
+    hipEvent_t e = c->evt_pool.back();
+    c->evt_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Launch helper: optional per-kernel event timing on the launch stream.
+struct Launch {
+  cw_ctx *c;
+  const char *name;
+  double bytes;
+  hipEvent_t a = nullptr;
+  Launch(cw_ctx *c_, const char *n, double by) : c(c_), name(n), bytes(by) {
+    if (c->prof) {
+      a = get_event(c);
+      (void)hipEventRecord(a, c->stream);
+    }
+  }
+  ~Launch() {
+    if (c->prof && a) {
+      hipEvent_t b = get_event(c);
+      (void)hipEventRecord(b, c->stream);
+      c->pending.push_back({name, a, b, bytes});
+    }
+  }
+};
+
+int check_launch(cw_ctx *c, const char *what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
+  return 0;
+}
+
+int collect_prof(cw_ctx *c) {
+  if (c->pending.empty()) return 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (auto &p : c->pending) {
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, p.a, p.b);
+    KStat &s = c->stats[p.name];
+    s.launches++;
+    s.ms += ms;
+    s.bytes += p.bytes;
+    c->evt_pool.push_back(p.a);
+    c->evt_pool.push_back(p.b);
+  }
+  c->pending.clear();
+  return 0;
+}
+
+uint32_t ceil_log2(uint64_t x) {
+  uint32_t r = 0;
+  while ((1ull << r) < x) r++;
+  return r;
+}
+
+// Host tables: tiles (sort/pass grids), splitter blocks and walker blocks.
+void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
+  auto &t = c->tab;
+  t.doc_off.resize(D + 1);
+  t.tile_start.clear();
+  t.tile_doc.clear();
+  t.tile_first.resize(D + 1);
+  t.doc_log2k.resize(D);
+  t.doc_W.resize(D);
+  t.walk_first.resize(D + 1);
+  t.wblk_doc.clear();
+  t.wblk_w0.clear();
+  uint32_t wtot = 0;
+  t.nmax = 0;
+  for (uint64_t d = 0; d < D; d++) {
+    const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
+    t.doc_off[d] = b;
+    t.nmax = std::max(t.nmax, n);
+    t.tile_first[d] = (uint32_t)t.tile_start.size();
+    for (uint32_t s = 0; s < n; s += TILE) {
+      t.tile_start.push_back(b + s);
+      t.tile_doc.push_back((uint32_t)d);
+    }
+    // splitter block size K = 2^log2k, at most MAX_SUBLISTS/2 blocks per doc
+    uint32_t log2k = std::max(MIN_LOG2K, ceil_log2((n + MAX_SUBLISTS / 2 - 1) / (MAX_SUBLISTS / 2)));
+    const uint32_t S = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;
+    const uint32_t W = 2 * S;
+    t.doc_log2k[d] = log2k;
+    t.doc_W[d] = W;
+    t.walk_first[d] = wtot;
+    for (uint32_t w0 = 0; w0 < W; w0 += WALK_THREADS) {
+      t.wblk_doc.push_back((uint32_t)d);
+      t.wblk_w0.push_back(w0);
+    }
+    wtot += W;
+  }
+  t.doc_off[D] = (uint32_t)off[D];
+  t.tile_first[D] = (uint32_t)t.tile_start.size();
+  t.walk_first[D] = wtot;
+  t.T = (uint32_t)t.tile_doc.size();
+  t.tile_start.push_back((uint32_t)off[D]);
+  t.Wtot = wtot;
+  t.Bw = (uint32_t)t.wblk_doc.size();
+}
+
+int upload_tables(cw_ctx *c) {
+  auto &t = c->tab;
+  std::vector<std::pair<const char *, const std::vector<uint32_t> *>> items = {
+      {"t_doc_off", &t.doc_off},   {"t_tile_start", &t.tile_start}, {"t_tile_doc", &t.tile_doc},
+      {"t_tile_first", &t.tile_first}, {"t_doc_log2k", &t.doc_log2k}, {"t_doc_W", &t.doc_W},
+      {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0}};
+  size_t total = 0;
+  for (auto &it : items) total += (it.second->size() + 64) * 4;
+  if (c->pinned_bytes < total) {
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    c->pinned = nullptr;
+    HIPCHK(c, hipHostMalloc(&c->pinned, total, hipHostMallocDefault));
+    c->pinned_bytes = total;
+  }
+  char *p = (char *)c->pinned;
+  for (auto &it : items) {
+    size_t bytes = it.second->size() * 4;
+    void *dst = scratch(c, it.first, bytes);
+    if (!dst) return fail(c, "out of device memory (%s)", it.first);
+    if (bytes) {
+      memcpy(p, it.second->data(), bytes);
+      HIPCHK(c, hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->stream));
+    }
+    p += (it.second->size() + 64) * 4;
+  }
+  return 0;
+}
+
+uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name].p; }
+
+// One segmented radix sort over key bits [shift0, shift0+bits) (LSD, RADIX_BITS
+// per pass, at least one pass).  Pass 0 reads (kin, vin) -- vin == nullptr means
+// identity values -- and the passes ping-pong between (kA,vA) and (kB,vB).
+template <typename K>
+int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
+               uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
+               K **kout, uint32_t **vout) {
+  auto &t = c->tab;
+  uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * RADIX);
+  if (!hist) return fail(c, "out of device memory (hist)");
+  const int passes = std::max(1, (int)((bits + RADIX_BITS - 1) / RADIX_BITS));
+  const K *ki = kin;
+  const uint32_t *vi = vin;
+  K *ko = kA;
+  uint32_t *vo = vA;
+  char nm[48];
+  const uint32_t D = (uint32_t)(t.doc_off.size() - 1);
+  for (int p = 0; p < passes; p++) {
+    const uint32_t shift = shift0 + p * RADIX_BITS;
+    const uint32_t left = bits > p * RADIX_BITS ? bits - p * RADIX_BITS : 1;
+    const uint32_t dmask = left >= RADIX_BITS ? RADIX - 1 : (1u << left) - 1;
+    snprintf(nm, sizeof nm, "%s_hist", tag);
+    {
+      Launch L(c, nm, (double)N * sizeof(K) + (double)t.T * RADIX * 4);
+      hipLaunchKernelGGL(k_radix_hist<K>, dim3(t.T), dim3(256), 0, c->stream, ki,
+                         dev_tab(c, "t_tile_start"), shift, dmask, hist);
+    }
+    if (check_launch(c, nm)) return -1;
+    snprintf(nm, sizeof nm, "%s_scan", tag);
+    {
+      Launch L(c, nm, (double)t.T * RADIX * 8);
+      hipLaunchKernelGGL(k_radix_scan, dim3(D), dim3(256), 0, c->stream, hist,
+                         dev_tab(c, "t_tile_first"), dev_tab(c, "t_doc_off"));
+    }
+    if (check_launch(c, nm)) return -1;
+    snprintf(nm, sizeof nm, "%s_scatter", tag);
+    {
+      Launch L(c, nm, (double)N * (2 * sizeof(K) + (vi ? 8 : 4)) + (double)t.T * RADIX * 4);
+      hipLaunchKernelGGL(k_radix_scatter<K>, dim3(t.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
+                         ko, vo, dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
+                         dev_tab(c, "t_doc_off"), hist, shift, dmask);
+    }
+    if (check_launch(c, nm)) return -1;
+    ki = ko;
+    vi = vo;
+    ko = (ko == kA) ? kB : kA;
+    vo = (vo == vA) ? vB : vA;
+  }
+  *kout = const_cast<K *>(ki);
+  *vout = const_cast<uint32_t *>(vi);
+  return 0;
+}
+
+int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_key,
+                       const uint64_t *cause_key, const uint8_t *kind, cw_list_result *out) {
+  const uint64_t D = bt->n_docs;
+  const uint32_t N = (uint32_t)bt->doc_offsets[D];
+  auto &t = c->tab;
+  const dim3 B256(256);
+
+  HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
+  if (out->visible_bits && N)
+    HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
+
+  uint32_t key_bits = bt->key_bits;
+  if (key_bits == 0 && N) {
+    unsigned long long *red = scratch_t<unsigned long long>(c, "red", 1);
+    if (!red) return fail(c, "out of device memory (red)");
+    HIPCHK(c, hipMemsetAsync(red, 0, 8, c->stream));
+    hipLaunchKernelGGL(k_or_reduce, dim3(1024), B256, 0, c->stream, id_key, N, red);
+    if (check_launch(c, "or_reduce")) return -1;
+    unsigned long long v = 0;
+    HIPCHK(c, hipMemcpyAsync(&v, red, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    key_bits = v ? 64 - __builtin_clzll(v) : 1;
+  }
+  if (key_bits > 64) key_bits = 64;
+
+  uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
+  uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
+  uint32_t *par = scratch_t<uint32_t>(c, "par", N), *epar = scratch_t<uint32_t>(c, "epar", N);
+  uint8_t *skind = scratch_t<uint8_t>(c, "skind", N);
+  uint32_t *ckA = scratch_t<uint32_t>(c, "ckA", N), *ckB = scratch_t<uint32_t>(c, "ckB", N);
+  uint32_t *cvA = scratch_t<uint32_t>(c, "cvA", N), *cvB = scratch_t<uint32_t>(c, "cvB", N);
+  uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
+  uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
+  uint64_t *link = scratch_t<uint64_t>(c, "link", N), *loc = scratch_t<uint64_t>(c, "loc", N);
+  uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
+  uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
+  uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
+  uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
+  if (!skA || !skB || !svA || !svB || !par || !epar || !skind || !ckA || !ckB || !cvA || !cvB ||
+      !nsc || !fcS || !fcN || !link || !loc || !vis8 || !wcnt || !wnext || !sbase)
+    return fail(c, "out of device memory (N=%u)", N);
+
+  uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc");
+  uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
+  uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
+  const dim3 GT(t.T);
+
+  if (N) {
+    // 1. id sort
+    uint64_t *skey;
+    uint32_t *sval;
+    if (radix_sort<uint64_t>(c, "idsort", id_key, nullptr, skA, svA, skB, svB, key_bits, 0, N,
+                             &skey, &sval))
+      return -1;
+
+    // 2. join
+    {
+      Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1));
+      hipLaunchKernelGGL(k_join, GT, B256, 0, c->stream, skey, sval, cause_key, kind, tile_start,
+                         tile_doc, doc_off, par, skind, out->status);
+    }
+    if (check_launch(c, "join")) return -1;
+
+    // 3. effective parent
+    {
+      Launch L(c, "effparent", (double)N * (4 + 1 + 4 + 4));
+      hipLaunchKernelGGL(k_eff, GT, B256, 0, c->stream, par, skind, tile_start, tile_doc, doc_off,
+                         epar, ckA);
+    }
+    if (check_launch(c, "effparent")) return -1;
+
+    // 4. child sort by (eff parent, class), values = rank (identity)
+    uint32_t *cks, *cvs;
+    const uint32_t cbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
+    if (radix_sort<uint32_t>(c, "childsort", ckA, nullptr, ckB, cvA, ckA, cvB, cbits, 0, N, &cks,
+                             &cvs))
+      return -1;
+
+    // 5. links
+    HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
+    {
+      Launch L(c, "links", (double)N * (4 + 4 + 4 + 4));
+      hipLaunchKernelGGL(k_links, GT, B256, 0, c->stream, cks, cvs, tile_start, tile_doc, doc_off,
+                         nsc, fcS, fcN);
+    }
+    if (check_launch(c, "links")) return -1;
+    {
+      Launch L(c, "linkfinal", (double)N * (4 + 4 + 4 + 4 + 1 + 8));
+      hipLaunchKernelGGL(k_link_final, GT, B256, 0, c->stream, nsc, fcS, fcN, epar, skind,
+                         tile_start, tile_doc, doc_off, doc_log2k, link);
+    }
+    if (check_launch(c, "linkfinal")) return -1;
+
+    // 6. Euler walk
+    {
+      Launch L(c, "walk", (double)N * (2 * 8 + 8));
+      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(WALK_THREADS), 0, c->stream, link,
+                         dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
+                         doc_W, walk_first, loc, wcnt, wnext, out->status);
+    }
+    if (check_launch(c, "walk")) return -1;
+
+    // 7. rank sublists (+ max lamport-ts per document)
+    {
+      Launch L(c, "rank", (double)t.Wtot * 12);
+      hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, 0, c->stream, wcnt, wnext, walk_first,
+                         doc_W, doc_off, skey, bt->ts_shift, sbase, out->max_ts, out->status);
+    }
+    if (check_launch(c, "rank")) return -1;
+
+    // 8. emit
+    {
+      Launch L(c, "emit", (double)N * (8 + 4 + 8 + 4 + 4 + 1));
+      hipLaunchKernelGGL(k_emit, GT, B256, 0, c->stream, loc, sval, link, sbase, walk_first, doc_W,
+                         tile_start, tile_doc, doc_off, out->weave_perm, vis8, out->visible_count,
+                         out->status);
+    }
+    if (check_launch(c, "emit")) return -1;
+
+    // 9. visibility bitmap
+    if (out->visible_bits) {
+      const uint32_t words = (N + 31) / 32;
+      Launch L(c, "packbits", (double)N + (double)words * 4);
+      hipLaunchKernelGGL(k_pack_bits, dim3((words + 255) / 256), B256, 0, c->stream, vis8, N,
+                         out->visible_bits);
+    }
+    if (check_launch(c, "packbits")) return -1;
+
+    // 10. yarns: stable partition of the id order by site rank
+    if (out->yarn_perm && bt->site_bits) {
+      uint64_t *yk;
+      uint32_t *yv;
+      uint64_t *ykA = skey == skA ? skB : skA;
+      uint32_t *yvA = sval == svA ? svB : svA;
+      // (skey, sval) stay intact: ping-pong through the free id buffers + link/loc
+      if (radix_sort<uint64_t>(c, "yarns", skey, sval, ykA, yvA, loc, nsc, bt->site_bits,
+                               bt->site_shift, N, &yk, &yv))
+        return -1;
+      HIPCHK(c, hipMemcpyAsync(out->yarn_perm, yv, (size_t)N * 4, hipMemcpyDeviceToDevice,
+                               c->stream));
+    }
+  }
+  // empty documents (no root) are flagged by the host wrapper
+  return 0;
+}
+
+int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace) {
+  if (!bt || !res) return fail(c, "null batch/result");
+  const uint64_t D = bt->n_docs;
+  if (!bt->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
+  const uint64_t N64 = bt->doc_offsets[D];
+  if (bt->doc_offsets[0] != 0) return fail(c, "doc_offsets[0] must be 0");
+  if (N64 >= 0xFFFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^32-1)",
+                                        (unsigned long long)N64);
+  for (uint64_t d = 0; d < D; d++) {
+    if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
+    if (bt->doc_offsets[d + 1] - bt->doc_offsets[d] > LINK_IDX)
+      return fail(c, "document %llu too large (limit 2^30-1 nodes)", (unsigned long long)d);
+  }
+  if (!res->weave_perm || !res->visible_count || !res->status)
+    return fail(c, "weave_perm, visible_count and status are required");
+  const uint32_t N = (uint32_t)N64;
+  HIPCHK(c, hipSetDevice(c->device));
+
+  // host tables (cached while the document layout repeats)
+  bool same = c->tab_on_device && c->last_off.size() == D + 1 &&
+              memcmp(c->last_off.data(), bt->doc_offsets, (D + 1) * 8) == 0;
+  if (!same) {
+    build_tables(c, D, bt->doc_offsets);
+    if (upload_tables(c)) return -1;
+    c->last_off.assign(bt->doc_offsets, bt->doc_offsets + D + 1);
+    c->tab_on_device = true;
+  }
+
+  const uint64_t *id = bt->id_key, *cause = bt->cause_key;
+  const uint8_t *kind = bt->kind;
+  cw_list_result dres = *res;
+  if (memspace == CW_MEM_HOST) {
+    if (N && (!id || !cause || !kind)) return fail(c, "null input arrays");
+    uint64_t *did = scratch_t<uint64_t>(c, "h_id", N), *dca = scratch_t<uint64_t>(c, "h_cause", N);
+    uint8_t *dk = scratch_t<uint8_t>(c, "h_kind", N);
+    dres.weave_perm = scratch_t<uint32_t>(c, "h_perm", N);
+    dres.visible_bits = res->visible_bits ? scratch_t<uint32_t>(c, "h_bits", ((size_t)N + 31) / 32) : nullptr;
+    dres.visible_count = scratch_t<uint32_t>(c, "h_vcount", D);
+    dres.max_ts = res->max_ts ? scratch_t<uint64_t>(c, "h_maxts", D) : nullptr;
+    dres.status = scratch_t<uint32_t>(c, "h_status", D);
+    dres.yarn_perm = res->yarn_perm ? scratch_t<uint32_t>(c, "h_yarn", N) : nullptr;
+    if (!did || !dca || !dk || !dres.weave_perm || !dres.visible_count || !dres.status ||
+        (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
+        (res->yarn_perm && !dres.yarn_perm))
+      return fail(c, "out of device memory (host-mode staging)");
+    if (N) {
+      HIPCHK(c, hipMemcpyAsync(did, id, (size_t)N * 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(dk, kind, N, hipMemcpyHostToDevice, c->stream));
+    }
+    id = did;
+    cause = dca;
+    kind = dk;
+  }
+  if (weave_lists_device(c, bt, id, cause, kind, &dres)) return -1;
+
+  if (memspace == CW_MEM_HOST) {
+    HIPCHK(c, hipMemcpyAsync(res->weave_perm, dres.weave_perm, (size_t)N * 4,
+                             hipMemcpyDeviceToHost, c->stream));
+    if (res->visible_bits)
+      HIPCHK(c, hipMemcpyAsync(res->visible_bits, dres.visible_bits, ((size_t)N + 31) / 32 * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(res->visible_count, dres.visible_count, D * 4, hipMemcpyDeviceToHost,
+                             c->stream));
+    if (res->max_ts)
+      HIPCHK(c, hipMemcpyAsync(res->max_ts, dres.max_ts, D * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(res->status, dres.status, D * 4, hipMemcpyDeviceToHost, c->stream));
+    if (res->yarn_perm)
+      HIPCHK(c, hipMemcpyAsync(res->yarn_perm, dres.yarn_perm, (size_t)N * 4,
+                               hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    // documents with no nodes have no root
+    for (uint64_t d = 0; d < D; d++)
+      if (bt->doc_offsets[d + 1] == bt->doc_offsets[d]) res->status[d] |= CW_STATUS_ROOT;
+  } else {
+    // empty documents: set the ROOT bit on the device
+    for (uint64_t d = 0; d < D; d++)
+      if (bt->doc_offsets[d + 1] == bt->doc_offsets[d]) {
+        static const uint32_t one = CW_STATUS_ROOT;
+        HIPCHK(c, hipMemcpyAsync(res->status + d, &one, 4, hipMemcpyHostToDevice, c->stream));
+      }
+    if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int cw_abi_version(void) { return CW_ABI_VERSION; }
+
+int cw_ctx_create(int device, cw_ctx **out) {
+  if (!out) return -1;
+  *out = nullptr;
+  cw_ctx *c = new cw_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess) {
+    delete c;
+    return -1;
+  }
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return -1;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return 0;
+}
+
+void cw_ctx_destroy(cw_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto &kv : c->bufs)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  for (auto &p : c->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : c->evt_pool) (void)hipEventDestroy(e);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char *cw_last_error(const cw_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int cw_ctx_set_stream(cw_ctx *c, void *s) {
+  if (!c) return -1;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return 0;
+}
+
+int cw_ctx_set_async(cw_ctx *c, int a) {
+  if (!c) return -1;
+  c->async = a != 0;
+  return 0;
+}
+
+int cw_ctx_set_profiling(cw_ctx *c, int on) {
+  if (!c) return -1;
+  c->prof = on != 0;
+  return 0;
+}
+
+int cw_get_kernel_stats(const cw_ctx *c, cw_kernel_stat *out, int cap) {
+  if (!c) return -1;
+  int i = 0;
+  for (auto &kv : c->stats) {
+    if (i < cap && out) {
+      memset(&out[i], 0, sizeof(cw_kernel_stat));
+      snprintf(out[i].name, sizeof out[i].name, "%s", kv.first.c_str());
+      out[i].launches = kv.second.launches;
+      out[i].total_ms = kv.second.ms;
+      out[i].bytes_alg = kv.second.bytes;
+    }
+    i++;
+  }
+  return i;
+}
+
+int cw_weave_lists(cw_ctx *c, const cw_list_batch *b, cw_list_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  if (memspace != CW_MEM_HOST && memspace != CW_MEM_DEVICE) return fail(c, "bad memspace");
+  return weave_lists_impl(c, b, r, memspace);
+}
+
+int cw_reset_kernel_stats(cw_ctx *c) {
+  if (!c) return -1;
+  c->stats.clear();
+  return 0;
+}
+
+}  // extern "C"

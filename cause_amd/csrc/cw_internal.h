@@ -1,0 +1,61 @@
+// cw_internal.h -- constants and small device helpers shared by the weave kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cw {
+
+// Sort tiles: a tile is a run of <= TILE consecutive nodes of ONE document.
+constexpr uint32_t TILE = 4096;
+constexpr uint32_t SORT_THREADS = 512;            // 8 waves
+constexpr uint32_t SORT_ITEMS = TILE / SORT_THREADS;
+constexpr uint32_t SORT_WAVES = SORT_THREADS / 64;
+constexpr uint32_t RADIX_BITS = 8;
+constexpr uint32_t RADIX = 1u << RADIX_BITS;
+
+// Euler walk: one walker per splitter arc; <= MAX_SUBLISTS sublists per document
+// so the sublist ranking of a document fits one workgroup's LDS.
+constexpr uint32_t WALK_THREADS = 256;
+constexpr uint32_t MAX_SUBLISTS = 4096;
+constexpr uint32_t MIN_LOG2K = 6;                 // >= 64 nodes per splitter block
+
+// link word: low 32 = first child (bit 31: node renders, bit 30: node is a
+// splitter), high 32 = next arc after the node's up arc.
+constexpr uint32_t LINK_VIS = 0x80000000u;
+constexpr uint32_t LINK_SPLIT = 0x40000000u;
+constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
+constexpr uint32_t NX_UP = 0x80000000u;           // next arc is up(parent)
+constexpr uint32_t NX_END = 0xFFFFFFFFu;          // root's up arc ends the tour
+
+constexpr uint8_t KIND_CLASS = 3, KIND_ROOT = 4, KIND_HIDE = 1, KIND_HHIDE = 2;
+
+__device__ __forceinline__ bool is_special(uint8_t k) { return (k & KIND_CLASS) != 0; }
+__device__ __forceinline__ bool is_hide(uint8_t k) {
+  return (k & KIND_CLASS) == KIND_HIDE || (k & KIND_CLASS) == KIND_HHIDE;
+}
+
+// Number of lanes below this one whose bit is set in m (wave64).
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t mix32(uint32_t a, uint32_t b) {
+  uint64_t x = (((uint64_t)a << 32) | b) * 0x9E3779B97F4A7C15ull;
+  x ^= x >> 29;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 32;
+  return (uint32_t)x;
+}
+
+// The splitter node of block j (nodes [j*K, (j+1)*K) of a document of n nodes):
+// the root for block 0, else a hashed position inside the block.  Hashing
+// avoids the periodicity of interleaved site chains.
+__device__ __forceinline__ uint32_t split_node(uint32_t doc, uint32_t j, uint32_t log2k, uint32_t n) {
+  if (j == 0) return 0;
+  uint32_t lo = j << log2k;
+  uint32_t k = 1u << log2k;
+  uint32_t h = mix32(doc, j);
+  return lo + ((n - lo >= k) ? (h & (k - 1)) : (h % (n - lo)));
+}
+
+}  // namespace cw

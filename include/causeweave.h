@@ -1,0 +1,134 @@
+/*
+ * causeweave.h -- C ABI of the MI355X-native weave for Cause (tetriscode/cause).
+ *
+ * One library, libcauseweave.so (gfx950 HIP kernels, cause_amd/csrc/), replaces
+ * the reference's `weave-fn` plug-in point for the reconstitute-from-nodes path:
+ *
+ *   c.list/weave 1-arity  (list.cljc:26-28)  -> cw_weave_lists  [weave order]
+ *   c.list/hide?           (list.cljc:48-55)  -> cw_weave_lists  [visible_bits]
+ *   c.list/causal-list->edn count (list.cljc:57-66, 77) -> visible_bits/_count
+ *   s/spin 1-arity         (shared.cljc:121-132) -> cw_weave_lists [yarn_perm]
+ *   s/refresh-ts           (shared.cljc:243-249) -> cw_weave_lists [max_ts]
+ *   s/refresh-caches       (shared.cljc:259-266) = all of the above in one call
+ *
+ * The JVM shim calls it from c.list/weave's 1-arity and from
+ * s/refresh-caches; insert/append/merge reach it through a full reweave.
+ *
+ * Conventions
+ *  - Plain pointers and sizes, no torch/HIP types.  Every buffer is owned by the
+ *    caller; the library keeps nothing after a call returns except reusable
+ *    device scratch inside the context.
+ *  - Ids are order-preserving packed 64-bit keys (cause_amd/pack.py):
+ *      key(a) < key(b)  <=>  (compare a b) < 0   (util.cljc:4-10)
+ *    CW_NIL (all ones) is nil and is reserved (root's cause).
+ *  - A document's nodes may come in any order (the ::nodes hash map,
+ *    shared.cljc:62).  The root [[0 "0" 0] nil nil] (shared.cljc:22-23) is one
+ *    of them, flagged CW_KIND_ROOT.
+ *  - Return value: 0 ok, < 0 error (cw_last_error has the text).  Per-document
+ *    problems are reported in status[] instead (CW_STATUS_*).  A document with
+ *    a non-zero status is outside the fast path's domain (it would throw in the
+ *    reference's s/insert, shared.cljc:163-178); its outputs are well-formed
+ *    but unspecified.
+ *  - A context is not thread-safe; use one context per host thread.  Calls are
+ *    re-entrant with respect to each other's inputs (pure functions; swap!
+ *    retries may repeat them).
+ */
+#ifndef CAUSEWEAVE_H
+#define CAUSEWEAVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CW_ABI_VERSION 1
+#define CW_NIL UINT64_MAX
+
+/* Node value class (shared.cljc:21 special-keywords) | CW_KIND_ROOT. */
+enum {
+  CW_KIND_NORMAL = 0,
+  CW_KIND_HIDE = 1,   /* :causal/hide   */
+  CW_KIND_HHIDE = 2,  /* :causal/h.hide */
+  CW_KIND_HSHOW = 3,  /* :causal/h.show */
+  CW_KIND_ROOT = 4
+};
+
+/* Per-document status bits. */
+enum {
+  CW_STATUS_ROOT = 1u << 0,        /* no root, several roots, or root not the smallest id */
+  CW_STATUS_DUP = 1u << 1,         /* two nodes share an id (shared.cljc:166-171)          */
+  CW_STATUS_ORPHAN = 1u << 2,      /* a cause is not in the document (shared.cljc:175-178) */
+  CW_STATUS_NON_LAMPORT = 1u << 3, /* a cause id is not older than its node                */
+  CW_STATUS_INTERNAL = 1u << 5     /* consistency check failed inside the pipeline         */
+};
+
+/* Where the arrays of a batch/result live. */
+enum { CW_MEM_HOST = 0, CW_MEM_DEVICE = 1 };
+
+typedef struct cw_ctx cw_ctx;
+
+/* ABI version (CW_ABI_VERSION). */
+int cw_abi_version(void);
+
+/* Create a context on HIP device `device` (its own stream).  0 on success. */
+int cw_ctx_create(int device, cw_ctx **out);
+void cw_ctx_destroy(cw_ctx *ctx);
+/* Text of the last error on this context ("" if none). */
+const char *cw_last_error(const cw_ctx *ctx);
+/* Launch on an existing HIP stream (hipStream_t passed as void*); NULL restores
+ * the context's own stream. */
+int cw_ctx_set_stream(cw_ctx *ctx, void *hip_stream);
+/* 0: synchronous calls (default).  1: device-memory calls return right after
+ * enqueueing (the caller synchronises the stream). */
+int cw_ctx_set_async(cw_ctx *ctx, int async);
+/* Per-kernel timing with HIP events on the launch stream (adds a sync per call). */
+int cw_ctx_set_profiling(cw_ctx *ctx, int on);
+
+typedef struct {
+  char name[48];
+  uint64_t launches;
+  double total_ms;     /* sum of event-measured durations                */
+  double bytes_alg;    /* algorithmic HBM bytes over all launches */
+} cw_kernel_stat;
+
+/* Copies up to `cap` stats; returns how many kernels have stats. */
+int cw_get_kernel_stats(const cw_ctx *ctx, cw_kernel_stat *out, int cap);
+int cw_reset_kernel_stats(cw_ctx *ctx);
+
+/* ---------------------------------------------------------------- lists ---- */
+typedef struct {
+  uint64_t n_docs;
+  const uint64_t *doc_offsets; /* HOST memory, [n_docs+1], doc d = [off[d], off[d+1]) */
+  const uint64_t *id_key;      /* [N] packed id of each node                           */
+  const uint64_t *cause_key;   /* [N] packed cause id (CW_NIL for the root)            */
+  const uint8_t *kind;         /* [N] CW_KIND_*                                        */
+  uint32_t key_bits;           /* significant bits of id keys; 0 = find on the device   */
+  uint32_t ts_shift;           /* lamport-ts = id_key >> ts_shift                       */
+  uint32_t site_shift;         /* site rank = (id_key >> site_shift) & (2^site_bits-1)  */
+  uint32_t site_bits;          /* 0 = no yarn output                                    */
+} cw_list_batch;
+
+typedef struct {
+  uint32_t *weave_perm;    /* [N]: position doc_off[d]+p holds the doc-local input index
+                              of the node at weave position p (root at p = 0)          */
+  uint32_t *visible_bits;  /* [(N+31)/32]: bit g (word g/32, bit g%32) set iff global
+                              weave position g renders (not hide?, list.cljc:48-55)     */
+  uint32_t *visible_count; /* [n_docs] count of rendered nodes (list.cljc:77)          */
+  uint64_t *max_ts;        /* [n_docs] ::lamport-ts after refresh-ts, or NULL         */
+  uint32_t *status;        /* [n_docs] CW_STATUS_* bits                                */
+  uint32_t *yarn_perm;     /* [N] or NULL: doc-local input indices grouped by site rank,
+                              id-ascending inside a site (the ::yarns cache)            */
+} cw_list_result;
+
+/* Full reweave of a batch of independent CausalLists (N = doc_offsets[n_docs]
+ * < 2^32, each document < 2^31 nodes).  `memspace` says where id_key /
+ * cause_key / kind and every result array live (doc_offsets is always host). */
+int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
+                   int memspace);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAUSEWEAVE_H */

@@ -1,0 +1,46 @@
+"""The C-ABI library loads on a CPU-only host and exports exactly what
+include/causeweave.h declares (no compute calls here)."""
+import ctypes
+import subprocess
+
+import pytest
+
+from cause_amd import abi
+
+
+def test_header_declares_the_entry_points():
+    names = abi.header_functions()
+    for must in ("cw_abi_version", "cw_ctx_create", "cw_ctx_destroy", "cw_last_error",
+                 "cw_ctx_set_stream", "cw_ctx_set_async", "cw_ctx_set_profiling",
+                 "cw_get_kernel_stats", "cw_reset_kernel_stats", "cw_weave_lists"):
+        assert must in names
+
+
+def test_library_exports_every_header_symbol():
+    L = abi.lib()
+    for name in abi.header_functions():
+        assert hasattr(L, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert set(abi.header_functions()) <= exported
+
+
+def test_abi_version():
+    assert abi.lib().cw_abi_version() == 1
+
+
+def test_struct_layout_matches_header():
+    # 4 pointers-or-u64 + 4 u32 fields, naturally aligned on x86-64
+    assert ctypes.sizeof(abi.CwListBatch) == 8 * 5 + 4 * 4
+    assert ctypes.sizeof(abi.CwListResult) == 8 * 6
+    assert ctypes.sizeof(abi.CwKernelStat) == 48 + 8 * 3
+
+
+def test_no_gpu_means_a_loud_error():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(abi.WeaveError):
+        abi.Weaver(0)

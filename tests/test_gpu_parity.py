@@ -1,0 +1,185 @@
+"""HIP weave vs the CPU oracle, bit-exact (run on the MI355X box: -m gpu).
+
+Every call goes through the C ABI (cause_amd.abi -> libcauseweave.so).
+Outputs compared: weave order (weave_perm), visibility (hide?, list.cljc:48-55),
+visible count (list.cljc:77), ::lamport-ts (refresh-ts, shared.cljc:243-249),
+yarns (spin, shared.cljc:121-132) and per-document status.
+"""
+import dataclasses
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from oracle import causal_ref as R
+from cause_amd import abi, gen, pack
+from tests import refgen as G
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def weaver():
+    with abi.Weaver(0) as w:
+        yield w
+
+
+def oracle_batch(off, idk, ck, kd, layout, method=oracle.METHOD_LITERAL):
+    perm, vis, st = oracle.batch_lists(off, idk, ck, kd, method=method)
+    D = len(off) - 1
+    vcount = np.array([int(vis[int(off[d]):int(off[d + 1])].sum()) for d in range(D)], np.uint32)
+    max_ts = np.array([int(idk[int(off[d]):int(off[d + 1])].max() >> np.uint64(layout.ts_shift))
+                       if off[d + 1] > off[d] else 0 for d in range(D)], np.uint64)
+    return perm, vis, st, vcount, max_ts
+
+
+def check_batch(weaver, off, idk, ck, kd, layout, method=oracle.METHOD_LITERAL, yarns=True):
+    res = weaver.weave_lists(off, idk, ck, kd, layout, yarns=yarns)
+    perm, vis, st, vcount, max_ts = oracle_batch(off, idk, ck, kd, layout, method)
+    ok = st == 0
+    assert np.array_equal(res.status, st), (res.status, st)
+    D = len(off) - 1
+    gvis = res.visible()
+    for d in np.nonzero(ok)[0]:
+        b, e = int(off[d]), int(off[d + 1])
+        assert np.array_equal(res.weave_perm[b:e], perm[b:e]), f"doc {d} order"
+        assert np.array_equal(gvis[b:e], vis[b:e]), f"doc {d} visibility"
+    assert np.array_equal(res.visible_count[ok], vcount[ok])
+    assert np.array_equal(res.max_ts[ok], max_ts[ok])
+    if yarns and layout.site_bits:
+        mask = (1 << layout.site_bits) - 1
+        for d in np.nonzero(ok)[0]:
+            b, e = int(off[d]), int(off[d + 1])
+            want = oracle.list_yarns(idk[b:e], layout.site_shift, mask)
+            assert np.array_equal(res.yarn_perm[b:e], want), f"doc {d} yarns"
+    return res
+
+
+def test_reference_edge_cases(weaver):
+    docs = [[R.ROOT_NODE] + case for case in G.EDGE_CASES]
+    rng = random.Random(1)
+    for d in docs:
+        rng.shuffle(d)
+    b = pack.pack_lists(docs)
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+def test_reference_random_histories(weaver):
+    rng = random.Random(42)
+    docs = []
+    for steps in (1, 2, 5, 9, 20, 60, 150):
+        for _ in range(30):
+            nodes, _ = G.random_history(rng, steps)
+            d = [R.ROOT_NODE] + nodes
+            rng.shuffle(d)
+            docs.append(d)
+    b = pack.pack_lists(docs)
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+def test_stress_histories(weaver):
+    rng = random.Random(7)
+    docs = []
+    for n in (10, 100, 700):
+        for p_special in (0.05, 0.3, 0.6):
+            for tx_chain in (0.0, 0.3):
+                d = G.stress_history(rng, n, p_special=p_special, p_conj=0.15,
+                                     tx_chain=tx_chain)
+                rng.shuffle(d)
+                docs.append(d)
+    b = pack.pack_lists(docs)
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+def test_tiny_and_empty_documents(weaver):
+    docs = [[R.ROOT_NODE], [], [R.ROOT_NODE, ((1, "aaaaaaaaaaaaa", 0), R.ROOT_ID, "x")],
+            [R.ROOT_NODE, ((1, "aaaaaaaaaaaaa", 0), R.ROOT_ID, R.HIDE)]]
+    b = pack.pack_lists(docs)
+    res = weaver.weave_lists(b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    assert list(res.status) == [0, abi.STATUS_ROOT, 0, 0]
+    assert list(res.visible_count) == [0, 0, 1, 0]
+    assert list(res.weave_perm[:1]) == [0]
+
+
+def test_out_of_domain_status(weaver):
+    s = "aaaaaaaaaaaaa"
+    docs = [
+        [R.ROOT_NODE, ((1, s, 0), R.ROOT_ID, "x"), ((2, s, 0), (7, "bbbbbbbbbbbbb", 0), "y")],
+        [R.ROOT_NODE, ((1, s, 0), (3, s, 0), "x"), ((3, s, 0), R.ROOT_ID, "y")],
+        [((1, s, 0), R.ROOT_ID, "x")],
+        [R.ROOT_NODE, ((1, s, 0), R.ROOT_ID, "x"), ((1, s, 0), R.ROOT_ID, "x")],
+        [R.ROOT_NODE, ((1, s, 0), R.ROOT_ID, "x")],
+    ]
+    b = pack.pack_lists(docs)
+    res = weaver.weave_lists(b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    assert res.status[0] & abi.STATUS_ORPHAN
+    assert res.status[1] & abi.STATUS_NON_LAMPORT
+    assert res.status[2] & abi.STATUS_ROOT
+    assert res.status[3] & abi.STATUS_DUP
+    assert res.status[4] == 0
+
+
+def test_generated_config2_shape(weaver):
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=5000)
+    off, idk, ck, kd = gen.generate(spec, 0, 120)
+    check_batch(weaver, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF)
+
+
+def test_generated_mixed_sizes(weaver):
+    """Documents spanning many sort tiles and many splitter blocks, plus
+    tiny ones, in one batch."""
+    parts = []
+    for n, D, seed in ((3, 50, 1), (4095, 3, 2), (4097, 3, 3), (70_000, 2, 4), (17, 40, 5)):
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n, seed=seed)
+        parts.append(gen.generate(spec, 0, D))
+    lay = pack.KeyLayout(17, 4, 0)
+    sizes = np.concatenate([np.diff(p[0]) for p in parts])
+    off = np.zeros(len(sizes) + 1, np.uint64)
+    off[1:] = np.cumsum(sizes)
+    idk = np.concatenate([p[1] for p in parts])
+    ck = np.concatenate([p[2] for p in parts])
+    kd = np.concatenate([p[3] for p in parts])
+    ck = np.where(ck == np.uint64(pack.NIL), ck, ck)  # same layout (site_bits 4)
+    check_batch(weaver, off, idk, ck, kd, lay, method=oracle.METHOD_EFF)
+
+
+def test_config1_single_large_list(weaver):
+    off, idk, ck, kd = gen.generate(gen.CONFIG1, 0, 1)
+    check_batch(weaver, off, idk, ck, kd, gen.CONFIG1.layout(), method=oracle.METHOD_LINKED)
+
+
+def test_typing_chain_depth(weaver):
+    """One site typing 200k characters in a row: the effective tree is a
+    single chain of depth n (the Euler walk must not depend on depth)."""
+    spec = dataclasses.replace(gen.CONFIG1, nodes_per_doc=200_000, n_sites=1, p_chain=1.0,
+                               shuffle=True)
+    off, idk, ck, kd = gen.generate(spec, 0, 1)
+    check_batch(weaver, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_LINKED)
+
+
+def test_all_caused_by_root(weaver):
+    """cons- shape (list.cljc:42-43): every node caused by the root."""
+    s = "aaaaaaaaaaaaa"
+    doc = [R.ROOT_NODE] + [((t, s, 0), R.ROOT_ID, "c") for t in range(1, 30_001)]
+    random.Random(3).shuffle(doc)
+    b = pack.pack_lists([doc])
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout,
+                method=oracle.METHOD_LINKED)
+
+
+def test_repeat_calls_are_identical(weaver):
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000)
+    off, idk, ck, kd = gen.generate(spec, 0, 30)
+    a = weaver.weave_lists(off, idk, ck, kd, spec.layout())
+    b = weaver.weave_lists(off, idk, ck, kd, spec.layout())
+    assert np.array_equal(a.weave_perm, b.weave_perm)
+    assert np.array_equal(a.visible_bits, b.visible_bits)
+
+
+def test_key_bits_found_on_device(weaver):
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000)
+    off, idk, ck, kd = gen.generate(spec, 0, 10)
+    a = weaver.weave_lists(off, idk, ck, kd, spec.layout())
+    b = weaver.weave_lists(off, idk, ck, kd, spec.layout(), key_bits=0)
+    assert np.array_equal(a.weave_perm, b.weave_perm)
