@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -42,9 +43,11 @@ using namespace cw;
 // Device kernels
 // ============================================================================
 
-// Block-wide exclusive scan of one value per thread (blockDim.x = 64*W).
+// Block-wide exclusive scan of one value per thread (blockDim.x = 64*W,
+// wtot has blockDim.x/64 entries).  NT = 0: block size taken at run time.
 template <int NT>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uint32_t *total) {
+  const int nw = NT ? NT / 64 : (int)(blockDim.x >> 6);
   const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -55,8 +58,7 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uin
   if (lane == 63) wtot[w] = x;
   __syncthreads();
   uint32_t before = 0, all = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; i++) {
+  for (int i = 0; i < nw; i++) {
     uint32_t t = wtot[i];
     before += (i < (int)w) ? t : 0u;
     all += t;
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(256) void k_radix_hist(const K *__restrict__ keys,
                                                     uint32_t shift, uint32_t dmask,
                                                     uint32_t *__restrict__ hist) {
   __shared__ uint32_t h[4][RADIX];
-  const uint32_t t = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), tid = threadIdx.x, w = tid >> 6;
   for (uint32_t i = tid; i < 4 * RADIX; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
   const uint32_t s = tile_start[t], e = tile_start[t + 1];
@@ -111,14 +113,15 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
     uint32_t *__restrict__ vals_out, const uint32_t *__restrict__ tile_start,
     const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
-    const uint32_t *__restrict__ offs, uint32_t shift, uint32_t dmask) {
+    const uint32_t *__restrict__ offs, uint32_t shift, uint32_t dmask,
+    uint32_t *__restrict__ inv) {
   __shared__ K skey[TILE];
   __shared__ uint32_t sval[TILE];
   __shared__ uint32_t wcnt[2][SORT_WAVES][RADIX];
   __shared__ uint32_t run[RADIX], bstart[RADIX], soff[RADIX];
   __shared__ uint32_t wtot[SORT_WAVES];
 
-  const uint32_t t = blockIdx.x, tid = threadIdx.x, w = tid >> 6;
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), tid = threadIdx.x, w = tid >> 6;
   const uint32_t s = tile_start[t], e = tile_start[t + 1];
   const uint32_t len = e - s;
   const uint32_t lbase = s - doc_off[tile_doc[t]];
@@ -185,6 +188,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const uint32_t dst = soff[d] + j - bstart[d];
     keys_out[dst] = kk;
     vals_out[dst] = sval[j];
+    if (inv) inv[s - lbase + sval[j]] = dst - (s - lbase);  // rank of each input node
   }
 }
 
@@ -204,15 +208,34 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_join(
+// Every 2^ls-th sorted id of each document, compacted (join's LDS index).
+__global__ __launch_bounds__(256) void k_sample(const uint64_t *__restrict__ skey,
+                                                const uint32_t *__restrict__ doc_off,
+                                                const uint32_t *__restrict__ doc_ls,
+                                                const uint32_t *__restrict__ samp_off,
+                                                uint64_t *__restrict__ samples) {
+  const uint32_t d = blockIdx.x, base = doc_off[d], n = doc_off[d + 1] - base;
+  const uint32_t ls = doc_ls[d], ns = samp_off[d + 1] - samp_off[d];
+  for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x)
+    samples[samp_off[d] + j] = skey[base + ((uint64_t)j << ls)];
+  (void)n;
+}
+
+// Join in sorted order: gather each node's cause id and kind, search the cause
+// among the document's sorted ids (LDS samples, then one span of 2^ls keys).
+__global__ __launch_bounds__(1024) void k_join(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
-    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
-    const uint32_t *__restrict__ doc_off, uint32_t *__restrict__ par,
-    uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
+    const uint64_t *__restrict__ samples, const uint32_t *__restrict__ samp_off,
+    const uint32_t *__restrict__ doc_ls, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    uint32_t *__restrict__ par, uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t S[];  // <= MAX_SAMPLES
   __shared__ uint32_t bst;
-  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  const uint32_t ls = doc_ls[d], s0 = samp_off[d], ns = samp_off[d + 1] - s0;
+  for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) S[j] = samples[s0 + j];
   if (threadIdx.x == 0) bst = 0;
   __syncthreads();
   uint32_t st = 0;
@@ -225,11 +248,24 @@ __global__ __launch_bounds__(256) void k_join(
       if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
     } else {
       if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
-      const uint64_t my = skey[i];
-      if (my == skey[i - 1]) st |= CW_STATUS_DUP;
       const uint64_t ck = cause_key[gi];
-      const uint32_t c = lower_bound_u64(skey + base, n, ck);
-      if (c == n || skey[base + c] != ck) st |= CW_STATUS_ORPHAN;
+      uint32_t lo = 0, len = ns;  // count of samples <= ck
+      while (len > 0) {
+        const uint32_t half = len >> 1;
+        if (S[lo + half] <= ck) { lo += half + 1; len -= half + 1; }
+        else len = half;
+      }
+      uint32_t c = n;
+      if (lo > 0) {
+        uint32_t a0 = (lo - 1) << ls;
+        uint32_t b0 = min(a0 + (1u << ls), n);
+        while (a0 < b0) {
+          const uint32_t m = (a0 + b0) >> 1;
+          if (skey[base + m] < ck) a0 = m + 1; else b0 = m;
+        }
+        c = a0;
+      }
+      if (c >= n || skey[base + c] != ck) st |= CW_STATUS_ORPHAN;
       else if (c >= r) st |= CW_STATUS_NON_LAMPORT;
       else p = c;
     }
@@ -243,14 +279,17 @@ __global__ __launch_bounds__(256) void k_join(
 
 // --- effective parent + child-sort key ---------------------------------------
 // child key = ((eff+1) << 1) | (special ? 0 : 1); the root gets 0 (sorts first).
-__global__ __launch_bounds__(256) void k_eff(const uint32_t *__restrict__ par,
+__global__ __launch_bounds__(1024) void k_eff(const uint32_t *__restrict__ par,
                                              const uint8_t *__restrict__ skind,
+                                             const uint64_t *__restrict__ skey,
+                                             uint32_t *__restrict__ status,
                                              const uint32_t *__restrict__ tile_start,
                                              const uint32_t *__restrict__ tile_doc,
                                              const uint32_t *__restrict__ doc_off,
                                              uint32_t *__restrict__ epar,
                                              uint32_t *__restrict__ ckey) {
-  const uint32_t t = blockIdx.x, base = doc_off[tile_doc[t]];
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t], base = doc_off[d];
+  bool dup = false;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
     const uint32_t r = i - base;
     if (r == 0) {
@@ -258,6 +297,7 @@ __global__ __launch_bounds__(256) void k_eff(const uint32_t *__restrict__ par,
       ckey[i] = 0;
       continue;
     }
+    dup |= skey[i] == skey[i - 1];
     const uint8_t k = skind[i];
     uint32_t c = par[i];
     const bool sp = is_special(k);
@@ -266,6 +306,7 @@ __global__ __launch_bounds__(256) void k_eff(const uint32_t *__restrict__ par,
     epar[i] = c;
     ckey[i] = ((c + 1) << 1) | (sp ? 0u : 1u);
   }
+  if (dup) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
 }
 
 // --- links --------------------------------------------------------------------
@@ -273,7 +314,7 @@ __global__ __launch_bounds__(256) void k_eff(const uint32_t *__restrict__ par,
 // Sibling order is specials by descending id, then non-specials by descending
 // id, so the next sibling inside a class is the previous group element and the
 // first child of a class is the group's last element.
-__global__ __launch_bounds__(256) void k_links(const uint32_t *__restrict__ ckey_s,
+__global__ __launch_bounds__(1024) void k_links(const uint32_t *__restrict__ ckey_s,
                                                const uint32_t *__restrict__ cval_s,
                                                const uint32_t *__restrict__ tile_start,
                                                const uint32_t *__restrict__ tile_doc,
@@ -281,7 +322,7 @@ __global__ __launch_bounds__(256) void k_links(const uint32_t *__restrict__ ckey
                                                uint32_t *__restrict__ nsc,
                                                uint32_t *__restrict__ fcS,
                                                uint32_t *__restrict__ fcN) {
-  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
     const uint32_t key = ckey_s[i];
@@ -295,13 +336,13 @@ __global__ __launch_bounds__(256) void k_links(const uint32_t *__restrict__ ckey
   }
 }
 
-__global__ __launch_bounds__(256) void k_link_final(
+__global__ __launch_bounds__(1024) void k_link_final(
     const uint32_t *__restrict__ nsc, const uint32_t *__restrict__ fcS,
     const uint32_t *__restrict__ fcN, const uint32_t *__restrict__ epar,
     const uint8_t *__restrict__ skind, const uint32_t *__restrict__ tile_start,
     const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, uint64_t *__restrict__ link) {
-  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
     const uint32_t r = i - base;
@@ -330,59 +371,113 @@ __global__ __launch_bounds__(256) void k_link_final(
 // Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
 // splitter block lw/2's splitter node and follows the tour until the next
 // splitter arc.  Every down arc it crosses gets (walker, local count).
-__global__ __launch_bounds__(WALK_THREADS) void k_walk(
+// Each lane advances NW walkers in lock-step so NW independent link loads are
+// in flight per lane (the walk is a pointer chase: latency, not bandwidth).
+template <int NW>
+__global__ __launch_bounds__(1024) void k_walk(
     const uint64_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
     const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_W,
     const uint32_t *__restrict__ walk_first, uint64_t *__restrict__ loc,
-    uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext, uint32_t *__restrict__ status) {
-  const uint32_t b = blockIdx.x, d = wblk_doc[b];
-  const uint32_t lw = wblk_w0[b] + threadIdx.x;
-  if (lw >= doc_W[d]) return;
+    uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext, uint32_t *__restrict__ status,
+    uint32_t walk_span) {
+  __shared__ uint32_t next_walker;
+  const uint32_t b = xcd_tile(blockIdx.x, gridDim.x), d = wblk_doc[b];
+  const uint32_t w0 = wblk_w0[b], w1 = min(w0 + walk_span, doc_W[d]);
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
-  uint32_t v = split_node(d, lw >> 1, log2k, n);
-  uint32_t dir = lw & 1;  // 0 = down, 1 = up
-  uint32_t cnt = 0, nextsub = NX_END;
-  if (dir == 0) {
-    loc[base + v] = (uint64_t)lw << 32;
-    cnt = 1;
-  }
-  uint64_t L = link[base + v];
+  const uint32_t f = walk_first[d];
   const uint32_t max_steps = 2 * n + 2;
-  for (uint32_t steps = 0;; steps++) {
-    uint32_t u, ndir;
-    if (dir == 0) {
-      const uint32_t fc = (uint32_t)L & LINK_IDX;
-      if (fc) { u = fc; ndir = 0; }
-      else { u = v; ndir = 1; }
-    } else {
-      const uint32_t nx = (uint32_t)(L >> 32);
-      if (nx == NX_END) break;
-      if (nx & NX_UP) { u = nx & ~NX_UP; ndir = 1; }
-      else { u = nx; ndir = 0; }
+  if (threadIdx.x == 0) next_walker = w0 + blockDim.x * NW;
+  __syncthreads();
+
+  // slot state: 0 idle, 1 starting (load link of v), 2 running (load link of u)
+  uint32_t st[NW], lw[NW], v[NW], dir[NW], cnt[NW], u[NW], nd[NW], steps[NW];
+  uint64_t L[NW];
+  auto start = [&](int k, uint32_t id) {
+    lw[k] = id;
+    v[k] = split_node(d, id >> 1, log2k, n);
+    dir[k] = id & 1;
+    cnt[k] = 0;
+    steps[k] = 0;
+    if (dir[k] == 0) {
+      loc[base + v[k]] = (uint64_t)id << 32;
+      cnt[k] = 1;
     }
-    const uint64_t Lu = (u == v) ? L : link[base + u];
-    if ((uint32_t)Lu & LINK_SPLIT) {
-      nextsub = ((u >> log2k) << 1) | ndir;
-      break;
+    st[k] = 1;
+  };
+  auto finish = [&](int k, uint32_t nextsub) {
+    wcnt[f + lw[k]] = cnt[k];
+    wnext[f + lw[k]] = nextsub;
+    const uint32_t id = atomicAdd(&next_walker, 1u);
+    if (id < w1) start(k, id);
+    else st[k] = 0;
+  };
+#pragma unroll
+  for (int k = 0; k < NW; k++) {
+    const uint32_t id = w0 + threadIdx.x + k * blockDim.x;
+    st[k] = 0;
+    if (id < w1) start(k, id);
+  }
+  for (;;) {
+    bool any = false;
+    // A: next arc of each running walker
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+      if (st[k] == 2) {
+        if (dir[k] == 0) {
+          const uint32_t fc = (uint32_t)L[k] & LINK_IDX;
+          if (fc) { u[k] = fc; nd[k] = 0; }
+          else { u[k] = v[k]; nd[k] = 1; }
+        } else {
+          const uint32_t nx = (uint32_t)(L[k] >> 32);
+          if (nx == NX_END) finish(k, NX_END);
+          else if (nx & NX_UP) { u[k] = nx & ~NX_UP; nd[k] = 1; }
+          else { u[k] = nx; nd[k] = 0; }
+        }
+      }
+      any |= st[k] != 0;
     }
-    if (ndir == 0) {
-      loc[base + u] = ((uint64_t)lw << 32) | cnt;
-      cnt++;
+    if (!any) break;
+    // B: independent loads
+    uint64_t X[NW];
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+      X[k] = L[k];
+      if (st[k] == 1) X[k] = link[base + v[k]];
+      else if (st[k] == 2 && u[k] != v[k]) X[k] = link[base + u[k]];
     }
-    v = u;
-    dir = ndir;
-    L = Lu;
-    if (steps > max_steps) {
-      atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
-      break;
+    // C: advance
+#pragma unroll
+    for (int k = 0; k < NW; k++) {
+      if (st[k] == 1) {
+        L[k] = X[k];
+        st[k] = 2;
+      } else if (st[k] == 2) {
+        if ((uint32_t)X[k] & LINK_SPLIT) {
+          finish(k, ((u[k] >> log2k) << 1) | nd[k]);
+        } else {
+          if (nd[k] == 0) {
+            loc[base + u[k]] = ((uint64_t)lw[k] << 32) | cnt[k];
+            cnt[k]++;
+          }
+          v[k] = u[k];
+          dir[k] = nd[k];
+          L[k] = X[k];
+          if (++steps[k] > max_steps) {
+            atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+            finish(k, NX_END);
+          }
+        }
+      }
     }
   }
-  wcnt[walk_first[d] + lw] = cnt;
-  wnext[walk_first[d] + lw] = nextsub;
 }
 
-// --- sublist ranking (one workgroup per document, Wyllie pointer jumping in LDS)
+// --- sublist ranking: one workgroup per document, all in LDS -------------------
+// The W sublists of a document form one linked list (the Euler tour).  Every
+// CHAIN-th sublist id heads an LDS chain; one lane per head walks its chain
+// (prefix sums in place), lane 0 ranks the <= W/CHAIN chains, then every
+// sublist gets chain base + local prefix = number of down arcs before it.
 __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               const uint32_t *__restrict__ wnext,
                                               const uint32_t *__restrict__ walk_first,
@@ -392,55 +487,74 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               uint32_t *__restrict__ sbase,
                                               uint64_t *__restrict__ max_ts,
                                               uint32_t *__restrict__ status) {
-  __shared__ uint32_t val[2][MAX_SUBLISTS];
-  __shared__ uint32_t nx[2][MAX_SUBLISTS];
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // nx[W], val[W]
+  __shared__ uint32_t ch_next[MAX_SUBLISTS / CHAIN], ch_sum[MAX_SUBLISTS / CHAIN];
+  __shared__ uint32_t ch_base[MAX_SUBLISTS / CHAIN];
+  __shared__ uint32_t bad_s;
   const uint32_t d = blockIdx.x, W = doc_W[d], f = walk_first[d];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   if (threadIdx.x == 0 && max_ts) max_ts[d] = n ? (skey[base + n - 1] >> ts_shift) : 0ull;
   if (W == 0) return;
+  uint32_t *nx = sm, *val = sm + W;
   for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
-    val[0][i] = wcnt[f + i];
-    nx[0][i] = wnext[f + i];
+    nx[i] = wnext[f + i];
+    val[i] = wcnt[f + i];
+  }
+  if (threadIdx.x == 0) bad_s = 0;
+  __syncthreads();
+  const uint32_t C = (W + CHAIN - 1) / CHAIN;
+  for (uint32_t h = threadIdx.x; h < C; h += blockDim.x) {
+    uint32_t j = h * CHAIN, acc = 0, steps = 0;
+    for (;;) {
+      const uint32_t x = nx[j], cval = val[j];
+      val[j] = acc;  // down arcs before j inside the chain
+      nx[j] = h;     // chain of j
+      acc += cval;
+      if (x == NX_END || x % CHAIN == 0 || x >= W || ++steps > W) {
+        ch_next[h] = (x == NX_END || x >= W) ? NX_END : x / CHAIN;
+        ch_sum[h] = acc;
+        if (x != NX_END && x % CHAIN != 0) bad_s = 1;
+        break;
+      }
+      j = x;
+    }
   }
   __syncthreads();
-  uint32_t cur = 0;
-  for (uint32_t span = 1; span < W; span <<= 1) {
-    for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
-      const uint32_t x = nx[cur][i];
-      if (x != NX_END) {
-        val[cur ^ 1][i] = val[cur][i] + val[cur][x];
-        nx[cur ^ 1][i] = nx[cur][x];
-      } else {
-        val[cur ^ 1][i] = val[cur][i];
-        nx[cur ^ 1][i] = NX_END;
-      }
+  if (threadIdx.x == 0) {
+    uint32_t run = 0, c = 0, steps = 0;
+    while (c != NX_END && steps++ <= C) {
+      ch_base[c] = run;
+      run += ch_sum[c];
+      c = ch_next[c];
     }
-    __syncthreads();
-    cur ^= 1;
+    if (run != n || bad_s) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
   }
-  const uint32_t total = val[cur][0];  // sublist 0 = down(root) heads the tour
-  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) sbase[f + i] = total - val[cur][i];
-  if (threadIdx.x == 0 && total != n) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x)
+    sbase[f + i] = ch_base[min(nx[i], C - 1)] + val[i];
 }
 
 // --- emit: rank order -> weave order -------------------------------------------
-__global__ __launch_bounds__(256) void k_emit(
+__global__ __launch_bounds__(1024) void k_emit(
     const uint64_t *__restrict__ loc, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ link, const uint32_t *__restrict__ sbase,
     const uint32_t *__restrict__ walk_first, const uint32_t *__restrict__ doc_W,
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, uint32_t *__restrict__ perm,
     uint8_t *__restrict__ vis8, uint32_t *__restrict__ vcount, uint32_t *__restrict__ status) {
-  __shared__ uint32_t wtot[4];
-  const uint32_t t = blockIdx.x, d = tile_doc[t];
+  __shared__ uint32_t wtot[16];
+  extern __shared__ __attribute__((aligned(16))) uint32_t sb[];  // walker bases of doc d
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d], W = doc_W[d];
+  for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) sb[j] = sbase[f + j];
+  __syncthreads();
   uint32_t nvis = 0;
   bool bad = false;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
     const uint64_t L = loc[i];
     const uint32_t lw = (uint32_t)(L >> 32);
     if (lw >= W) { bad = true; continue; }
-    const uint32_t pos = sbase[f + lw] + (uint32_t)L;
+    const uint32_t pos = sb[lw] + (uint32_t)L;
     if (pos >= n) { bad = true; continue; }
     const uint32_t v = ((uint32_t)link[i] & LINK_VIS) ? 1u : 0u;
     perm[base + pos] = sval[i];
@@ -449,7 +563,7 @@ __global__ __launch_bounds__(256) void k_emit(
   }
   if (bad) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
   uint32_t total;
-  block_exscan<256>(nvis, wtot, &total);
+  block_exscan<0>(nvis, wtot, &total);
   if (threadIdx.x == 0 && total) atomicAdd(&vcount[d], total);
 }
 
@@ -523,10 +637,13 @@ struct cw_ctx {
   std::vector<uint64_t> last_off;
   struct Tables {
     std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
-        wblk_doc, wblk_w0;
-    uint32_t T = 0, Wtot = 0, Bw = 0, nmax = 0;
+        wblk_doc, wblk_w0, doc_ls, samp_off;
+    uint32_t T = 0, Wtot = 0, Bw = 0, nmax = 0, Stot = 0, Wmax = 0, Smax = 0;
   } tab;
   bool tab_on_device = false;
+  // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
+           walk_nw = 1, join_lds = 0;
 };
 
 namespace {
@@ -643,8 +760,12 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.walk_first.resize(D + 1);
   t.wblk_doc.clear();
   t.wblk_w0.clear();
-  uint32_t wtot = 0;
+  t.doc_ls.resize(D);
+  t.samp_off.resize(D + 1);
+  uint32_t wtot = 0, stot = 0;
   t.nmax = 0;
+  t.Wmax = 0;
+  t.Smax = 0;
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
     t.doc_off[d] = b;
@@ -654,22 +775,33 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
       t.tile_start.push_back(b + s);
       t.tile_doc.push_back((uint32_t)d);
     }
-    // splitter block size K = 2^log2k, at most MAX_SUBLISTS/2 blocks per doc
-    uint32_t log2k = std::max(MIN_LOG2K, ceil_log2((n + MAX_SUBLISTS / 2 - 1) / (MAX_SUBLISTS / 2)));
+    // splitter block size K = 2^log2k, at most MAX_SUBLISTS/2 splitters per doc
+    uint32_t log2k = std::max(c->min_log2k, ceil_log2((n + MAX_SUBLISTS / 2 - 1) / (MAX_SUBLISTS / 2)));
     const uint32_t S = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;
     const uint32_t W = 2 * S;
     t.doc_log2k[d] = log2k;
     t.doc_W[d] = W;
+    t.Wmax = std::max(t.Wmax, W);
     t.walk_first[d] = wtot;
-    for (uint32_t w0 = 0; w0 < W; w0 += WALK_THREADS) {
+    for (uint32_t w0 = 0; w0 < W; w0 += c->walk_span) {
       t.wblk_doc.push_back((uint32_t)d);
       t.wblk_w0.push_back(w0);
     }
     wtot += W;
+    // join samples: every 2^ls-th sorted id, at most MAX_SAMPLES per document
+    const uint32_t ls =
+        std::max(MIN_LOG2_STRIDE, ceil_log2((n + MAX_SAMPLES - 1) / MAX_SAMPLES));
+    t.doc_ls[d] = ls;
+    t.samp_off[d] = stot;
+    const uint32_t ns = n ? ((n - 1) >> ls) + 1 : 0;
+    t.Smax = std::max(t.Smax, ns);
+    stot += ns;
   }
   t.doc_off[D] = (uint32_t)off[D];
   t.tile_first[D] = (uint32_t)t.tile_start.size();
   t.walk_first[D] = wtot;
+  t.samp_off[D] = stot;
+  t.Stot = stot;
   t.T = (uint32_t)t.tile_doc.size();
   t.tile_start.push_back((uint32_t)off[D]);
   t.Wtot = wtot;
@@ -681,7 +813,8 @@ int upload_tables(cw_ctx *c) {
   std::vector<std::pair<const char *, const std::vector<uint32_t> *>> items = {
       {"t_doc_off", &t.doc_off},   {"t_tile_start", &t.tile_start}, {"t_tile_doc", &t.tile_doc},
       {"t_tile_first", &t.tile_first}, {"t_doc_log2k", &t.doc_log2k}, {"t_doc_W", &t.doc_W},
-      {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0}};
+      {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0},
+      {"t_doc_ls", &t.doc_ls},     {"t_samp_off", &t.samp_off}};
   size_t total = 0;
   for (auto &it : items) total += (it.second->size() + 64) * 4;
   if (c->pinned_bytes < total) {
@@ -712,7 +845,7 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 template <typename K>
 int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
-               K **kout, uint32_t **vout) {
+               K **kout, uint32_t **vout, uint32_t *inv = nullptr) {
   auto &t = c->tab;
   uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * RADIX);
   if (!hist) return fail(c, "out of device memory (hist)");
@@ -743,10 +876,12 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scatter", tag);
     {
-      Launch L(c, nm, (double)N * (2 * sizeof(K) + (vi ? 8 : 4)) + (double)t.T * RADIX * 4);
+      const bool last = p + 1 == passes;
+      Launch L(c, nm, (double)N * (2 * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)) +
+                          (double)t.T * RADIX * 4);
       hipLaunchKernelGGL(k_radix_scatter<K>, dim3(t.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
                          ko, vo, dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
-                         dev_tab(c, "t_doc_off"), hist, shift, dmask);
+                         dev_tab(c, "t_doc_off"), hist, shift, dmask, last ? inv : nullptr);
     }
     if (check_launch(c, nm)) return -1;
     ki = ko;
@@ -806,6 +941,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
   uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
   const dim3 GT(t.T);
+  const dim3 TB(c->tb);
 
   if (N) {
     // 1. id sort
@@ -816,18 +952,28 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       return -1;
 
     // 2. join
+    uint64_t *samples = scratch_t<uint64_t>(c, "samples", t.Stot);
+    if (!samples) return fail(c, "out of device memory (samples)");
+    {
+      Launch L(c, "sample", (double)t.Stot * (64 + 8));
+      hipLaunchKernelGGL(k_sample, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
+                         dev_tab(c, "t_doc_ls"), dev_tab(c, "t_samp_off"), samples);
+    }
+    if (check_launch(c, "sample")) return -1;
     {
       Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1));
-      hipLaunchKernelGGL(k_join, GT, B256, 0, c->stream, skey, sval, cause_key, kind, tile_start,
-                         tile_doc, doc_off, par, skind, out->status);
+      hipLaunchKernelGGL(k_join, GT, TB, (size_t)t.Smax * 8 + c->join_lds, c->stream, skey, sval,
+                         cause_key, kind, samples,
+                         dev_tab(c, "t_samp_off"), dev_tab(c, "t_doc_ls"), tile_start, tile_doc,
+                         doc_off, par, skind, out->status);
     }
     if (check_launch(c, "join")) return -1;
 
     // 3. effective parent
     {
-      Launch L(c, "effparent", (double)N * (4 + 1 + 4 + 4));
-      hipLaunchKernelGGL(k_eff, GT, B256, 0, c->stream, par, skind, tile_start, tile_doc, doc_off,
-                         epar, ckA);
+      Launch L(c, "effparent", (double)N * (4 + 1 + 8 + 4 + 4));
+      hipLaunchKernelGGL(k_eff, GT, TB, 0, c->stream, par, skind, skey, out->status, tile_start,
+                         tile_doc, doc_off, epar, ckA);
     }
     if (check_launch(c, "effparent")) return -1;
 
@@ -843,13 +989,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
     {
       Launch L(c, "links", (double)N * (4 + 4 + 4 + 4));
-      hipLaunchKernelGGL(k_links, GT, B256, 0, c->stream, cks, cvs, tile_start, tile_doc, doc_off,
+      hipLaunchKernelGGL(k_links, GT, TB, 0, c->stream, cks, cvs, tile_start, tile_doc, doc_off,
                          nsc, fcS, fcN);
     }
     if (check_launch(c, "links")) return -1;
     {
       Launch L(c, "linkfinal", (double)N * (4 + 4 + 4 + 4 + 1 + 8));
-      hipLaunchKernelGGL(k_link_final, GT, B256, 0, c->stream, nsc, fcS, fcN, epar, skind,
+      hipLaunchKernelGGL(k_link_final, GT, TB, 0, c->stream, nsc, fcS, fcN, epar, skind,
                          tile_start, tile_doc, doc_off, doc_log2k, link);
     }
     if (check_launch(c, "linkfinal")) return -1;
@@ -857,16 +1003,18 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     // 6. Euler walk
     {
       Launch L(c, "walk", (double)N * (2 * 8 + 8));
-      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(WALK_THREADS), 0, c->stream, link,
+      auto kw = c->walk_nw >= 4 ? k_walk<4> : c->walk_nw == 2 ? k_walk<2> : k_walk<1>;
+      hipLaunchKernelGGL(kw, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream, link,
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
-                         doc_W, walk_first, loc, wcnt, wnext, out->status);
+                         doc_W, walk_first, loc, wcnt, wnext, out->status, c->walk_span);
     }
     if (check_launch(c, "walk")) return -1;
 
     // 7. rank sublists (+ max lamport-ts per document)
     {
       Launch L(c, "rank", (double)t.Wtot * 12);
-      hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, 0, c->stream, wcnt, wnext, walk_first,
+      hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
+                         wnext, walk_first,
                          doc_W, doc_off, skey, bt->ts_shift, sbase, out->max_ts, out->status);
     }
     if (check_launch(c, "rank")) return -1;
@@ -874,7 +1022,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     // 8. emit
     {
       Launch L(c, "emit", (double)N * (8 + 4 + 8 + 4 + 4 + 1));
-      hipLaunchKernelGGL(k_emit, GT, B256, 0, c->stream, loc, sval, link, sbase, walk_first, doc_W,
+      hipLaunchKernelGGL(k_emit, GT, TB, (size_t)t.Wmax * 4, c->stream, loc, sval, link, sbase, walk_first, doc_W,
                          tile_start, tile_doc, doc_off, out->weave_perm, vis8, out->visible_count,
                          out->status);
     }
@@ -1017,6 +1165,17 @@ int cw_ctx_create(int device, cw_ctx **out) {
     return -1;
   }
   c->stream = c->own_stream;
+  auto knob = [](const char *name, uint32_t dflt) {
+    const char *v = getenv(name);
+    return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
+  };
+  c->tb = knob("CW_TB", 1024);
+  c->walk_threads = knob("CW_WALK_THREADS", 512);
+  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 1024));
+  c->walk_lds = knob("CW_WALK_LDS", 0);
+  c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
+  c->walk_nw = knob("CW_WALK_NW", 1);
+  c->join_lds = knob("CW_JOIN_LDS", 0);
   *out = c;
   return 0;
 }

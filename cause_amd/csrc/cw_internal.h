@@ -13,11 +13,18 @@ constexpr uint32_t SORT_WAVES = SORT_THREADS / 64;
 constexpr uint32_t RADIX_BITS = 8;
 constexpr uint32_t RADIX = 1u << RADIX_BITS;
 
+// Join: per-document sample of the sorted ids (every 2^ls-th key, <= MAX_SAMPLES)
+// staged in LDS so the cause search touches global memory only at the end.
+constexpr uint32_t MAX_SAMPLES = 8192;             // 64 KiB of LDS
+constexpr uint32_t MIN_LOG2_STRIDE = 3;
+
 // Euler walk: one walker per splitter arc; <= MAX_SUBLISTS sublists per document
 // so the sublist ranking of a document fits one workgroup's LDS.
 constexpr uint32_t WALK_THREADS = 256;
-constexpr uint32_t MAX_SUBLISTS = 4096;
-constexpr uint32_t MIN_LOG2K = 6;                 // >= 64 nodes per splitter block
+constexpr uint32_t WALK_SPAN = 2048;              // walkers pulled by one workgroup
+constexpr uint32_t MAX_SUBLISTS = 16384;          // rank: 128 KiB of LDS
+constexpr uint32_t CHAIN = 64;                     // rank: sublists per LDS chain head
+constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter block
 
 // link word: low 32 = first child (bit 31: node renders, bit 30: node is a
 // splitter), high 32 = next arc after the node's up arc.
@@ -37,6 +44,14 @@ __device__ __forceinline__ bool is_hide(uint8_t k) {
 // Number of lanes below this one whose bit is set in m (wave64).
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Blocks b, b+8, b+16, ... are dealt to the same XCD (MI355X_MICROARCH.md,
+// "Workgroup dispatch").  Give each XCD a contiguous range of tiles so one
+// document's tiles share one L2; bijective for any grid size.  Speed only.
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
+  const uint32_t q = nb >> 3, r = nb & 7, x = b & 7;
+  return x * q + min(x, r) + (b >> 3);
 }
 
 __device__ __forceinline__ uint32_t mix32(uint32_t a, uint32_t b) {

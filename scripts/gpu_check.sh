@@ -1,0 +1,34 @@
+#!/bin/bash
+# Run on the GPU box (via gpurun): parity tests, bench, kernel-trace profile.
+#   scripts/gpu_check.sh [tests|bench|prof|pmc ...]   (default: tests bench prof)
+# Every GPU step has its own time limit; the first failure ends the script.
+set -e
+R="${GRAFT_REPO_ROOT:-$PWD}"
+cd "$R"
+mkdir -p gpurun_out
+steps="${*:-tests bench prof}"
+for s in $steps; do
+  case "$s" in
+    tests)
+      timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1 ;;
+    bench)
+      timeout -k 10 600 python bench.py --steps 5 --warmup 2 > gpurun_out/bench.log 2>&1 ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats \
+        --output-format csv -d "$R/gpurun_out/prof" -o run -- \
+        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu > "$R/gpurun_out/bench_prof.log" 2>&1) ;;
+    pmc)
+      # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes
+      for ctr in ${PMC_COUNTERS:-FETCH_SIZE WRITE_SIZE}; do
+        (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace \
+          --pmc "$ctr" --output-format csv -d "$R/gpurun_out/pmc_$ctr" -o run -- \
+          python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu ${PMC_BENCH_ARGS:-} > "$R/gpurun_out/pmc_$ctr.log" 2>&1)
+      done ;;
+    list)
+      (cd /tmp && rocprofv3 -L > "$R/gpurun_out/counters.txt" 2>&1) ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+  echo "step $s ok"
+done
