@@ -1,0 +1,200 @@
+"""Host-side mirror of the reference's list interface, with the weave on the GPU.
+
+Same names, argument meaning and errors as the reference (causal.collections.
+shared / list); a causal tree is a dict with the reference's ct keys
+(``nodes``, ``yarns``, ``weave``, ``lamport_ts``, ``site_id``, ``uuid``, ``type``).
+Every ``weave`` arity is a full reweave on the MI355X through the C ABI
+(cw_weave_lists) -- exact by SURVEY F7 (incremental insertion in any causal
+order equals the full reweave).  There is no CPU weave in this module.
+
+    shared.cljc:151-192   insert / append           -> insert, append
+    shared.cljc:259-266   refresh-caches            -> refresh_caches
+    list.cljc:20-34       weave (all arities)       -> list_weave / weave_lists
+    list.cljc:36-43       conj- / cons-             -> list_conj / list_cons
+    list.cljc:48-72       hide? / ->edn / ->list    -> causal_list_to_edn / _to_list
+"""
+from __future__ import annotations
+
+import random
+import threading
+
+import numpy as np
+
+from . import abi, pack
+
+
+class Keyword:
+    """A Clojure keyword ``:ns/name``."""
+
+    __slots__ = ("ns", "name")
+
+    def __init__(self, ns, name):
+        self.ns, self.name = ns, name
+
+    def __eq__(self, other):
+        return (getattr(other, "ns", None), getattr(other, "name", None)) == (self.ns, self.name) \
+            and hasattr(other, "ns")
+
+    def __hash__(self):
+        return hash(("kw", self.ns, self.name))
+
+    def __repr__(self):
+        return f":{self.ns}/{self.name}" if self.ns else f":{self.name}"
+
+
+HIDE = Keyword("causal", "hide")          # core.cljc:15
+H_HIDE = Keyword("causal", "h.hide")
+H_SHOW = Keyword("causal", "h.show")
+ROOT_ID = (0, "0", 0)                      # shared.cljc:22
+ROOT_NODE = (ROOT_ID, None, None)          # shared.cljc:23
+
+
+class CauseError(Exception):
+    """ex-info of the reference: ``causes`` is the :causes set."""
+
+    def __init__(self, msg, causes):
+        super().__init__(msg)
+        self.causes = causes
+
+
+_weaver = None
+_lock = threading.Lock()
+
+
+def weaver() -> abi.Weaver:
+    """The process-wide GPU context (device 0)."""
+    global _weaver
+    with _lock:
+        if _weaver is None:
+            _weaver = abi.Weaver(0)
+        return _weaver
+
+
+def new_node(ts, site, *rest):
+    """shared.cljc:77-84"""
+    if len(rest) == 2:
+        return ((ts, site, 0), rest[0], rest[1])
+    tx, cause, value = rest
+    return ((ts, site, tx), cause, value)
+
+
+def _uid(rng, n):
+    first = "ABCDEFGHIJKLMNOPQRSTUVWXYZ_abcdefghijklmnopqrstuvwxyz"
+    return rng.choice(first) + "".join(rng.choice("0123456789" + first) for _ in range(n - 1))
+
+
+def new_site_id(rng=random):
+    return _uid(rng, 13)
+
+
+def new_list_ct(site_id=None, uuid=None, rng=random):
+    """list.cljc:11-18"""
+    return {"type": "list", "lamport_ts": 0, "uuid": uuid or _uid(rng, 21),
+            "site_id": site_id or new_site_id(rng),
+            "nodes": {ROOT_ID: (None, None)}, "yarns": {"0": [ROOT_NODE]},
+            "weave": [ROOT_NODE], "_visible": [False]}
+
+
+def weave_lists(cts):
+    """Full reweave of many list cts in ONE GPU call (the batch entry point).
+    Returns new cts with ::weave, ::yarns, ::lamport-ts and rendered flags."""
+    docs = [[(i, b[0], b[1]) for i, b in ct["nodes"].items()] for ct in cts]
+    b = pack.pack_lists(docs)
+    res = weaver().weave_lists(b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    vis = res.visible()
+    out = []
+    for d, (ct, nodes) in enumerate(zip(cts, docs)):
+        lo, hi = int(b.offsets[d]), int(b.offsets[d + 1])
+        st = int(res.status[d])
+        if st & abi.STATUS_ORPHAN:
+            raise CauseError("The cause of this node is not in the tree.", {"cause-must-exist"})
+        if st:
+            raise CauseError(f"document outside the weave's domain (status {st})", {"weave-domain"})
+        new = dict(ct)
+        new["weave"] = [nodes[p] for p in res.weave_perm[lo:hi]]
+        new["_visible"] = [bool(v) for v in vis[lo:hi]]
+        yarns = {}
+        if res.yarn_perm is not None:
+            for p in res.yarn_perm[lo:hi]:
+                nd = nodes[p]
+                yarns.setdefault(nd[0][1], []).append(nd)
+        new["yarns"] = yarns
+        new["_max_ts"] = int(res.max_ts[d])
+        out.append(new)
+    return out
+
+
+def list_weave(ct, node=None, more=None):
+    """list.cljc:20-34 -- every arity is the full GPU reweave;
+    like the reference, a node that is not in ::nodes leaves ct unchanged."""
+    if node is not None and node[0] not in ct["nodes"]:
+        return ct
+    return weave_lists([ct])[0]
+
+
+def refresh_caches(weave_fn, ct):
+    """shared.cljc:259-266: yarns (spin), lamport-ts (refresh-ts) and the weave
+    all come from the one GPU call."""
+    out = weave_fn(ct)
+    out = dict(out)
+    out["lamport_ts"] = out.get("_max_ts", ct["lamport_ts"])
+    return out
+
+
+def insert(weave_fn, ct, node, more=None):
+    """shared.cljc:151-184 (same validations, same ex-info causes)."""
+    nodes = [node] + list(more or [])
+    if len({(n[0][0], n[0][1]) for n in nodes}) > 1:
+        raise CauseError("All nodes must belong to the same tx.", {"txs"})
+    existing = ct["nodes"].get(node[0])
+    if existing is not None:
+        if (node[1], node[2]) == existing:
+            return ct
+        raise CauseError("This node is already in the tree and can't be changed.",
+                         {"append-only", "edits-not-allowed"})
+    is_key = isinstance(node[1], (str, Keyword))
+    if not is_key and node[1] not in ct["nodes"]:
+        raise CauseError("The cause of this node is not in the tree.", {"cause-must-exist"})
+    out = dict(ct)
+    if node[0][0] > ct["lamport_ts"]:
+        out["lamport_ts"] = node[0][0]
+    nm = dict(ct["nodes"])
+    for n in nodes:
+        nm[n[0]] = (n[1], n[2])
+    out["nodes"] = nm
+    woven = weave_fn(out, node, more)
+    woven = dict(woven)
+    woven["lamport_ts"] = out["lamport_ts"]
+    return woven
+
+
+def append(weave_fn, ct, cause, value):
+    """shared.cljc:186-192"""
+    ct2 = dict(ct)
+    ct2["lamport_ts"] = ct["lamport_ts"] + 1
+    return insert(weave_fn, ct2, new_node(ct2["lamport_ts"], ct2["site_id"], cause, value))
+
+
+def list_conj(ct, v):
+    """list.cljc:36-40"""
+    return append(list_weave, ct, ct["weave"][-1][0], v)
+
+
+def list_cons(v, ct):
+    """list.cljc:42-43"""
+    return append(list_weave, ct, ROOT_ID, v)
+
+
+def causal_list_to_list(ct):
+    """list.cljc:68-72 (rendered flags from the GPU, hide? list.cljc:48-55)."""
+    return [n for n, v in zip(ct["weave"], ct["_visible"]) if v]
+
+
+def causal_list_to_edn(ct):
+    """list.cljc:57-66"""
+    return [n[2] for n in causal_list_to_list(ct)]
+
+
+def count(ct):
+    """list.cljc:77"""
+    return len(causal_list_to_list(ct))

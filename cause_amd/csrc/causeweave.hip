@@ -69,91 +69,80 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uin
 }
 
 // --- segmented LSD radix sort ------------------------------------------------
+// A pass sorts by one digit of <= MAX_DIGIT bits (<= 2048 bins).  Each tile is
+// first sorted by the digit inside LDS (two stable sub-passes of <= 6 bits:
+// wave ballots + per-wave counters), then written out as digit runs.
 template <typename K>
 __global__ __launch_bounds__(256) void k_radix_hist(const K *__restrict__ keys,
                                                     const uint32_t *__restrict__ tile_start,
-                                                    uint32_t shift, uint32_t dmask,
+                                                    uint32_t shift, uint32_t dbits,
                                                     uint32_t *__restrict__ hist) {
-  __shared__ uint32_t h[4][RADIX];
+  __shared__ uint32_t h[4][MAX_BINS];
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), tid = threadIdx.x, w = tid >> 6;
-  for (uint32_t i = tid; i < 4 * RADIX; i += 256) (&h[0][0])[i] = 0;
+  const uint32_t nb = 1u << dbits, dmask = nb - 1;
+  for (uint32_t i = tid; i < 4 * nb; i += 256) h[i / nb][i % nb] = 0;
   __syncthreads();
   const uint32_t s = tile_start[t], e = tile_start[t + 1];
   for (uint32_t i = s + tid; i < e; i += 256)
     atomicAdd(&h[w][(uint32_t)(keys[i] >> shift) & dmask], 1u);
   __syncthreads();
-  hist[(size_t)t * RADIX + tid] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+  for (uint32_t b = tid; b < nb; b += 256)
+    hist[(size_t)t * nb + b] = h[0][b] + h[1][b] + h[2][b] + h[3][b];
 }
 
 // Per document: turn the (tile, digit) counts into global output offsets,
-// digit-major then tile order (stable).
-__global__ __launch_bounds__(256) void k_radix_scan(uint32_t *__restrict__ hist,
-                                                    const uint32_t *__restrict__ tile_first,
-                                                    const uint32_t *__restrict__ doc_off) {
-  __shared__ uint32_t wtot[4];
-  const uint32_t d = blockIdx.x, b = threadIdx.x;
+// digit-major then tile order (stable).  1024 threads, <= 2 bins each.
+__global__ __launch_bounds__(1024) void k_radix_scan(uint32_t *__restrict__ hist,
+                                                     const uint32_t *__restrict__ tile_first,
+                                                     const uint32_t *__restrict__ doc_off,
+                                                     uint32_t dbits) {
+  __shared__ uint32_t wtot[16];
+  const uint32_t d = blockIdx.x, nb = 1u << dbits;
+  const uint32_t bpt = (nb + blockDim.x - 1) / blockDim.x;  // 1 or 2
+  const uint32_t b0 = threadIdx.x * bpt;
   const uint32_t t0 = tile_first[d], t1 = tile_first[d + 1];
   if (t0 == t1) return;  // empty document (uniform per block)
-  uint32_t tot = 0;
-  for (uint32_t t = t0; t < t1; t++) tot += hist[(size_t)t * RADIX + b];
-  uint32_t run = doc_off[d] + block_exscan<256>(tot, wtot, nullptr);
-  for (uint32_t t = t0; t < t1; t++) {
-    uint32_t c = hist[(size_t)t * RADIX + b];
-    hist[(size_t)t * RADIX + b] = run;
-    run += c;
-  }
+  uint32_t tot[2] = {0, 0};
+  for (uint32_t t = t0; t < t1; t++)
+    for (uint32_t k = 0; k < bpt; k++)
+      if (b0 + k < nb) tot[k] += hist[(size_t)t * nb + b0 + k];
+  uint32_t run[2];
+  run[0] = doc_off[d] + block_exscan<0>(tot[0] + tot[1], wtot, nullptr);
+  run[1] = run[0] + tot[0];
+  for (uint32_t t = t0; t < t1; t++)
+    for (uint32_t k = 0; k < bpt; k++)
+      if (b0 + k < nb) {
+        const uint32_t c = hist[(size_t)t * nb + b0 + k];
+        hist[(size_t)t * nb + b0 + k] = run[k];
+        run[k] += c;
+      }
 }
 
-// Stable scatter of one tile.  vals_in == nullptr means "value = doc-local
-// index of the element" (first pass).  Ranks inside the tile come from
-// wave-level digit matching (8 ballots) and per-wave digit counters in LDS;
-// the tile is reordered in LDS so the global writes are digit runs.
-template <typename K>
-__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
-    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
-    uint32_t *__restrict__ vals_out, const uint32_t *__restrict__ tile_start,
-    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
-    const uint32_t *__restrict__ offs, uint32_t shift, uint32_t dmask,
-    uint32_t *__restrict__ inv) {
-  __shared__ K skey[TILE];
-  __shared__ uint32_t sval[TILE];
-  __shared__ uint32_t wcnt[2][SORT_WAVES][RADIX];
-  __shared__ uint32_t run[RADIX], bstart[RADIX], soff[RADIX];
-  __shared__ uint32_t wtot[SORT_WAVES];
-
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), tid = threadIdx.x, w = tid >> 6;
-  const uint32_t s = tile_start[t], e = tile_start[t + 1];
-  const uint32_t len = e - s;
-  const uint32_t lbase = s - doc_off[tile_doc[t]];
-
-  if (tid < RADIX) {
-    run[tid] = 0;
-    soff[tid] = offs[(size_t)t * RADIX + tid];
-  }
-  for (uint32_t i = tid; i < SORT_WAVES * RADIX; i += SORT_THREADS) (&wcnt[0][0][0])[i] = 0;
+// Stable rank of SORT_ITEMS striped items per lane by a sub-digit of sbits
+// (<= 6) bits: returns each item's position inside the tile.
+__device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[SORT_ITEMS], uint32_t len,
+                                              uint32_t sbits, uint32_t (&pos)[SORT_ITEMS],
+                                              uint32_t (*wcnt)[SORT_WAVES][SUB_BINS],
+                                              uint32_t *run) {
+  const uint32_t tid = threadIdx.x, w = tid >> 6, nbin = 1u << sbits;
+  if (tid < SUB_BINS) run[tid] = 0;
+  for (uint32_t i = tid; i < SORT_WAVES * SUB_BINS; i += SORT_THREADS) (&wcnt[0][0][0])[i] = 0;
   __syncthreads();
-
-  K key[SORT_ITEMS];
-  uint32_t val[SORT_ITEMS], rk[SORT_ITEMS];
 #pragma unroll
   for (uint32_t k = 0; k < SORT_ITEMS; k++) {
-    const uint32_t j = k * SORT_THREADS + tid;
-    const bool valid = j < len;
-    key[k] = valid ? keys_in[s + j] : (K)0;
-    val[k] = valid ? (vals_in ? vals_in[s + j] : lbase + j) : 0u;
-    const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
+    const bool valid = k * SORT_THREADS + tid < len;
+    const uint32_t dd = sd[k];
     uint64_t m = __ballot(valid);
-#pragma unroll
-    for (uint32_t bit = 0; bit < RADIX_BITS; bit++) {
-      const bool on = (d >> bit) & 1u;
+    for (uint32_t bit = 0; bit < sbits; bit++) {
+      const bool on = (dd >> bit) & 1u;
       const uint64_t b = __ballot(on);
       m &= on ? b : ~b;
     }
     const uint32_t lr = lanes_below(m);
     const uint32_t buf = k & 1;
-    if (valid && lr == 0) wcnt[buf][w][d] = (uint32_t)__popcll(m);
+    if (valid && lr == 0) wcnt[buf][w][dd] = (uint32_t)__popcll(m);
     __syncthreads();
-    if (tid < RADIX) {
+    if (tid < nbin) {
       uint32_t r = run[tid];
 #pragma unroll
       for (uint32_t ww = 0; ww < SORT_WAVES; ww++) {
@@ -165,20 +154,106 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
       run[tid] = r;
     }
     __syncthreads();
-    rk[k] = valid ? wcnt[buf][w][d] + lr : 0u;
+    pos[k] = valid ? wcnt[buf][w][dd] + lr : 0u;
   }
-  uint32_t cnt = tid < RADIX ? run[tid] : 0u;
-  uint32_t ex = block_exscan<SORT_THREADS>(cnt, wtot, nullptr);
-  if (tid < RADIX) bstart[tid] = ex;
+  // bin starts (64 bins: one wave)
+  if (tid < 64) {
+    const uint32_t v = tid < nbin ? run[tid] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (tid >= (uint32_t)o) x += y;
+    }
+    run[tid] = x - v;
+  }
   __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < SORT_ITEMS; k++) pos[k] += run[sd[k]];
+  __syncthreads();
+}
+
+// Stable scatter of one tile by digit (key >> shift) & (2^dbits - 1).
+// vals_in == nullptr means "value = doc-local index of the element".
+// inv != nullptr (last pass only) also records each input node's rank.
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
+    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ offs, uint32_t shift, uint32_t dbits, uint32_t sub0,
+    uint32_t *__restrict__ inv) {
+  __shared__ K skey[TILE];
+  __shared__ uint32_t sval[TILE];
+  __shared__ uint32_t soff[MAX_BINS], bstart[MAX_BINS];
+  __shared__ uint32_t wcnt[2][SORT_WAVES][SUB_BINS];
+  __shared__ uint32_t run[64];
+  __shared__ uint32_t wtot[SORT_WAVES];
+
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), tid = threadIdx.x;
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  const uint32_t len = e - s;
+  const uint32_t lbase = s - doc_off[tile_doc[t]];
+  const uint32_t nb = 1u << dbits, dmask = nb - 1;
+
+  for (uint32_t b = tid; b < nb; b += SORT_THREADS) {
+    soff[b] = offs[(size_t)t * nb + b];
+    bstart[b] = 0;
+  }
+  __syncthreads();
+  K key[SORT_ITEMS];
+  uint32_t val[SORT_ITEMS], sd[SORT_ITEMS], pos[SORT_ITEMS];
 #pragma unroll
   for (uint32_t k = 0; k < SORT_ITEMS; k++) {
     const uint32_t j = k * SORT_THREADS + tid;
-    if (j < len) {
-      const uint32_t d = (uint32_t)(key[k] >> shift) & dmask;
-      const uint32_t p = bstart[d] + rk[k];
-      skey[p] = key[k];
-      sval[p] = val[k];
+    const bool valid = j < len;
+    key[k] = valid ? keys_in[s + j] : (K)0;
+    val[k] = valid ? (vals_in ? vals_in[s + j] : lbase + j) : 0u;
+    const uint32_t dg = (uint32_t)(key[k] >> shift) & dmask;
+    if (valid) atomicAdd(&bstart[dg], 1u);
+    sd[k] = dg & ((1u << sub0) - 1);
+  }
+  // sub-pass A: low sub-digit
+  rank_subdigit(sd, len, sub0, pos, wcnt, run);
+  const uint32_t sub1 = dbits - sub0;
+  if (sub1 > 0) {
+#pragma unroll
+    for (uint32_t k = 0; k < SORT_ITEMS; k++)
+      if (k * SORT_THREADS + tid < len) {
+        skey[pos[k]] = key[k];
+        sval[pos[k]] = val[k];
+      }
+    __syncthreads();
+    // sub-pass B: high sub-digit, over the tile in sub-pass A order
+#pragma unroll
+    for (uint32_t k = 0; k < SORT_ITEMS; k++) {
+      const uint32_t j = k * SORT_THREADS + tid;
+      if (j < len) {
+        key[k] = skey[j];
+        val[k] = sval[j];
+      }
+      sd[k] = ((uint32_t)(key[k] >> shift) & dmask) >> sub0;
+    }
+    rank_subdigit(sd, len, sub1, pos, wcnt, run);
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < SORT_ITEMS; k++)
+    if (k * SORT_THREADS + tid < len) {
+      skey[pos[k]] = key[k];
+      sval[pos[k]] = val[k];
+    }
+  // digit starts inside the tile
+  {
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;  // <= 4 bins per lane (2048 / 512)
+    const uint32_t b0 = tid * 4;
+    if (b0 < nb) { c0 = bstart[b0]; c1 = bstart[b0 + 1]; c2 = bstart[b0 + 2]; c3 = bstart[b0 + 3]; }
+    if (nb < 4 && b0 < nb) { c1 = nb > 1 ? c1 : 0; c2 = nb > 2 ? c2 : 0; c3 = 0; }
+    const uint32_t ex = block_exscan<SORT_THREADS>(c0 + c1 + c2 + c3, wtot, nullptr);
+    if (b0 < nb) {
+      bstart[b0] = ex;
+      if (b0 + 1 < nb) bstart[b0 + 1] = ex + c0;
+      if (b0 + 2 < nb) bstart[b0 + 2] = ex + c0 + c1;
+      if (b0 + 3 < nb) bstart[b0 + 3] = ex + c0 + c1 + c2;
     }
   }
   __syncthreads();
@@ -371,105 +446,82 @@ __global__ __launch_bounds__(1024) void k_link_final(
 // Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
 // splitter block lw/2's splitter node and follows the tour until the next
 // splitter arc.  Every down arc it crosses gets (walker, local count).
-// Each lane advances NW walkers in lock-step so NW independent link loads are
-// in flight per lane (the walk is a pointer chase: latency, not bandwidth).
-template <int NW>
+// Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
+// splitter block lw/2's splitter node and follows the tour to the next splitter
+// arc.  The down arcs it crosses (node rank | renders << 31) are appended to its
+// sublist's slot of `cap` entries; a full slot continues as a new sublist
+// (id >= W, from a per-document counter), so slots are written sequentially
+// by one lane and no per-node scatter is needed.
 __global__ __launch_bounds__(1024) void k_walk(
     const uint64_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
     const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
-    const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_W,
-    const uint32_t *__restrict__ walk_first, uint64_t *__restrict__ loc,
-    uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext, uint32_t *__restrict__ status,
-    uint32_t walk_span) {
+    const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_log2cap,
+    const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ doc_Wcap,
+    const uint32_t *__restrict__ walk_first, const uint64_t *__restrict__ slot_first,
+    uint32_t *__restrict__ slots, uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext,
+    uint32_t *__restrict__ dyn_ctr, uint32_t *__restrict__ status, uint32_t walk_span) {
   __shared__ uint32_t next_walker;
   const uint32_t b = xcd_tile(blockIdx.x, gridDim.x), d = wblk_doc[b];
-  const uint32_t w0 = wblk_w0[b], w1 = min(w0 + walk_span, doc_W[d]);
+  const uint32_t W = doc_W[d], Wcap = doc_Wcap[d];
+  const uint32_t w0 = wblk_w0[b], w1 = min(w0 + walk_span, W);
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  const uint32_t log2cap = doc_log2cap[d], cap = 1u << log2cap;
   const uint32_t f = walk_first[d];
+  uint32_t *const sl = slots + slot_first[d];
   const uint32_t max_steps = 2 * n + 2;
-  if (threadIdx.x == 0) next_walker = w0 + blockDim.x * NW;
+  if (threadIdx.x == 0) next_walker = w0 + blockDim.x;
   __syncthreads();
-
-  // slot state: 0 idle, 1 starting (load link of v), 2 running (load link of u)
-  uint32_t st[NW], lw[NW], v[NW], dir[NW], cnt[NW], u[NW], nd[NW], steps[NW];
-  uint64_t L[NW];
-  auto start = [&](int k, uint32_t id) {
-    lw[k] = id;
-    v[k] = split_node(d, id >> 1, log2k, n);
-    dir[k] = id & 1;
-    cnt[k] = 0;
-    steps[k] = 0;
-    if (dir[k] == 0) {
-      loc[base + v[k]] = (uint64_t)id << 32;
-      cnt[k] = 1;
+  for (uint32_t lw = w0 + threadIdx.x; lw < w1; lw = atomicAdd(&next_walker, 1u)) {
+    uint32_t v = split_node(d, lw >> 1, log2k, n);
+    uint32_t dir = lw & 1;  // 0 = down, 1 = up
+    uint32_t x = lw, cnt = 0, nextsub = NX_END;
+    uint64_t L = link[base + v];
+    if (dir == 0) {
+      sl[(size_t)x << log2cap] = v | ((uint32_t)L & LINK_VIS);
+      cnt = 1;
     }
-    st[k] = 1;
-  };
-  auto finish = [&](int k, uint32_t nextsub) {
-    wcnt[f + lw[k]] = cnt[k];
-    wnext[f + lw[k]] = nextsub;
-    const uint32_t id = atomicAdd(&next_walker, 1u);
-    if (id < w1) start(k, id);
-    else st[k] = 0;
-  };
-#pragma unroll
-  for (int k = 0; k < NW; k++) {
-    const uint32_t id = w0 + threadIdx.x + k * blockDim.x;
-    st[k] = 0;
-    if (id < w1) start(k, id);
-  }
-  for (;;) {
-    bool any = false;
-    // A: next arc of each running walker
-#pragma unroll
-    for (int k = 0; k < NW; k++) {
-      if (st[k] == 2) {
-        if (dir[k] == 0) {
-          const uint32_t fc = (uint32_t)L[k] & LINK_IDX;
-          if (fc) { u[k] = fc; nd[k] = 0; }
-          else { u[k] = v[k]; nd[k] = 1; }
-        } else {
-          const uint32_t nx = (uint32_t)(L[k] >> 32);
-          if (nx == NX_END) finish(k, NX_END);
-          else if (nx & NX_UP) { u[k] = nx & ~NX_UP; nd[k] = 1; }
-          else { u[k] = nx; nd[k] = 0; }
-        }
+    for (uint32_t steps = 0;; steps++) {
+      uint32_t u, nd;
+      if (dir == 0) {
+        const uint32_t fc = (uint32_t)L & LINK_IDX;
+        if (fc) { u = fc; nd = 0; }
+        else { u = v; nd = 1; }
+      } else {
+        const uint32_t nx = (uint32_t)(L >> 32);
+        if (nx == NX_END) break;
+        if (nx & NX_UP) { u = nx & ~NX_UP; nd = 1; }
+        else { u = nx; nd = 0; }
       }
-      any |= st[k] != 0;
-    }
-    if (!any) break;
-    // B: independent loads
-    uint64_t X[NW];
-#pragma unroll
-    for (int k = 0; k < NW; k++) {
-      X[k] = L[k];
-      if (st[k] == 1) X[k] = link[base + v[k]];
-      else if (st[k] == 2 && u[k] != v[k]) X[k] = link[base + u[k]];
-    }
-    // C: advance
-#pragma unroll
-    for (int k = 0; k < NW; k++) {
-      if (st[k] == 1) {
-        L[k] = X[k];
-        st[k] = 2;
-      } else if (st[k] == 2) {
-        if ((uint32_t)X[k] & LINK_SPLIT) {
-          finish(k, ((u[k] >> log2k) << 1) | nd[k]);
-        } else {
-          if (nd[k] == 0) {
-            loc[base + u[k]] = ((uint64_t)lw[k] << 32) | cnt[k];
-            cnt[k]++;
-          }
-          v[k] = u[k];
-          dir[k] = nd[k];
-          L[k] = X[k];
-          if (++steps[k] > max_steps) {
+      const uint64_t Lu = (u == v) ? L : link[base + u];
+      if ((uint32_t)Lu & LINK_SPLIT) {
+        nextsub = ((u >> log2k) << 1) | nd;
+        break;
+      }
+      if (nd == 0) {
+        if (cnt == cap) {  // slot full: continue as a new sublist
+          const uint32_t y = W + atomicAdd(&dyn_ctr[d], 1u);
+          if (y >= Wcap) {
             atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
-            finish(k, NX_END);
+            break;
           }
+          wcnt[f + x] = cap;
+          wnext[f + x] = y;
+          x = y;
+          cnt = 0;
         }
+        sl[((size_t)x << log2cap) + cnt] = u | ((uint32_t)Lu & LINK_VIS);
+        cnt++;
+      }
+      v = u;
+      dir = nd;
+      L = Lu;
+      if (steps > max_steps) {
+        atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+        break;
       }
     }
+    wcnt[f + x] = cnt;
+    wnext[f + x] = nextsub;
   }
 }
 
@@ -482,6 +534,7 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               const uint32_t *__restrict__ wnext,
                                               const uint32_t *__restrict__ walk_first,
                                               const uint32_t *__restrict__ doc_W,
+                                              const uint32_t *__restrict__ dyn_ctr,
                                               const uint32_t *__restrict__ doc_off,
                                               const uint64_t *__restrict__ skey, uint32_t ts_shift,
                                               uint32_t *__restrict__ sbase,
@@ -491,7 +544,8 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
   __shared__ uint32_t ch_next[MAX_SUBLISTS / CHAIN], ch_sum[MAX_SUBLISTS / CHAIN];
   __shared__ uint32_t ch_base[MAX_SUBLISTS / CHAIN];
   __shared__ uint32_t bad_s;
-  const uint32_t d = blockIdx.x, W = doc_W[d], f = walk_first[d];
+  const uint32_t d = blockIdx.x, f = walk_first[d];
+  const uint32_t W = min(doc_W[d] + dyn_ctr[d], walk_first[d + 1] - f);  // static + continued
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   if (threadIdx.x == 0 && max_ts) max_ts[d] = n ? (skey[base + n - 1] >> ts_shift) : 0ull;
   if (W == 0) return;
@@ -534,32 +588,43 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
     sbase[f + i] = ch_base[min(nx[i], C - 1)] + val[i];
 }
 
-// --- emit: rank order -> weave order -------------------------------------------
-__global__ __launch_bounds__(1024) void k_emit(
-    const uint64_t *__restrict__ loc, const uint32_t *__restrict__ sval,
-    const uint64_t *__restrict__ link, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ walk_first, const uint32_t *__restrict__ doc_W,
-    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
-    const uint32_t *__restrict__ doc_off, uint32_t *__restrict__ perm,
-    uint8_t *__restrict__ vis8, uint32_t *__restrict__ vcount, uint32_t *__restrict__ status) {
-  __shared__ uint32_t wtot[16];
-  extern __shared__ __attribute__((aligned(16))) uint32_t sb[];  // walker bases of doc d
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
-  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d], W = doc_W[d];
-  for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) sb[j] = sbase[f + j];
-  __syncthreads();
+// --- emit: sublist slots -> weave order ------------------------------------------
+// Entry k of sublist x is the node at weave position sbase[x] + k.  One lane
+// per sublist (its slot is contiguous); a block covers 256 consecutive
+// sublists of one document.
+__global__ __launch_bounds__(256) void k_emit(
+    const uint32_t *__restrict__ slots, const uint64_t *__restrict__ slot_first,
+    const uint32_t *__restrict__ wcnt, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ sval, const uint32_t *__restrict__ eblk_doc,
+    const uint32_t *__restrict__ eblk_x0, const uint32_t *__restrict__ walk_first,
+    const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ dyn_ctr,
+    const uint32_t *__restrict__ doc_log2cap, const uint32_t *__restrict__ doc_off,
+    uint32_t *__restrict__ perm, uint8_t *__restrict__ vis8, uint32_t *__restrict__ vcount,
+    uint32_t *__restrict__ status) {
+  __shared__ uint32_t wtot[4];
+  const uint32_t b = xcd_tile(blockIdx.x, gridDim.x), d = eblk_doc[b];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d];
+  const uint32_t Weff = min(doc_W[d] + dyn_ctr[d], walk_first[d + 1] - f);
+  const uint32_t log2cap = doc_log2cap[d];
+  const uint32_t x = eblk_x0[b] + threadIdx.x;
   uint32_t nvis = 0;
   bool bad = false;
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint64_t L = loc[i];
-    const uint32_t lw = (uint32_t)(L >> 32);
-    if (lw >= W) { bad = true; continue; }
-    const uint32_t pos = sb[lw] + (uint32_t)L;
-    if (pos >= n) { bad = true; continue; }
-    const uint32_t v = ((uint32_t)link[i] & LINK_VIS) ? 1u : 0u;
-    perm[base + pos] = sval[i];
-    vis8[base + pos] = (uint8_t)v;
-    nvis += v;
+  if (x < Weff) {
+    const uint32_t cnt = wcnt[f + x], p0 = sbase[f + x];
+    const uint32_t *sl = slots + slot_first[d] + ((size_t)x << log2cap);
+    if (p0 + cnt > n || cnt > (1u << log2cap)) {
+      bad = true;
+    } else {
+      for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t e = sl[k];
+        const uint32_t r = e & LINK_IDX;
+        if (r >= n) { bad = true; continue; }
+        const uint32_t v = e >> 31;
+        perm[base + p0 + k] = sval[base + r];
+        vis8[base + p0 + k] = (uint8_t)v;
+        nvis += v;
+      }
+    }
   }
   if (bad) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
   uint32_t total;
@@ -637,13 +702,15 @@ struct cw_ctx {
   std::vector<uint64_t> last_off;
   struct Tables {
     std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
-        wblk_doc, wblk_w0, doc_ls, samp_off;
-    uint32_t T = 0, Wtot = 0, Bw = 0, nmax = 0, Stot = 0, Wmax = 0, Smax = 0;
+        wblk_doc, wblk_w0, doc_ls, samp_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0;
+    std::vector<uint64_t> slot_first;
+    uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Stot = 0, Wmax = 0, Smax = 0;
+    uint64_t slots = 0;
   } tab;
   bool tab_on_device = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
   uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
-           walk_nw = 1, join_lds = 0;
+           join_lds = 0, max_digit = MAX_DIGIT, min_log2cap = 4;
 };
 
 namespace {
@@ -719,6 +786,9 @@ struct Launch {
   }
 };
 
+// HSA dispatch packets carry the grid size in work-items as 32 bits.
+bool grid_ok(uint64_t blocks, uint64_t threads) { return blocks * threads < (1ull << 32); }
+
 int check_launch(cw_ctx *c, const char *what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(c, "launch %s: %s", what, hipGetErrorString(e));
@@ -760,6 +830,12 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.walk_first.resize(D + 1);
   t.wblk_doc.clear();
   t.wblk_w0.clear();
+  t.eblk_doc.clear();
+  t.eblk_x0.clear();
+  t.doc_log2cap.resize(D);
+  t.doc_Wcap.resize(D);
+  t.slot_first.resize(D + 1);
+  uint64_t slots = 0;
   t.doc_ls.resize(D);
   t.samp_off.resize(D + 1);
   uint32_t wtot = 0, stot = 0;
@@ -775,19 +851,37 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
       t.tile_start.push_back(b + s);
       t.tile_doc.push_back((uint32_t)d);
     }
-    // splitter block size K = 2^log2k, at most MAX_SUBLISTS/2 splitters per doc
-    uint32_t log2k = std::max(c->min_log2k, ceil_log2((n + MAX_SUBLISTS / 2 - 1) / (MAX_SUBLISTS / 2)));
+    // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
+    // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
+    uint32_t log2k = c->min_log2k, log2cap = std::max(log2k + 1, c->min_log2cap);
+    auto subl = [&]() {
+      return 2 * (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
+             (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
+    };
+    while (subl() > MAX_SUBLISTS) {
+      if (log2k + 1 < log2cap) log2k++;
+      else log2cap++;
+    }
     const uint32_t S = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;
     const uint32_t W = 2 * S;
+    const uint32_t Wcap = n ? (uint32_t)subl() : 0;
     t.doc_log2k[d] = log2k;
+    t.doc_log2cap[d] = log2cap;
     t.doc_W[d] = W;
-    t.Wmax = std::max(t.Wmax, W);
+    t.doc_Wcap[d] = Wcap;
+    t.Wmax = std::max(t.Wmax, Wcap);
     t.walk_first[d] = wtot;
+    t.slot_first[d] = slots;
+    slots += (uint64_t)Wcap << log2cap;
     for (uint32_t w0 = 0; w0 < W; w0 += c->walk_span) {
       t.wblk_doc.push_back((uint32_t)d);
       t.wblk_w0.push_back(w0);
     }
-    wtot += W;
+    for (uint32_t x0 = 0; x0 < Wcap; x0 += 256) {
+      t.eblk_doc.push_back((uint32_t)d);
+      t.eblk_x0.push_back(x0);
+    }
+    wtot += Wcap;
     // join samples: every 2^ls-th sorted id, at most MAX_SAMPLES per document
     const uint32_t ls =
         std::max(MIN_LOG2_STRIDE, ceil_log2((n + MAX_SAMPLES - 1) / MAX_SAMPLES));
@@ -800,6 +894,9 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.doc_off[D] = (uint32_t)off[D];
   t.tile_first[D] = (uint32_t)t.tile_start.size();
   t.walk_first[D] = wtot;
+  t.slot_first[D] = slots;
+  t.slots = slots;
+  t.Be = (uint32_t)t.eblk_doc.size();
   t.samp_off[D] = stot;
   t.Stot = stot;
   t.T = (uint32_t)t.tile_doc.size();
@@ -814,8 +911,10 @@ int upload_tables(cw_ctx *c) {
       {"t_doc_off", &t.doc_off},   {"t_tile_start", &t.tile_start}, {"t_tile_doc", &t.tile_doc},
       {"t_tile_first", &t.tile_first}, {"t_doc_log2k", &t.doc_log2k}, {"t_doc_W", &t.doc_W},
       {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0},
-      {"t_doc_ls", &t.doc_ls},     {"t_samp_off", &t.samp_off}};
-  size_t total = 0;
+      {"t_doc_ls", &t.doc_ls},     {"t_samp_off", &t.samp_off}, {"t_doc_log2cap", &t.doc_log2cap},
+      {"t_doc_Wcap", &t.doc_Wcap}, {"t_eblk_doc", &t.eblk_doc}, {"t_eblk_x0", &t.eblk_x0}};
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still be read
+  size_t total = (t.slot_first.size() + 64) * 8;
   for (auto &it : items) total += (it.second->size() + 64) * 4;
   if (c->pinned_bytes < total) {
     if (c->pinned) (void)hipHostFree(c->pinned);
@@ -834,56 +933,69 @@ int upload_tables(cw_ctx *c) {
     }
     p += (it.second->size() + 64) * 4;
   }
+  {
+    size_t bytes = t.slot_first.size() * 8;
+    void *dst = scratch(c, "t_slot_first", bytes);
+    if (!dst) return fail(c, "out of device memory (t_slot_first)");
+    memcpy(p, t.slot_first.data(), bytes);
+    HIPCHK(c, hipMemcpyAsync(dst, p, bytes, hipMemcpyHostToDevice, c->stream));
+  }
   return 0;
 }
 
 uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name].p; }
 
-// One segmented radix sort over key bits [shift0, shift0+bits) (LSD, RADIX_BITS
-// per pass, at least one pass).  Pass 0 reads (kin, vin) -- vin == nullptr means
-// identity values -- and the passes ping-pong between (kA,vA) and (kB,vB).
+// One segmented radix sort over key bits [shift0, shift0+bits): LSD passes of
+// <= MAX_DIGIT bits (at least one pass).  Pass 0 reads (kin, vin) -- vin ==
+// nullptr means identity values -- and the passes ping-pong between (kA,vA)
+// and (kB,vB).
 template <typename K>
 int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
                K **kout, uint32_t **vout, uint32_t *inv = nullptr) {
   auto &t = c->tab;
-  uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * RADIX);
+  if (bits == 0) bits = 1;
+  const uint32_t maxd = std::min<uint32_t>(c->max_digit, MAX_DIGIT);
+  const int passes = (int)((bits + maxd - 1) / maxd);
+  uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * (1u << ((bits + passes - 1) / passes)));
   if (!hist) return fail(c, "out of device memory (hist)");
-  const int passes = std::max(1, (int)((bits + RADIX_BITS - 1) / RADIX_BITS));
   const K *ki = kin;
   const uint32_t *vi = vin;
   K *ko = kA;
   uint32_t *vo = vA;
   char nm[48];
   const uint32_t D = (uint32_t)(t.doc_off.size() - 1);
+  uint32_t shift = shift0;
   for (int p = 0; p < passes; p++) {
-    const uint32_t shift = shift0 + p * RADIX_BITS;
-    const uint32_t left = bits > p * RADIX_BITS ? bits - p * RADIX_BITS : 1;
-    const uint32_t dmask = left >= RADIX_BITS ? RADIX - 1 : (1u << left) - 1;
+    const uint32_t dbits = bits / passes + ((uint32_t)p < bits % passes ? 1u : 0u);
+    const uint32_t nb = 1u << dbits;
+    const uint32_t sub0 = dbits <= SUB_BITS ? dbits : (dbits + 1) / 2;
     snprintf(nm, sizeof nm, "%s_hist", tag);
     {
-      Launch L(c, nm, (double)N * sizeof(K) + (double)t.T * RADIX * 4);
+      Launch L(c, nm, (double)N * sizeof(K) + (double)t.T * nb * 4);
       hipLaunchKernelGGL(k_radix_hist<K>, dim3(t.T), dim3(256), 0, c->stream, ki,
-                         dev_tab(c, "t_tile_start"), shift, dmask, hist);
+                         dev_tab(c, "t_tile_start"), shift, dbits, hist);
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scan", tag);
     {
-      Launch L(c, nm, (double)t.T * RADIX * 8);
-      hipLaunchKernelGGL(k_radix_scan, dim3(D), dim3(256), 0, c->stream, hist,
-                         dev_tab(c, "t_tile_first"), dev_tab(c, "t_doc_off"));
+      Launch L(c, nm, (double)t.T * nb * 8);
+      hipLaunchKernelGGL(k_radix_scan, dim3(D), dim3(1024), 0, c->stream, hist,
+                         dev_tab(c, "t_tile_first"), dev_tab(c, "t_doc_off"), dbits);
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scatter", tag);
     {
       const bool last = p + 1 == passes;
       Launch L(c, nm, (double)N * (2 * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)) +
-                          (double)t.T * RADIX * 4);
+                          (double)t.T * nb * 4);
       hipLaunchKernelGGL(k_radix_scatter<K>, dim3(t.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
                          ko, vo, dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
-                         dev_tab(c, "t_doc_off"), hist, shift, dmask, last ? inv : nullptr);
+                         dev_tab(c, "t_doc_off"), hist, shift, dbits, sub0,
+                         last ? inv : nullptr);
     }
     if (check_launch(c, nm)) return -1;
+    shift += dbits;
     ki = ko;
     vi = vo;
     ko = (ko == kA) ? kB : kA;
@@ -914,8 +1026,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     hipLaunchKernelGGL(k_or_reduce, dim3(1024), B256, 0, c->stream, id_key, N, red);
     if (check_launch(c, "or_reduce")) return -1;
     unsigned long long v = 0;
-    HIPCHK(c, hipMemcpyAsync(&v, red, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(&v, red, 8, hipMemcpyDeviceToHost));
     key_bits = v ? 64 - __builtin_clzll(v) : 1;
   }
   if (key_bits > 64) key_bits = 64;
@@ -928,13 +1040,15 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *cvA = scratch_t<uint32_t>(c, "cvA", N), *cvB = scratch_t<uint32_t>(c, "cvB", N);
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
-  uint64_t *link = scratch_t<uint64_t>(c, "link", N), *loc = scratch_t<uint64_t>(c, "loc", N);
+  uint64_t *link = scratch_t<uint64_t>(c, "link", N);
+  uint32_t *slots = scratch_t<uint32_t>(c, "slots", t.slots);
+  uint32_t *dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
   uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
   uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
   uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
   uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
   if (!skA || !skB || !svA || !svB || !par || !epar || !skind || !ckA || !ckB || !cvA || !cvB ||
-      !nsc || !fcS || !fcN || !link || !loc || !vis8 || !wcnt || !wnext || !sbase)
+      !nsc || !fcS || !fcN || !link || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase)
     return fail(c, "out of device memory (N=%u)", N);
 
   uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc");
@@ -942,6 +1056,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
   const dim3 GT(t.T);
   const dim3 TB(c->tb);
+  if (!grid_ok(t.T, std::max(c->tb, SORT_THREADS)) || !grid_ok(t.Bw, c->walk_threads) ||
+      !grid_ok(t.Be, 256) || !grid_ok(D, 1024))
+    return fail(c, "batch too large for one dispatch (split the batch)");
 
   if (N) {
     // 1. id sort
@@ -1001,12 +1118,14 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (check_launch(c, "linkfinal")) return -1;
 
     // 6. Euler walk
+    HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
     {
-      Launch L(c, "walk", (double)N * (2 * 8 + 8));
-      auto kw = c->walk_nw >= 4 ? k_walk<4> : c->walk_nw == 2 ? k_walk<2> : k_walk<1>;
-      hipLaunchKernelGGL(kw, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream, link,
+      Launch L(c, "walk", (double)N * (2 * 8 + 4));
+      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream, link,
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
-                         doc_W, walk_first, loc, wcnt, wnext, out->status, c->walk_span);
+                         dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
+                         out->status, c->walk_span);
     }
     if (check_launch(c, "walk")) return -1;
 
@@ -1014,17 +1133,19 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     {
       Launch L(c, "rank", (double)t.Wtot * 12);
       hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
-                         wnext, walk_first,
-                         doc_W, doc_off, skey, bt->ts_shift, sbase, out->max_ts, out->status);
+                         wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, bt->ts_shift, sbase,
+                         out->max_ts, out->status);
     }
     if (check_launch(c, "rank")) return -1;
 
     // 8. emit
     {
-      Launch L(c, "emit", (double)N * (8 + 4 + 8 + 4 + 4 + 1));
-      hipLaunchKernelGGL(k_emit, GT, TB, (size_t)t.Wmax * 4, c->stream, loc, sval, link, sbase, walk_first, doc_W,
-                         tile_start, tile_doc, doc_off, out->weave_perm, vis8, out->visible_count,
-                         out->status);
+      Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
+      hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, sval,
+                         dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
+                         dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
+                         out->visible_count, out->status);
     }
     if (check_launch(c, "emit")) return -1;
 
@@ -1044,7 +1165,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       uint64_t *ykA = skey == skA ? skB : skA;
       uint32_t *yvA = sval == svA ? svB : svA;
       // (skey, sval) stay intact: ping-pong through the free id buffers + link/loc
-      if (radix_sort<uint64_t>(c, "yarns", skey, sval, ykA, yvA, loc, nsc, bt->site_bits,
+      if (radix_sort<uint64_t>(c, "yarns", skey, sval, ykA, yvA, link, nsc, bt->site_bits,
                                bt->site_shift, N, &yk, &yv))
         return -1;
       HIPCHK(c, hipMemcpyAsync(out->yarn_perm, yv, (size_t)N * 4, hipMemcpyDeviceToDevice,
@@ -1100,10 +1221,13 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
         (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
         (res->yarn_perm && !dres.yarn_perm))
       return fail(c, "out of device memory (host-mode staging)");
+    // Pageable host memory: blocking copies (hipMemcpyAsync from/to pageable
+    // memory is not reliably ordered by a later stream synchronize).
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     if (N) {
-      HIPCHK(c, hipMemcpyAsync(did, id, (size_t)N * 8, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(dk, kind, N, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpy(did, id, (size_t)N * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
     }
     id = did;
     cause = dca;
@@ -1112,30 +1236,27 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   if (weave_lists_device(c, bt, id, cause, kind, &dres)) return -1;
 
   if (memspace == CW_MEM_HOST) {
-    HIPCHK(c, hipMemcpyAsync(res->weave_perm, dres.weave_perm, (size_t)N * 4,
-                             hipMemcpyDeviceToHost, c->stream));
-    if (res->visible_bits)
-      HIPCHK(c, hipMemcpyAsync(res->visible_bits, dres.visible_bits, ((size_t)N + 31) / 32 * 4,
-                               hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(res->visible_count, dres.visible_count, D * 4, hipMemcpyDeviceToHost,
-                             c->stream));
-    if (res->max_ts)
-      HIPCHK(c, hipMemcpyAsync(res->max_ts, dres.max_ts, D * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(res->status, dres.status, D * 4, hipMemcpyDeviceToHost, c->stream));
-    if (res->yarn_perm)
-      HIPCHK(c, hipMemcpyAsync(res->yarn_perm, dres.yarn_perm, (size_t)N * 4,
-                               hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(res->weave_perm, dres.weave_perm, (size_t)N * 4, hipMemcpyDeviceToHost));
+    if (res->visible_bits)
+      HIPCHK(c, hipMemcpy(res->visible_bits, dres.visible_bits, ((size_t)N + 31) / 32 * 4,
+                          hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->visible_count, dres.visible_count, D * 4, hipMemcpyDeviceToHost));
+    if (res->max_ts)
+      HIPCHK(c, hipMemcpy(res->max_ts, dres.max_ts, D * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->status, dres.status, D * 4, hipMemcpyDeviceToHost));
+    if (res->yarn_perm)
+      HIPCHK(c, hipMemcpy(res->yarn_perm, dres.yarn_perm, (size_t)N * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipDeviceSynchronize());
     // documents with no nodes have no root
     for (uint64_t d = 0; d < D; d++)
       if (bt->doc_offsets[d + 1] == bt->doc_offsets[d]) res->status[d] |= CW_STATUS_ROOT;
   } else {
     // empty documents: set the ROOT bit on the device
     for (uint64_t d = 0; d < D; d++)
-      if (bt->doc_offsets[d + 1] == bt->doc_offsets[d]) {
-        static const uint32_t one = CW_STATUS_ROOT;
-        HIPCHK(c, hipMemcpyAsync(res->status + d, &one, 4, hipMemcpyHostToDevice, c->stream));
-      }
+      if (bt->doc_offsets[d + 1] == bt->doc_offsets[d])
+        HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)(res->status + d), CW_STATUS_ROOT, 1,
+                                    c->stream));
     if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   if (c->prof) return collect_prof(c);
@@ -1170,12 +1291,14 @@ int cw_ctx_create(int device, cw_ctx **out) {
     return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
   };
   c->tb = knob("CW_TB", 1024);
-  c->walk_threads = knob("CW_WALK_THREADS", 512);
-  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 1024));
+  c->walk_threads = knob("CW_WALK_THREADS", 1024);
+  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 2048));
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
-  c->walk_nw = knob("CW_WALK_NW", 1);
+  c->min_log2cap = knob("CW_LOG2CAP", 4);
   c->join_lds = knob("CW_JOIN_LDS", 0);
+
+  c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
   *out = c;
   return 0;
 }

@@ -10,8 +10,10 @@ constexpr uint32_t TILE = 4096;
 constexpr uint32_t SORT_THREADS = 512;            // 8 waves
 constexpr uint32_t SORT_ITEMS = TILE / SORT_THREADS;
 constexpr uint32_t SORT_WAVES = SORT_THREADS / 64;
-constexpr uint32_t RADIX_BITS = 8;
-constexpr uint32_t RADIX = 1u << RADIX_BITS;
+constexpr uint32_t MAX_DIGIT = 11;                // bits per LSD pass
+constexpr uint32_t MAX_BINS = 1u << MAX_DIGIT;
+constexpr uint32_t SUB_BITS = 6;                  // in-tile sub-pass digit
+constexpr uint32_t SUB_BINS = 1u << SUB_BITS;
 
 // Join: per-document sample of the sorted ids (every 2^ls-th key, <= MAX_SAMPLES)
 // staged in LDS so the cause search touches global memory only at the end.

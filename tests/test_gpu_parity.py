@@ -183,3 +183,50 @@ def test_key_bits_found_on_device(weaver):
     a = weaver.weave_lists(off, idk, ck, kd, spec.layout())
     b = weaver.weave_lists(off, idk, ck, kd, spec.layout(), key_bits=0)
     assert np.array_equal(a.weave_perm, b.weave_perm)
+
+
+KNOBS = [{}, {"CW_LOG2CAP": "5"}, {"CW_LOG2K": "4", "CW_LOG2CAP": "5"},
+         {"CW_MAX_DIGIT": "8"}, {"CW_WALK_THREADS": "256", "CW_WALK_SPAN": "512"}]
+
+
+@pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
+def test_config2_documents_any_geometry(knobs, monkeypatch):
+    """Full-size config-2 documents (50,001 nodes) under every launch geometry
+    knob: the output must not depend on splitter density, slot size, digit
+    width or walker grouping."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    spec = gen.CONFIG2
+    off, idk, ck, kd = gen.generate(spec, 0, 24)
+    with abi.Weaver(0) as w:
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"CW_LOG2CAP": "5"}], ids=["default", "cap32"])
+def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
+    """The whole bench workload (10,000 config-2 documents, 5e8 nodes) against
+    the oracle, every document, plus permutation validity."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    spec = gen.CONFIG2
+    off, idk, ck, kd = gen.generate(spec, 0, 10_000, nthreads=32)
+    with abi.Weaver(0) as w:
+        res = w.weave_lists(off, idk, ck, kd, spec.layout(), yarns=False)
+    assert not res.status.any(), np.nonzero(res.status)[0][:10]
+    perm, vis, st = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF, nthreads=32)
+    assert not st.any()
+    bad = [d for d in range(10_000)
+           if not np.array_equal(res.weave_perm[int(off[d]):int(off[d + 1])],
+                                 perm[int(off[d]):int(off[d + 1])])]
+    if bad:
+        d = bad[0]
+        b, e = int(off[d]), int(off[d + 1])
+        g, o = res.weave_perm[b:e], perm[b:e]
+        lk, _ = oracle.list_weave(idk[b:e], ck[b:e], kd[b:e], oracle.METHOD_LINKED)
+        diff = np.nonzero(g != o)[0]
+        raise AssertionError(
+            f"{len(bad)} documents differ, first {bad[:5]}; doc {d}: {len(diff)} positions, "
+            f"first {diff[:4]}, gpu {g[diff[:4]]}, oracle {o[diff[:4]]}, gpu==linked "
+            f"{np.array_equal(g, lk)}, oracle==linked {np.array_equal(o, lk)}, gpu is a perm "
+            f"{len(np.unique(g)) == e - b}")
+    assert np.array_equal(res.visible(), vis)
