@@ -75,15 +75,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from cause_amd import abi, gen
+    from cause_amd import abi, gen, shard
     import dataclasses
 
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
     layout = spec.layout()
     D = a.docs
-    d0 = rank * D  # weak scaling: each rank owns its own contiguous documents
+    d0, d1 = shard.doc_range(rank, world, docs_per_rank=D)  # weak scaling, no data exchange
     t0 = time.time()
-    off, idk, ck, kd = gen.generate(spec, d0, d0 + D, nthreads=16)
+    off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16)
     N = len(idk)
     t_gen = time.time() - t0
     g_id = torch.from_numpy(idk.view(np.int64)).to(dev)
@@ -128,11 +128,7 @@ def main():
     w.set_profiling(False)
     stats = w.kernel_stats()
 
-    dt_max = dt
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt_max = float(t.item())
+    dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
     total_nodes = N * world * a.steps
     value = total_nodes / dt_max
 

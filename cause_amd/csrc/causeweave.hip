@@ -118,19 +118,22 @@ __global__ __launch_bounds__(1024) void k_radix_scan(uint32_t *__restrict__ hist
       }
 }
 
-// Stable rank of SORT_ITEMS striped items per lane by a sub-digit of sbits
-// (<= 6) bits: returns each item's position inside the tile.
-__device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[SORT_ITEMS], uint32_t len,
-                                              uint32_t sbits, uint32_t (&pos)[SORT_ITEMS],
-                                              uint32_t (*wcnt)[SORT_WAVES][SUB_BINS],
+// Stable rank of ITEMS striped items per lane (item k of lane t is element
+// k*NT + t) by a sub-digit of sbits (<= 6) bits: returns each item's position
+// inside the tile of `len` elements.
+template <int NT, int ITEMS>
+__device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[ITEMS], uint32_t len,
+                                              uint32_t sbits, uint32_t (&pos)[ITEMS],
+                                              uint32_t (*wcnt)[NT / 64][SUB_BINS],
                                               uint32_t *run) {
+  constexpr int NW = NT / 64;
   const uint32_t tid = threadIdx.x, w = tid >> 6, nbin = 1u << sbits;
   if (tid < SUB_BINS) run[tid] = 0;
-  for (uint32_t i = tid; i < SORT_WAVES * SUB_BINS; i += SORT_THREADS) (&wcnt[0][0][0])[i] = 0;
+  for (uint32_t i = tid; i < NW * SUB_BINS; i += NT) (&wcnt[0][0][0])[i] = 0;
   __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < SORT_ITEMS; k++) {
-    const bool valid = k * SORT_THREADS + tid < len;
+  for (uint32_t k = 0; k < ITEMS; k++) {
+    const bool valid = k * NT + tid < len;
     const uint32_t dd = sd[k];
     uint64_t m = __ballot(valid);
     for (uint32_t bit = 0; bit < sbits; bit++) {
@@ -145,7 +148,7 @@ __device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[SORT_ITEMS], 
     if (tid < nbin) {
       uint32_t r = run[tid];
 #pragma unroll
-      for (uint32_t ww = 0; ww < SORT_WAVES; ww++) {
+      for (uint32_t ww = 0; ww < NW; ww++) {
         const uint32_t c = wcnt[buf][ww][tid];
         wcnt[buf][ww][tid] = r;
         r += c;
@@ -169,7 +172,7 @@ __device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[SORT_ITEMS], 
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < SORT_ITEMS; k++) pos[k] += run[sd[k]];
+  for (uint32_t k = 0; k < ITEMS; k++) pos[k] += run[sd[k]];
   __syncthreads();
 }
 
@@ -214,7 +217,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     sd[k] = dg & ((1u << sub0) - 1);
   }
   // sub-pass A: low sub-digit
-  rank_subdigit(sd, len, sub0, pos, wcnt, run);
+  rank_subdigit<SORT_THREADS, SORT_ITEMS>(sd, len, sub0, pos, wcnt, run);
   const uint32_t sub1 = dbits - sub0;
   if (sub1 > 0) {
 #pragma unroll
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
       }
       sd[k] = ((uint32_t)(key[k] >> shift) & dmask) >> sub0;
     }
-    rank_subdigit(sd, len, sub1, pos, wcnt, run);
+    rank_subdigit<SORT_THREADS, SORT_ITEMS>(sd, len, sub1, pos, wcnt, run);
   }
 #pragma unroll
   for (uint32_t k = 0; k < SORT_ITEMS; k++)
@@ -352,97 +355,162 @@ __global__ __launch_bounds__(1024) void k_join(
   if (threadIdx.x == 0 && bst) atomicOr(&status[d], bst);
 }
 
-// --- effective parent + child-sort key ---------------------------------------
-// child key = ((eff+1) << 1) | (special ? 0 : 1); the root gets 0 (sorts first).
-__global__ __launch_bounds__(1024) void k_eff(const uint32_t *__restrict__ par,
-                                             const uint8_t *__restrict__ skind,
-                                             const uint64_t *__restrict__ skey,
-                                             uint32_t *__restrict__ status,
-                                             const uint32_t *__restrict__ tile_start,
-                                             const uint32_t *__restrict__ tile_doc,
-                                             const uint32_t *__restrict__ doc_off,
-                                             uint32_t *__restrict__ epar,
-                                             uint32_t *__restrict__ ckey) {
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t], base = doc_off[d];
-  bool dup = false;
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t r = i - base;
-    if (r == 0) {
-      epar[i] = 0;
-      ckey[i] = 0;
-      continue;
+// --- tree: effective parents, sibling order, links (one workgroup per document) --
+// Effective parent: a special keeps its cause, a non-special climbs
+// through special causes.  Siblings are ordered specials by descending id, then
+// non-specials by descending id (weave-later?, shared.cljc:202-223): with the
+// group key (eff parent, class) the next sibling of r is the previous node of
+// the same group in rank order, and the first child is the group's last node.
+// Ranks are swept in tiles of TREE_TILE: each tile is sorted by group key in
+// LDS (stable), neighbours inside the tile link directly, and a per-group
+// "last node so far" table (fcS/fcN, which ends as the first-child table)
+// links across tiles.  A second sweep assembles the link word the walk uses.
+template <int NT, int TILE_T>
+__global__ __launch_bounds__(NT) void k_tree(
+    const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ doc_log2k, uint32_t kbits, uint32_t bm_words,
+    uint32_t *__restrict__ epar, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+    uint32_t *__restrict__ fcN, uint64_t *__restrict__ link, uint32_t *__restrict__ status) {
+  constexpr uint32_t IT = TILE_T / NT;
+  __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T];
+  __shared__ uint32_t wcnt[2][NT / 64][SUB_BINS];
+  __shared__ uint32_t run[64];
+  // special / hide bit per rank (LDS when the document fits bm_words words)
+  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  const bool in_lds = ((n + 31) >> 5) <= bm_words;
+  uint32_t *spec_bm = bm, *hide_bm = bm + bm_words;
+  if (in_lds) {
+    // one ballot per wave per 64 ranks: bit r of the bitmap = special(rank r)
+    for (uint32_t r0 = (tid >> 6) << 6; r0 < n; r0 += NT) {
+      const uint32_t r = r0 + (tid & 63);
+      const uint8_t kd = r < n ? skind[base + r] : 0;
+      const uint64_t sm = __ballot(r < n && is_special(kd));
+      const uint64_t hm = __ballot(r < n && is_hide(kd));
+      if ((tid & 63) == 0) {
+        spec_bm[r0 >> 5] = (uint32_t)sm;
+        hide_bm[r0 >> 5] = (uint32_t)hm;
+        if ((r0 >> 5) + 1 < bm_words) {
+          spec_bm[(r0 >> 5) + 1] = (uint32_t)(sm >> 32);
+          hide_bm[(r0 >> 5) + 1] = (uint32_t)(hm >> 32);
+        }
+      }
     }
-    dup |= skey[i] == skey[i - 1];
-    const uint8_t k = skind[i];
-    uint32_t c = par[i];
-    const bool sp = is_special(k);
-    if (!sp)
-      while (c != 0 && is_special(skind[base + c])) c = par[base + c];
-    epar[i] = c;
-    ckey[i] = ((c + 1) << 1) | (sp ? 0u : 1u);
+    __syncthreads();
+  }
+  auto special_at = [&](uint32_t r) -> bool {
+    return in_lds ? ((spec_bm[r >> 5] >> (r & 31)) & 1u) : is_special(skind[base + r]);
+  };
+  auto hide_at = [&](uint32_t r) -> bool {
+    return in_lds ? ((hide_bm[r >> 5] >> (r & 31)) & 1u) : is_hide(skind[base + r]);
+  };
+  bool dup = false;
+  for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
+    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+    uint32_t key[IT], rk[IT], sd[IT], pos[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid, r = r0 + j;
+      key[k] = 0;
+      rk[k] = j;
+      if (j < len && r > 0) {
+        const bool sp = special_at(r);
+        uint32_t c = par[base + r];
+        if (!sp)
+          while (c != 0 && special_at(c)) c = par[base + c];
+        epar[base + r] = c;
+        key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
+        dup |= skey[base + r] == skey[base + r - 1];
+      } else if (j < len) {
+        epar[base] = 0;
+      }
+    }
+    // stable LDS sort of the tile by group key, 6 bits per sub-pass
+    for (uint32_t shift = 0; shift < kbits; shift += SUB_BITS) {
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) sd[k] = (key[k] >> shift) & (SUB_BINS - 1);
+      rank_subdigit<NT, IT>(sd, len, min(SUB_BITS, kbits - shift), pos, wcnt, run);
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++)
+        if (k * NT + tid < len) {
+          tkey[pos[k]] = key[k];
+          trank[pos[k]] = rk[k];
+        }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = k * NT + tid;
+        if (j < len) {
+          key[k] = tkey[j];
+          rk[k] = trank[j];
+        }
+      }
+      __syncthreads();
+    }
+    // next sibling inside the class: previous node of the group; a group's
+    // first node in the tile takes the group's last node of earlier tiles
+    uint32_t prv[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid;
+      const uint32_t kk = key[k];
+      prv[k] = 0;
+      if (j < len && kk != 0) {
+        if (j > 0 && tkey[j - 1] == kk) {
+          prv[k] = r0 + trank[j - 1];
+        } else {
+          uint32_t *tab = (kk & 1) ? fcN : fcS;
+          prv[k] = __hip_atomic_load(&tab[base + (kk >> 1) - 1], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++)
+      if (k * NT + tid < len) tns[rk[k]] = prv[k];
+    __syncthreads();  // every group's old "last" is read before it is replaced
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid;
+      if (j >= len) continue;
+      const uint32_t kk = key[k];
+      if (kk != 0 && !(j + 1 < len && tkey[j + 1] == kk)) {
+        uint32_t *tab = (kk & 1) ? fcN : fcS;
+        __hip_atomic_store(&tab[base + (kk >> 1) - 1], r0 + rk[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
+    __syncthreads();
   }
   if (dup) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
-}
-
-// --- links --------------------------------------------------------------------
-// Over the child-sorted array: groups (eff parent, class) in ascending rank.
-// Sibling order is specials by descending id, then non-specials by descending
-// id, so the next sibling inside a class is the previous group element and the
-// first child of a class is the group's last element.
-__global__ __launch_bounds__(1024) void k_links(const uint32_t *__restrict__ ckey_s,
-                                               const uint32_t *__restrict__ cval_s,
-                                               const uint32_t *__restrict__ tile_start,
-                                               const uint32_t *__restrict__ tile_doc,
-                                               const uint32_t *__restrict__ doc_off,
-                                               uint32_t *__restrict__ nsc,
-                                               uint32_t *__restrict__ fcS,
-                                               uint32_t *__restrict__ fcN) {
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
-  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t key = ckey_s[i];
-    if (key == 0) continue;  // the root
-    const uint32_t j = i - base, r = cval_s[i];
-    const uint32_t e = (key >> 1) - 1;
-    const bool prev_same = j > 0 && ckey_s[i - 1] == key;
-    const bool next_same = j + 1 < n && ckey_s[i + 1] == key;
-    nsc[base + r] = prev_same ? cval_s[i - 1] : 0u;
-    if (!next_same) ((key & 1) ? fcN : fcS)[base + e] = r;
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_link_final(
-    const uint32_t *__restrict__ nsc, const uint32_t *__restrict__ fcS,
-    const uint32_t *__restrict__ fcN, const uint32_t *__restrict__ epar,
-    const uint8_t *__restrict__ skind, const uint32_t *__restrict__ tile_start,
-    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
-    const uint32_t *__restrict__ doc_log2k, uint64_t *__restrict__ link) {
-  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
-  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t r = i - base;
-    const uint8_t k = skind[i];
-    const bool sp = is_special(k);
-    const uint32_t fs = fcS[i], fn = fcN[i];
+  // the sweep below reads what this workgroup wrote above
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  __syncthreads();
+  for (uint32_t r = tid; r < n; r += NT) {
+    const bool sp = special_at(r);
+    const uint32_t fs = fcS[base + r], fn = fcN[base + r];
     const uint32_t fc = fs ? fs : fn;
     uint32_t nx;
+    const uint32_t e = epar[base + r];
     if (r == 0) {
       nx = NX_END;
     } else {
-      uint32_t ns = nsc[i];
-      if (!ns && sp) ns = fcN[base + epar[i]];  // last special -> newest non-special
-      nx = ns ? ns : (NX_UP | epar[i]);
+      uint32_t ns = nsc[base + r];
+      if (!ns && sp) ns = fcN[base + e];  // last special -> newest non-special
+      nx = ns ? ns : (NX_UP | e);
     }
-    // the next weave node after a non-special is its first child,
-    // which is its newest special child when it has one.
-    const bool vis = !sp && r != 0 && !(fs && is_hide(skind[base + fs]));
+    // after a non-special comes its first child, which is its newest
+    // special child when it has one.
+    const bool vis = !sp && r != 0 && !(fs && hide_at(fs));
     const bool split = r == split_node(d, r >> log2k, log2k, n);
     const uint32_t lo = fc | (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
-    link[i] = (uint64_t)lo | ((uint64_t)nx << 32);
+    link[base + r] = (uint64_t)lo | ((uint64_t)nx << 32);
   }
 }
 
-// --- Euler walk ----------------------------------------------------------------
 // Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
 // splitter block lw/2's splitter node and follows the tour until the next
 // splitter arc.  Every down arc it crosses gets (walker, local count).
@@ -710,7 +778,7 @@ struct cw_ctx {
   bool tab_on_device = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
   uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
-           join_lds = 0, max_digit = MAX_DIGIT, min_log2cap = 4;
+           join_lds = 0, max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
 };
 
 namespace {
@@ -1036,8 +1104,6 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
   uint32_t *par = scratch_t<uint32_t>(c, "par", N), *epar = scratch_t<uint32_t>(c, "epar", N);
   uint8_t *skind = scratch_t<uint8_t>(c, "skind", N);
-  uint32_t *ckA = scratch_t<uint32_t>(c, "ckA", N), *ckB = scratch_t<uint32_t>(c, "ckB", N);
-  uint32_t *cvA = scratch_t<uint32_t>(c, "cvA", N), *cvB = scratch_t<uint32_t>(c, "cvB", N);
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
   uint64_t *link = scratch_t<uint64_t>(c, "link", N);
@@ -1047,7 +1113,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
   uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
   uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
-  if (!skA || !skB || !svA || !svB || !par || !epar || !skind || !ckA || !ckB || !cvA || !cvB ||
+  if (!skA || !skB || !svA || !svB || !par || !epar || !skind ||
       !nsc || !fcS || !fcN || !link || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase)
     return fail(c, "out of device memory (N=%u)", N);
 
@@ -1086,36 +1152,24 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }
     if (check_launch(c, "join")) return -1;
 
-    // 3. effective parent
-    {
-      Launch L(c, "effparent", (double)N * (4 + 1 + 8 + 4 + 4));
-      hipLaunchKernelGGL(k_eff, GT, TB, 0, c->stream, par, skind, skey, out->status, tile_start,
-                         tile_doc, doc_off, epar, ckA);
-    }
-    if (check_launch(c, "effparent")) return -1;
-
-    // 4. child sort by (eff parent, class), values = rank (identity)
-    uint32_t *cks, *cvs;
-    const uint32_t cbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
-    if (radix_sort<uint32_t>(c, "childsort", ckA, nullptr, ckB, cvA, ckA, cvB, cbits, 0, N, &cks,
-                             &cvs))
-      return -1;
-
-    // 5. links
+    // 3-5. effective parents, sibling order, links
     HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
     HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
     {
-      Launch L(c, "links", (double)N * (4 + 4 + 4 + 4));
-      hipLaunchKernelGGL(k_links, GT, TB, 0, c->stream, cks, cvs, tile_start, tile_doc, doc_off,
-                         nsc, fcS, fcN);
+      const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
+      // special/hide bitmaps in LDS for documents up to 2^18 nodes
+      const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
+      Launch L(c, "tree", (double)N * (4 + 1 + 8 + 4 + 4 + 8 + 4 + 4 + 4 + 4 + 8));
+      if (c->tree_cfg == 1)
+        hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
+                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
+                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
+      else
+        hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
+                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
+                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
     }
-    if (check_launch(c, "links")) return -1;
-    {
-      Launch L(c, "linkfinal", (double)N * (4 + 4 + 4 + 4 + 1 + 8));
-      hipLaunchKernelGGL(k_link_final, GT, TB, 0, c->stream, nsc, fcS, fcN, epar, skind,
-                         tile_start, tile_doc, doc_off, doc_log2k, link);
-    }
-    if (check_launch(c, "linkfinal")) return -1;
+    if (check_launch(c, "tree")) return -1;
 
     // 6. Euler walk
     HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
@@ -1296,6 +1350,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
   c->min_log2cap = knob("CW_LOG2CAP", 4);
+  c->tree_cfg = knob("CW_TREE", 0);
   c->join_lds = knob("CW_JOIN_LDS", 0);
 
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));

@@ -15,6 +15,10 @@ constexpr uint32_t MAX_BINS = 1u << MAX_DIGIT;
 constexpr uint32_t SUB_BITS = 6;                  // in-tile sub-pass digit
 constexpr uint32_t SUB_BINS = 1u << SUB_BITS;
 
+// Tree sweep: one workgroup per document, ranks in LDS-sorted tiles.
+constexpr uint32_t TREE_THREADS = 1024;
+constexpr uint32_t TREE_TILE = 4096;
+
 // Join: per-document sample of the sorted ids (every 2^ls-th key, <= MAX_SAMPLES)
 // staged in LDS so the cause search touches global memory only at the end.
 constexpr uint32_t MAX_SAMPLES = 8192;             // 64 KiB of LDS
