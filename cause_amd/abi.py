@@ -19,6 +19,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "causeweave.h")
 
 CW_MEM_HOST, CW_MEM_DEVICE = 0, 1
 STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1, 2, 4, 8, 32
+STATUS_MAP_KEY = 16
 
 
 class CwListBatch(C.Structure):
@@ -32,6 +33,18 @@ class CwListResult(C.Structure):
     _fields_ = [("weave_perm", C.c_void_p), ("visible_bits", C.c_void_p),
                 ("visible_count", C.c_void_p), ("max_ts", C.c_void_p), ("status", C.c_void_p),
                 ("yarn_perm", C.c_void_p)]
+
+
+class CwMapBatch(C.Structure):
+    _fields_ = [("n_colls", C.c_uint64), ("coll_offsets", C.POINTER(C.c_uint64)),
+                ("id_key", C.c_void_p), ("cause", C.c_void_p), ("cause_is_id", C.c_void_p),
+                ("kind", C.c_void_p), ("key_bits", C.c_uint32), ("token_bits", C.c_uint32)]
+
+
+class CwMapResult(C.Structure):
+    _fields_ = [("cap_segs", C.c_uint64), ("n_segs", C.c_uint64), ("seg_offsets", C.c_void_p),
+                ("seg_coll", C.c_void_p), ("seg_key", C.c_void_p), ("seg_active", C.c_void_p),
+                ("seg_perm", C.c_void_p), ("status", C.c_void_p)]
 
 
 class CwKernelStat(C.Structure):
@@ -75,6 +88,9 @@ def lib():
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
                                      C.c_int]
         L.cw_weave_lists.restype = C.c_int
+        L.cw_weave_maps.argtypes = [C.c_void_p, C.POINTER(CwMapBatch), C.POINTER(CwMapResult),
+                                    C.c_int]
+        L.cw_weave_maps.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -93,6 +109,20 @@ class ListResult:
         n = len(self.weave_perm)
         b = np.unpackbits(self.visible_bits.view(np.uint8), bitorder="little")
         return b[:n]
+
+
+@dataclass
+class MapResult:
+    """Key weaves of a batch of maps, per collection in ascending key-token order."""
+    seg_offsets: np.ndarray  # uint64[S+1] into seg_perm
+    seg_coll: np.ndarray     # uint32[S]
+    seg_key: np.ndarray      # uint64[S] key token
+    seg_active: np.ndarray   # int64[S] collection-local input index, -1 = ::blank
+    seg_perm: np.ndarray     # uint32[N+S] root (UINT32_MAX) then input indices, weave order
+    status: np.ndarray       # uint32[n_colls]
+
+    def key_weave(self, s):
+        return self.seg_perm[int(self.seg_offsets[s]):int(self.seg_offsets[s + 1])]
 
 
 def _ptr(a):
@@ -194,3 +224,32 @@ class Weaver:
                          g("status"), g("yarn_perm"))
         self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
                     "cw_weave_lists")
+
+    def weave_maps(self, offsets, id_key, cause, cause_is_id, kind, token_bits,
+                   key_bits=0) -> MapResult:
+        """Host-memory call of cw_weave_maps."""
+        i = np.ascontiguousarray(id_key, np.uint64)
+        c = np.ascontiguousarray(cause, np.uint64)
+        ci = np.ascontiguousarray(cause_is_id, np.uint8)
+        k = np.ascontiguousarray(kind, np.uint8)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        D, N = len(off) - 1, len(i)
+        if int(off[-1]) != N:
+            raise ValueError("offsets[-1] != number of nodes")
+        b = CwMapBatch()
+        b.n_colls = D
+        b.coll_offsets = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        b.id_key, b.cause, b.cause_is_id, b.kind = _ptr(i), _ptr(c), _ptr(ci), _ptr(k)
+        b.key_bits = key_bits
+        b.token_bits = token_bits
+        cap = max(N, 1)
+        out = MapResult(np.zeros(cap + 1, np.uint64), np.zeros(cap, np.uint32),
+                        np.zeros(cap, np.uint64), np.zeros(cap, np.int64),
+                        np.zeros(N + cap, np.uint32), np.zeros(max(D, 1), np.uint32))
+        r = CwMapResult(cap, 0, _ptr(out.seg_offsets), _ptr(out.seg_coll), _ptr(out.seg_key),
+                        _ptr(out.seg_active), _ptr(out.seg_perm), _ptr(out.status))
+        self._check(self._L.cw_weave_maps(self._h, C.byref(b), C.byref(r), CW_MEM_HOST),
+                    "cw_weave_maps")
+        S = int(r.n_segs)
+        return MapResult(out.seg_offsets[:S + 1], out.seg_coll[:S], out.seg_key[:S],
+                         out.seg_active[:S], out.seg_perm[:N + S], out.status[:D])

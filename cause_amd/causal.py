@@ -198,3 +198,106 @@ def causal_list_to_edn(ct):
 def count(ct):
     """list.cljc:77"""
     return len(causal_list_to_list(ct))
+
+
+# ------------------------------------------------------------------------- maps
+# map.cljc: the map interface over cw_weave_maps.  A map ct's ``weave`` is
+# {key: key weave (root first)}; ``_active`` is {key: active node or BLANK}.
+BLANK = Keyword("causal.collections.map", "blank")   # ::blank, map.cljc:52
+
+
+def new_map_ct(site_id=None, uuid=None, rng=random):
+    """map.cljc:12-19"""
+    return {"type": "map", "lamport_ts": 0, "uuid": uuid or _uid(rng, 21),
+            "site_id": site_id or new_site_id(rng), "nodes": {}, "yarns": {}, "weave": {},
+            "_active": {}}
+
+
+def _unpack_id(key, layout, rank):
+    inv = {r: s for s, r in rank.items()}
+    ts = key >> layout.ts_shift
+    site = (key >> layout.site_shift) & ((1 << layout.site_bits) - 1)
+    tx = key & ((1 << layout.tx_bits) - 1)
+    return (ts, inv[site], tx)
+
+
+def weave_maps(cts):
+    """Full reweave of many map cts in ONE GPU call (c.map/weave 1-arity,
+    map.cljc:21-28, for each); also computes active-node per key."""
+    docs = [[(i, b[0], b[1]) for i, b in ct["nodes"].items()] for ct in cts]
+    pm = pack.pack_maps(docs)
+    res = weaver().weave_maps(pm.offsets, pm.id_key, pm.cause, pm.cause_is_id, pm.kind,
+                              pm.token_bits, pm.layout.key_bits)
+    out = []
+    segs_of = {}
+    for s, d in enumerate(res.seg_coll.tolist()):
+        segs_of.setdefault(d, []).append(s)
+    for d, (ct, nodes) in enumerate(zip(cts, docs)):
+        st = int(res.status[d])
+        if st:
+            raise CauseError(f"map outside the weave's domain (status {st})", {"weave-domain"})
+        weave, active = {}, {}
+        for s in segs_of.get(d, []):
+            k = int(res.seg_key[s])
+            if k == pack.NIL:
+                key = None
+            elif k >> 63:
+                key = _unpack_id(k & ((1 << 63) - 1), pm.layout, pm.ranks[d])
+            else:
+                key = pm.keys[k]
+            weave[key] = [ROOT_NODE] + [nodes[p] for p in res.key_weave(s)[1:]]
+            a = int(res.seg_active[s])
+            active[key] = BLANK if a < 0 else (nodes[a][0], key, nodes[a][2])
+        new = dict(ct)
+        new["weave"] = weave
+        new["_active"] = active
+        out.append(new)
+    return out
+
+
+def map_weave(ct, node=None, more=None):
+    """map.cljc:21-45 -- every arity is the full GPU reweave."""
+    if node is not None and node[0] not in ct["nodes"]:
+        return ct
+    return weave_maps([ct])[0]
+
+
+def active_node(ct, k):
+    """map.cljc:47-59 (computed on the GPU with the weave)."""
+    return ct["_active"].get(k, BLANK)
+
+
+def map_get(ct, k):
+    """map.cljc:61-66"""
+    n = active_node(ct, k)
+    return None if n is BLANK else n[2]
+
+
+def map_count(ct):
+    """map.cljc:68-73"""
+    return sum(1 for n in ct["_active"].values() if n is not BLANK)
+
+
+def map_assoc(ct, k, v):
+    """map.cljc:75-81"""
+    if v != map_get(ct, k):
+        return append(map_weave, ct, k, v)
+    return ct
+
+
+def map_dissoc(ct, k):
+    """map.cljc:83-89"""
+    v = map_get(ct, k)
+    if v is not None and v is not False:
+        return append(map_weave, ct, k, HIDE)
+    return ct
+
+
+def causal_map_to_edn(ct):
+    """map.cljc:94-103 (nested collections are opaque values here)."""
+    return {n[1]: n[2] for n in ct["_active"].values() if n is not BLANK}
+
+
+def causal_map_to_list(ct):
+    """map.cljc:105-109"""
+    return [n for n in ct["_active"].values() if n is not BLANK]

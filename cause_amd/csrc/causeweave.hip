@@ -300,7 +300,9 @@ __global__ __launch_bounds__(256) void k_sample(const uint64_t *__restrict__ ske
 }
 
 // Join in sorted order: gather each node's cause id and kind, search the cause
-// among the document's sorted ids (LDS samples, then one span of 2^ls keys).
+// among the document's sorted ids: a branchless search of the LDS sample
+// (every 2^ls-th id), then one 2^ls-key span of global memory.  Each lane
+// handles JOIN_ITEMS nodes with their loads and searches interleaved.
 __global__ __launch_bounds__(1024) void k_join(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
@@ -308,6 +310,7 @@ __global__ __launch_bounds__(1024) void k_join(
     const uint32_t *__restrict__ doc_ls, const uint32_t *__restrict__ tile_start,
     const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
     uint32_t *__restrict__ par, uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
+  constexpr int IT = JOIN_ITEMS;
   extern __shared__ __attribute__((aligned(16))) uint64_t S[];  // <= MAX_SAMPLES
   __shared__ uint32_t bst;
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
@@ -316,39 +319,63 @@ __global__ __launch_bounds__(1024) void k_join(
   for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) S[j] = samples[s0 + j];
   if (threadIdx.x == 0) bst = 0;
   __syncthreads();
+  uint32_t top = 1;
+  while (top <= ns) top <<= 1;
+  const uint32_t ts = tile_start[t], te = tile_start[t + 1];
   uint32_t st = 0;
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t r = i - base;
-    const uint32_t gi = base + sval[i];
-    const uint8_t kd = kind[gi];
-    uint32_t p = 0;
-    if (r == 0) {
-      if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
-    } else {
-      if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
-      const uint64_t ck = cause_key[gi];
-      uint32_t lo = 0, len = ns;  // count of samples <= ck
-      while (len > 0) {
-        const uint32_t half = len >> 1;
-        if (S[lo + half] <= ck) { lo += half + 1; len -= half + 1; }
-        else len = half;
-      }
-      uint32_t c = n;
-      if (lo > 0) {
-        uint32_t a0 = (lo - 1) << ls;
-        uint32_t b0 = min(a0 + (1u << ls), n);
-        while (a0 < b0) {
-          const uint32_t m = (a0 + b0) >> 1;
-          if (skey[base + m] < ck) a0 = m + 1; else b0 = m;
-        }
-        c = a0;
-      }
-      if (c >= n || skey[base + c] != ck) st |= CW_STATUS_ORPHAN;
-      else if (c >= r) st |= CW_STATUS_NON_LAMPORT;
-      else p = c;
+  for (uint32_t i0 = ts + threadIdx.x; i0 < te; i0 += IT * blockDim.x) {
+    uint32_t gi[IT];
+    uint8_t kd[IT];
+    uint64_t ck[IT];
+    uint32_t lo[IT];
+    bool v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const uint32_t i = i0 + k * blockDim.x;
+      v[k] = i < te;
+      gi[k] = v[k] ? base + sval[i] : base;
     }
-    par[i] = p;
-    skind[i] = kd;
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      kd[k] = v[k] ? kind[gi[k]] : 0;
+      ck[k] = v[k] ? cause_key[gi[k]] : 0;
+      lo[k] = 0;
+    }
+    // lo = number of samples <= ck (branchless, interleaved)
+    for (uint32_t bstep = top >> 1; bstep; bstep >>= 1) {
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const uint32_t q = lo[k] + bstep;
+        if (q <= ns && S[q - 1] <= ck[k]) lo[k] = q;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      if (!v[k]) continue;
+      const uint32_t i = i0 + k * blockDim.x;
+      const uint32_t r = i - base;
+      uint32_t p = 0;
+      if (r == 0) {
+        if (!(kd[k] & KIND_ROOT)) st |= CW_STATUS_ROOT;
+      } else {
+        if (kd[k] & KIND_ROOT) st |= CW_STATUS_ROOT;
+        uint32_t c = n;
+        if (lo[k] > 0) {
+          uint32_t a0 = (lo[k] - 1) << ls;
+          uint32_t b0 = min(a0 + (1u << ls), n);
+          while (a0 < b0) {
+            const uint32_t m = (a0 + b0) >> 1;
+            if (skey[base + m] < ck[k]) a0 = m + 1; else b0 = m;
+          }
+          c = a0;
+        }
+        if (c >= n || skey[base + c] != ck[k]) st |= CW_STATUS_ORPHAN;
+        else if (c >= r) st |= CW_STATUS_NON_LAMPORT;
+        else p = c;
+      }
+      par[i] = p;
+      skind[i] = kd[k];
+    }
   }
   if (st) atomicOr(&bst, st);
   __syncthreads();
@@ -422,7 +449,8 @@ __global__ __launch_bounds__(NT) void k_tree(
           while (c != 0 && special_at(c)) c = par[base + c];
         epar[base + r] = c;
         key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
-        dup |= skey[base + r] == skey[base + r - 1];
+        const uint64_t me = skey[base + r];
+        dup |= me == skey[base + r - 1];
       } else if (j < len) {
         epar[base] = 0;
       }
@@ -597,7 +625,8 @@ __global__ __launch_bounds__(1024) void k_walk(
 // The W sublists of a document form one linked list (the Euler tour).  Every
 // CHAIN-th sublist id heads an LDS chain; one lane per head walks its chain
 // (prefix sums in place), lane 0 ranks the <= W/CHAIN chains, then every
-// sublist gets chain base + local prefix = number of down arcs before it.
+// sublist gets chain base + local prefix = number of down arcs before it, and
+// its index in tour order (order[] lists sublists in tour order for the emit).
 __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               const uint32_t *__restrict__ wnext,
                                               const uint32_t *__restrict__ walk_first,
@@ -606,11 +635,12 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               const uint32_t *__restrict__ doc_off,
                                               const uint64_t *__restrict__ skey, uint32_t ts_shift,
                                               uint32_t *__restrict__ sbase,
+                                              uint32_t *__restrict__ order,
                                               uint64_t *__restrict__ max_ts,
                                               uint32_t *__restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // nx[W], val[W]
-  __shared__ uint32_t ch_next[MAX_SUBLISTS / CHAIN], ch_sum[MAX_SUBLISTS / CHAIN];
-  __shared__ uint32_t ch_base[MAX_SUBLISTS / CHAIN];
+  constexpr uint32_t NCH = MAX_SUBLISTS / CHAIN;
+  __shared__ uint32_t ch_next[NCH], ch_sum[NCH], ch_len[NCH], ch_base[NCH], ch_tbase[NCH];
   __shared__ uint32_t bad_s;
   const uint32_t d = blockIdx.x, f = walk_first[d];
   const uint32_t W = min(doc_W[d] + dyn_ctr[d], walk_first[d + 1] - f);  // static + continued
@@ -626,15 +656,17 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
   __syncthreads();
   const uint32_t C = (W + CHAIN - 1) / CHAIN;
   for (uint32_t h = threadIdx.x; h < C; h += blockDim.x) {
-    uint32_t j = h * CHAIN, acc = 0, steps = 0;
+    uint32_t j = h * CHAIN, acc = 0, len = 0;
     for (;;) {
       const uint32_t x = nx[j], cval = val[j];
-      val[j] = acc;  // down arcs before j inside the chain
-      nx[j] = h;     // chain of j
+      val[j] = acc;            // down arcs before j inside the chain
+      nx[j] = (h << 24) | len;  // chain of j, index of j inside the chain
       acc += cval;
-      if (x == NX_END || x % CHAIN == 0 || x >= W || ++steps > W) {
+      len++;
+      if (x == NX_END || x % CHAIN == 0 || x >= W || len > W) {
         ch_next[h] = (x == NX_END || x >= W) ? NX_END : x / CHAIN;
         ch_sum[h] = acc;
+        ch_len[h] = len;
         if (x != NX_END && x % CHAIN != 0) bad_s = 1;
         break;
       }
@@ -643,17 +675,23 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t run = 0, c = 0, steps = 0;
+    uint32_t run = 0, trun = 0, c = 0, steps = 0;
     while (c != NX_END && steps++ <= C) {
       ch_base[c] = run;
+      ch_tbase[c] = trun;
       run += ch_sum[c];
+      trun += ch_len[c];
       c = ch_next[c];
     }
-    if (run != n || bad_s) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+    if (run != n || trun != W || bad_s) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x)
-    sbase[f + i] = ch_base[min(nx[i], C - 1)] + val[i];
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
+    const uint32_t h = min(nx[i] >> 24, C - 1), li = nx[i] & 0xFFFFFFu;
+    sbase[f + i] = ch_base[h] + val[i];
+    const uint32_t ti = ch_tbase[h] + li;
+    if (ti < W) order[f + ti] = i;
+  }
 }
 
 // --- emit: sublist slots -> weave order ------------------------------------------
@@ -663,7 +701,8 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
 __global__ __launch_bounds__(256) void k_emit(
     const uint32_t *__restrict__ slots, const uint64_t *__restrict__ slot_first,
     const uint32_t *__restrict__ wcnt, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ sval, const uint32_t *__restrict__ eblk_doc,
+    const uint32_t *__restrict__ order, const uint32_t *__restrict__ sval,
+    const uint32_t *__restrict__ eblk_doc,
     const uint32_t *__restrict__ eblk_x0, const uint32_t *__restrict__ walk_first,
     const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ dyn_ctr,
     const uint32_t *__restrict__ doc_log2cap, const uint32_t *__restrict__ doc_off,
@@ -674,10 +713,11 @@ __global__ __launch_bounds__(256) void k_emit(
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d];
   const uint32_t Weff = min(doc_W[d] + dyn_ctr[d], walk_first[d + 1] - f);
   const uint32_t log2cap = doc_log2cap[d];
-  const uint32_t x = eblk_x0[b] + threadIdx.x;
+  const uint32_t ti = eblk_x0[b] + threadIdx.x;  // tour index: lanes write adjacent ranges
   uint32_t nvis = 0;
   bool bad = false;
-  if (x < Weff) {
+  const uint32_t x = ti < Weff ? order[f + ti] : 0u;
+  if (ti < Weff && x < Weff) {
     const uint32_t cnt = wcnt[f + x], p0 = sbase[f + x];
     const uint32_t *sl = slots + slot_first[d] + ((size_t)x << log2cap);
     if (p0 + cnt > n || cnt > (1u << log2cap)) {
@@ -727,6 +767,218 @@ __global__ void k_or_reduce(const uint64_t *__restrict__ keys, uint32_t N,
     acc |= keys[i];
   for (int o = 32; o > 0; o >>= 1) acc |= __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, (unsigned long long)acc);
+}
+
+// ============================================================================
+// Maps (c.map/weave 1-arity, map.cljc:26-45): every (collection, key) pair is
+// an independent list weave rooted at a virtual [[0 "0" 0] nil nil].  The map
+// kernels resolve each node's key, group nodes by key and lay every key weave
+// out as a list document (root first), which the list pipeline then weaves.
+// ============================================================================
+constexpr uint32_t MAP_NO_PARENT = 0xFFFFFFFFu;  // cause-in-weave = the virtual root
+constexpr uint32_t MAP_CHAIN = 0xFFFFFFFEu;      // orphan: appended after its predecessor
+
+// Per id-sorted node: the key (map.cljc:31-34) as a grouping value and the
+// rank of its cause-in-weave (map.cljc:35-37).  Grouping values, with
+// W = max(token_bits, key_bits):
+//   token t                         t              (cause is a key)
+//   id X               1 << W | X     (the cause node is id-caused by X)
+//   nil                             2 << W         (the cause node is absent)
+// In an id or nil key weave no node's cause is in the weave (each is an
+// orphan there), so weave-node appends every node at the end: the weave is
+// the root then the nodes in id order (shared.cljc:226-241, asap never holds).
+__global__ __launch_bounds__(256) void k_map_key(
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ cause, const uint8_t *__restrict__ cause_is_id,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    uint32_t token_bits, uint32_t W, uint64_t *__restrict__ segk, uint32_t *__restrict__ mpar,
+    uint8_t *__restrict__ mkind, uint32_t *__restrict__ status) {
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  const uint64_t tmask = (1ull << token_bits) - 1;
+  uint32_t bad = 0;
+  for (uint32_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+    const uint32_t gi = base + sval[i];
+    const uint64_t c = cause[gi];
+    uint64_t key;
+    uint32_t p;
+    if (i > base && skey[i - 1] == skey[i]) bad |= CW_STATUS_DUP;
+    if (cause_is_id[gi]) {
+      const uint32_t r = lower_bound_u64(skey + base, n, c);
+      if (r < n && skey[base + r] == c) {
+        const uint32_t gc = base + sval[base + r];
+        if (cause_is_id[gc]) {
+          key = (1ull << W) | cause[gc];
+          p = MAP_CHAIN;
+        } else {
+          key = cause[gc] & tmask;
+          if (cause[gc] > tmask) bad |= CW_STATUS_MAP_KEY;
+          p = r;
+        }
+      } else {
+        key = 2ull << W;
+        p = MAP_CHAIN;
+        if (c == 0) bad |= CW_STATUS_MAP_KEY;  // caused by the root id itself
+      }
+    } else {
+      key = c & tmask;
+      if (c > tmask) bad |= CW_STATUS_MAP_KEY;
+      p = MAP_NO_PARENT;
+    }
+    segk[i] = key;
+    mpar[i] = p;
+    mkind[i] = kind[gi];
+  }
+  if (bad) atomicOr(&status[d], bad);
+}
+
+// Key-weave heads in the key-sorted order: element j starts a key weave when
+// it is the first of its collection or its key differs from j-1's.
+__device__ __forceinline__ bool seg_head(const uint64_t *__restrict__ segk, uint32_t j,
+                                         uint32_t cbase) {
+  return j == cbase || segk[j] != segk[j - 1];
+}
+
+__global__ __launch_bounds__(256) void k_seg_count(const uint64_t *__restrict__ segk,
+                                                   const uint32_t *__restrict__ tile_start,
+                                                   const uint32_t *__restrict__ tile_doc,
+                                                   const uint32_t *__restrict__ doc_off,
+                                                   uint32_t *__restrict__ tile_cnt) {
+  __shared__ uint32_t wtot[4];
+  const uint32_t t = blockIdx.x, cbase = doc_off[tile_doc[t]];
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  uint32_t cnt = 0;
+  for (uint32_t j = s + threadIdx.x; j < e; j += 256) cnt += seg_head(segk, j, cbase) ? 1u : 0u;
+  uint32_t total;
+  block_exscan<256>(cnt, wtot, &total);
+  if (threadIdx.x == 0) tile_cnt[t] = total;
+}
+
+// Numbers the key weaves (tile_sbase = exclusive prefix of k_seg_count) and
+// records, per key weave, its first sorted element, collection and key; per
+// element, its key weave.  Each lane owns a contiguous run of the tile.
+__global__ __launch_bounds__(256) void k_seg_mark(
+    const uint64_t *__restrict__ segk, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ tile_sbase, uint32_t W, uint32_t *__restrict__ seg_of,
+    uint32_t *__restrict__ seg_start, uint32_t *__restrict__ seg_coll,
+    uint64_t *__restrict__ seg_key) {
+  __shared__ uint32_t wtot[4];
+  const uint32_t t = blockIdx.x, d = tile_doc[t], cbase = doc_off[d];
+  const uint32_t s = tile_start[t], e = tile_start[t + 1];
+  const uint32_t per = (e - s + 255) / 256;
+  const uint32_t j0 = min(e, s + threadIdx.x * per), j1 = min(e, j0 + per);
+  uint32_t cnt = 0;
+  for (uint32_t j = j0; j < j1; j++) cnt += seg_head(segk, j, cbase) ? 1u : 0u;
+  uint32_t sid = tile_sbase[t] + block_exscan<256>(cnt, wtot, nullptr) - 1;
+  for (uint32_t j = j0; j < j1; j++) {
+    if (seg_head(segk, j, cbase)) {
+      sid++;
+      seg_start[sid] = j;
+      seg_coll[sid] = d;
+      const uint64_t g = segk[j], cls = g >> W;
+      seg_key[sid] = cls == 0 ? g : cls == 1 ? (CW_MAP_ID_KEY | (g & ((1ull << W) - 1))) : CW_NIL;
+    }
+    seg_of[j] = sid;
+  }
+}
+
+// Lays the key weaves out as list documents: key weave s occupies
+// [seg_start[s] + s, seg_start[s+1] + s + 1) with its root first.  Ids keep
+// their packing (real ids are > 0, the virtual root is id 0).
+__global__ __launch_bounds__(256) void k_seg_build(
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint32_t *__restrict__ mpar, const uint8_t *__restrict__ mkind,
+    const uint32_t *__restrict__ rank_s, const uint32_t *__restrict__ seg_of,
+    const uint32_t *__restrict__ seg_coll, const uint32_t *__restrict__ coll_off, uint32_t N,
+    uint64_t *__restrict__ lid, uint64_t *__restrict__ lcause, uint8_t *__restrict__ lkind,
+    uint32_t *__restrict__ lmap) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= N) return;
+  const uint32_t sg = seg_of[j], cbase = coll_off[seg_coll[sg]];
+  const uint32_t i = cbase + rank_s[j];
+  const uint32_t out = j + sg + 1;
+  const uint32_t p = mpar[i];
+  uint64_t lc;
+  if (p == MAP_NO_PARENT) {
+    lc = 0ull;
+  } else if (p == MAP_CHAIN) {  // the previous node of the key weave (or its root)
+    lc = (j > 0 && seg_of[j - 1] == sg) ? skey[cbase + rank_s[j - 1]] : 0ull;
+  } else {
+    lc = skey[cbase + p];
+  }
+  lid[out] = skey[i];
+  lcause[out] = lc;
+  lkind[out] = mkind[i] & 3u;  // a map has no root node of its own
+  lmap[out] = sval[i];
+}
+
+__global__ __launch_bounds__(256) void k_seg_roots(const uint32_t *__restrict__ seg_start,
+                                                   uint32_t S, uint64_t *__restrict__ lid,
+                                                   uint64_t *__restrict__ lcause,
+                                                   uint8_t *__restrict__ lkind,
+                                                   uint32_t *__restrict__ lmap) {
+  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sg >= S) return;
+  const uint32_t out = seg_start[sg] + sg;
+  lid[out] = 0;
+  lcause[out] = CW_NIL;
+  lkind[out] = CW_KIND_ROOT;
+  lmap[out] = 0xFFFFFFFFu;
+}
+
+// Weave positions -> collection-local input indices (root -> UINT32_MAX).
+__global__ __launch_bounds__(256) void k_seg_perm(const uint32_t *__restrict__ lperm,
+                                                  const uint32_t *__restrict__ lmap,
+                                                  const uint64_t *__restrict__ seg_off,
+                                                  const uint32_t *__restrict__ seg_of,
+                                                  const uint32_t *__restrict__ seg_start,
+                                                  uint32_t N, uint32_t S,
+                                                  uint32_t *__restrict__ seg_perm) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t g, sg;
+  if (x < N) {
+    sg = seg_of[x];
+    g = x + sg + 1;
+  } else if (x < N + S) {
+    sg = x - N;
+    g = seg_start[sg] + sg;
+  } else {
+    return;
+  }
+  const uint64_t o = seg_off[sg];
+  seg_perm[g] = lmap[o + lperm[g]];
+}
+
+// active-node (map.cljc:47-59) per key weave, and the collection status.
+// Scans the key weave from its first node; in practice it stops within a few.
+__global__ __launch_bounds__(256) void k_seg_active(
+    const uint32_t *__restrict__ lperm, const uint8_t *__restrict__ lkind,
+    const uint32_t *__restrict__ seg_perm, const uint64_t *__restrict__ seg_off,
+    const uint32_t *__restrict__ seg_coll, const uint32_t *__restrict__ lstatus, uint32_t S,
+    int64_t *__restrict__ seg_active, uint32_t *__restrict__ status) {
+  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sg >= S) return;
+  const uint64_t o = seg_off[sg];
+  const uint32_t len = (uint32_t)(seg_off[sg + 1] - o);
+  auto kd = [&](uint32_t p) { return (uint32_t)lkind[o + lperm[o + p]]; };
+  int64_t act = -1;
+  // [_ [_ _ first-v]]: a hide right after the root blanks the key
+  if (!(len > 1 && is_hide(kd(1)))) {
+    uint32_t k = len > 1 ? kd(1) : 0u;
+    for (uint32_t p = 1; p < len; p++) {
+      const uint32_t nk = p + 1 < len ? kd(p + 1) : 0u;
+      if (!is_special(k) && !(p + 1 < len && is_hide(nk))) {
+        act = (int64_t)seg_perm[o + p];
+        break;
+      }
+      k = nk;
+    }
+  }
+  seg_active[sg] = act;
+  if (lstatus[sg]) atomicOr(&status[seg_coll[sg]], lstatus[sg]);
 }
 
 // ============================================================================
@@ -921,13 +1173,13 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
     }
     // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
-    uint32_t log2k = c->min_log2k, log2cap = std::max(log2k + 1, c->min_log2cap);
+    uint32_t log2k = c->min_log2k, log2cap = c->min_log2cap;
     auto subl = [&]() {
       return 2 * (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
     };
     while (subl() > MAX_SUBLISTS) {
-      if (log2k + 1 < log2cap) log2k++;
+      if (log2k < log2cap) log2k++;
       else log2cap++;
     }
     const uint32_t S = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;
@@ -1074,6 +1326,33 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
   return 0;
 }
 
+// Significant bits of a device array of keys (one OR reduction + 8-byte D2H).
+int find_key_bits(cw_ctx *c, const uint64_t *keys, uint32_t N, uint32_t *bits) {
+  unsigned long long *red = scratch_t<unsigned long long>(c, "red", 1);
+  if (!red) return fail(c, "out of device memory (red)");
+  HIPCHK(c, hipMemsetAsync(red, 0, 8, c->stream));
+  hipLaunchKernelGGL(k_or_reduce, dim3(1024), dim3(256), 0, c->stream, keys, N, red);
+  if (check_launch(c, "or_reduce")) return -1;
+  unsigned long long v = 0;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(&v, red, 8, hipMemcpyDeviceToHost));
+  *bits = v ? 64 - __builtin_clzll(v) : 1;
+  return 0;
+}
+
+// Host tables for a document layout, rebuilt only when the layout changes.
+int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
+  const bool same = c->tab_on_device && c->last_off.size() == D + 1 &&
+                    memcmp(c->last_off.data(), off, (D + 1) * 8) == 0;
+  if (same) return 0;
+  c->tab_on_device = false;
+  build_tables(c, D, off);
+  if (upload_tables(c)) return -1;
+  c->last_off.assign(off, off + D + 1);
+  c->tab_on_device = true;
+  return 0;
+}
+
 int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_key,
                        const uint64_t *cause_key, const uint8_t *kind, cw_list_result *out) {
   const uint64_t D = bt->n_docs;
@@ -1087,17 +1366,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
 
   uint32_t key_bits = bt->key_bits;
-  if (key_bits == 0 && N) {
-    unsigned long long *red = scratch_t<unsigned long long>(c, "red", 1);
-    if (!red) return fail(c, "out of device memory (red)");
-    HIPCHK(c, hipMemsetAsync(red, 0, 8, c->stream));
-    hipLaunchKernelGGL(k_or_reduce, dim3(1024), B256, 0, c->stream, id_key, N, red);
-    if (check_launch(c, "or_reduce")) return -1;
-    unsigned long long v = 0;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(&v, red, 8, hipMemcpyDeviceToHost));
-    key_bits = v ? 64 - __builtin_clzll(v) : 1;
-  }
+  if (key_bits == 0 && N && find_key_bits(c, id_key, N, &key_bits)) return -1;
   if (key_bits > 64) key_bits = 64;
 
   uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
@@ -1113,8 +1382,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
   uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
   uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
+  uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
   if (!skA || !skB || !svA || !svB || !par || !epar || !skind ||
-      !nsc || !fcS || !fcN || !link || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase)
+      !nsc || !fcS || !fcN || !link || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase || !order)
     return fail(c, "out of device memory (N=%u)", N);
 
   uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc");
@@ -1160,7 +1430,11 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       // special/hide bitmaps in LDS for documents up to 2^18 nodes
       const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
       Launch L(c, "tree", (double)N * (4 + 1 + 8 + 4 + 4 + 8 + 4 + 4 + 4 + 4 + 8));
-      if (c->tree_cfg == 1)
+      if (c->tree_cfg == 2)
+        hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
+                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
+                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
+      else if (c->tree_cfg == 1)
         hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
                            (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
                            kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
@@ -1188,7 +1462,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       Launch L(c, "rank", (double)t.Wtot * 12);
       hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
                          wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, bt->ts_shift, sbase,
-                         out->max_ts, out->status);
+                         order, out->max_ts, out->status);
     }
     if (check_launch(c, "rank")) return -1;
 
@@ -1196,7 +1470,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     {
       Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
       hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
-                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, sval,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
                          dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
                          dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
                          out->visible_count, out->status);
@@ -1249,14 +1523,7 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   HIPCHK(c, hipSetDevice(c->device));
 
   // host tables (cached while the document layout repeats)
-  bool same = c->tab_on_device && c->last_off.size() == D + 1 &&
-              memcmp(c->last_off.data(), bt->doc_offsets, (D + 1) * 8) == 0;
-  if (!same) {
-    build_tables(c, D, bt->doc_offsets);
-    if (upload_tables(c)) return -1;
-    c->last_off.assign(bt->doc_offsets, bt->doc_offsets + D + 1);
-    c->tab_on_device = true;
-  }
+  if (ensure_tables(c, D, bt->doc_offsets)) return -1;
 
   const uint64_t *id = bt->id_key, *cause = bt->cause_key;
   const uint8_t *kind = bt->kind;
@@ -1317,6 +1584,200 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   return 0;
 }
 
+// Key weaves of at most this many documents / nodes go through one list call
+// (keeps every launch grid of the list pipeline inside the dispatch limits).
+constexpr uint64_t MAP_CHUNK_DOCS = 1ull << 20, MAP_CHUNK_NODES = 1ull << 30;
+
+int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int memspace) {
+  if (!bt || !res) return fail(c, "null batch/result");
+  if (memspace != CW_MEM_HOST) return fail(c, "cw_weave_maps: only CW_MEM_HOST is supported");
+  const uint64_t D = bt->n_colls;
+  if (!bt->coll_offsets) return fail(c, "coll_offsets is required (host memory)");
+  if (bt->coll_offsets[0] != 0) return fail(c, "coll_offsets[0] must be 0");
+  const uint64_t N64 = bt->coll_offsets[D];
+  // key weaves add one root each: N + S <= 2N must stay below 2^32
+  if (N64 >= 0x7FFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^31-1)",
+                                        (unsigned long long)N64);
+  for (uint64_t d = 0; d < D; d++) {
+    if (bt->coll_offsets[d + 1] < bt->coll_offsets[d]) return fail(c, "coll_offsets not monotone");
+    if (bt->coll_offsets[d + 1] - bt->coll_offsets[d] >= LINK_IDX)
+      return fail(c, "collection %llu too large", (unsigned long long)d);
+  }
+  if (!res->seg_offsets || !res->seg_coll || !res->seg_key || !res->seg_active ||
+      !res->seg_perm || !res->status)
+    return fail(c, "every cw_map_result array is required");
+  if (bt->token_bits == 0 || bt->token_bits > 62) return fail(c, "token_bits must be 1..62");
+  const uint32_t N = (uint32_t)N64;
+  HIPCHK(c, hipSetDevice(c->device));
+  res->n_segs = 0;
+  res->seg_offsets[0] = 0;
+  if (N == 0) {
+    memset(res->status, 0, D * 4);
+    return 0;
+  }
+  if (!bt->id_key || !bt->cause || !bt->cause_is_id || !bt->kind)
+    return fail(c, "null input arrays");
+
+  // collection tables: id sort, key resolution and key grouping run per collection
+  if (ensure_tables(c, D, bt->coll_offsets)) return -1;
+  auto &t = c->tab;
+  const uint32_t T = t.T;
+  uint64_t *id = scratch_t<uint64_t>(c, "m_id", N), *cause = scratch_t<uint64_t>(c, "m_cause", N);
+  uint8_t *cis = scratch_t<uint8_t>(c, "m_cis", N), *kind = scratch_t<uint8_t>(c, "m_kind", N);
+  uint32_t *status = scratch_t<uint32_t>(c, "m_status", D);
+  uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
+  uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
+  uint64_t *segk = scratch_t<uint64_t>(c, "m_segk", N);
+  uint32_t *mpar = scratch_t<uint32_t>(c, "m_mpar", N);
+  uint8_t *mkind = scratch_t<uint8_t>(c, "m_mkind", N);
+  uint64_t *kA = scratch_t<uint64_t>(c, "m_kA", N), *kB = scratch_t<uint64_t>(c, "m_kB", N);
+  uint32_t *vA = scratch_t<uint32_t>(c, "m_vA", N), *vB = scratch_t<uint32_t>(c, "m_vB", N);
+  uint32_t *tcnt = scratch_t<uint32_t>(c, "m_tcnt", T), *tsb = scratch_t<uint32_t>(c, "m_tsb", T);
+  uint32_t *seg_of = scratch_t<uint32_t>(c, "m_segof", N);
+  if (!id || !cause || !cis || !kind || !status || !skA || !skB || !svA || !svB || !segk ||
+      !mpar || !mkind || !kA || !kB || !vA || !vB || !tcnt || !tsb || !seg_of)
+    return fail(c, "out of device memory (maps, N=%u)", N);
+  if (!grid_ok(T, SORT_THREADS) || !grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
+
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(id, bt->id_key, (size_t)N * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(cause, bt->cause, (size_t)N * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(cis, bt->cause_is_id, N, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(kind, bt->kind, N, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemsetAsync(status, 0, D * 4, c->stream));
+  uint32_t key_bits = bt->key_bits;
+  if (key_bits == 0 && find_key_bits(c, id, N, &key_bits)) return -1;
+  if (key_bits > 62) return fail(c, "map ids need %u bits (limit 62)", key_bits);
+  const uint32_t W = std::max(bt->token_bits, key_bits);
+
+  // 1. (sort (::s/nodes ct)) per collection -- map.cljc:28
+  uint64_t *skey;
+  uint32_t *sval;
+  if (radix_sort<uint64_t>(c, "m_idsort", id, nullptr, skA, svA, skB, svB, key_bits, 0, N, &skey,
+                           &sval))
+    return -1;
+  // 2. key and cause-in-weave per node -- map.cljc:31-37
+  {
+    Launch L(c, "m_key", (double)N * (8 + 4 + 8 + 1 + 1 + 8 + 4 + 1) + (double)N * 2 * 8);
+    hipLaunchKernelGGL(k_map_key, dim3(T), dim3(256), 0, c->stream, skey, sval, cause, cis, kind,
+                       dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
+                       dev_tab(c, "t_doc_off"), bt->token_bits, W, segk, mpar, mkind, status);
+  }
+  if (check_launch(c, "m_key")) return -1;
+  // 3. stable grouping by key (id order kept inside a key)
+  uint64_t *ks;
+  uint32_t *rank_s;
+  if (radix_sort<uint64_t>(c, "m_keysort", segk, nullptr, kA, vA, kB, vB, W + 2, 0, N, &ks,
+                           &rank_s))
+    return -1;
+  {
+    Launch L(c, "m_segcount", (double)N * 8);
+    hipLaunchKernelGGL(k_seg_count, dim3(T), dim3(256), 0, c->stream, ks,
+                       dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
+                       dev_tab(c, "t_doc_off"), tcnt);
+  }
+  if (check_launch(c, "m_segcount")) return -1;
+  std::vector<uint32_t> h_tsb(T);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(h_tsb.data(), tcnt, (size_t)T * 4, hipMemcpyDeviceToHost));
+  uint64_t S = 0;
+  for (uint32_t i = 0; i < T; i++) {
+    const uint32_t v = h_tsb[i];
+    h_tsb[i] = (uint32_t)S;
+    S += v;
+  }
+  if (S > res->cap_segs)
+    return fail(c, "cap_segs too small: %llu key weaves", (unsigned long long)S);
+  HIPCHK(c, hipMemcpy(tsb, h_tsb.data(), (size_t)T * 4, hipMemcpyHostToDevice));
+  uint32_t *seg_start = scratch_t<uint32_t>(c, "m_segstart", S + 1);
+  uint32_t *seg_coll = scratch_t<uint32_t>(c, "m_segcoll", S);
+  uint64_t *seg_key = scratch_t<uint64_t>(c, "m_segkey", S);
+  const size_t NL = (size_t)N + S;
+  uint64_t *lid = scratch_t<uint64_t>(c, "m_lid", NL), *lcause = scratch_t<uint64_t>(c, "m_lcause", NL);
+  uint8_t *lkind = scratch_t<uint8_t>(c, "m_lkind", NL);
+  uint32_t *lmap = scratch_t<uint32_t>(c, "m_lmap", NL), *lperm = scratch_t<uint32_t>(c, "m_lperm", NL);
+  uint32_t *lvc = scratch_t<uint32_t>(c, "m_lvc", S), *lst = scratch_t<uint32_t>(c, "m_lst", S);
+  uint64_t *seg_off = scratch_t<uint64_t>(c, "m_segoff", S + 1);
+  uint32_t *seg_perm = scratch_t<uint32_t>(c, "m_segperm", NL);
+  int64_t *seg_act = scratch_t<int64_t>(c, "m_segact", S);
+  if (!seg_start || !seg_coll || !seg_key || !lid || !lcause || !lkind || !lmap || !lperm || !lvc ||
+      !lst || !seg_off || !seg_perm || !seg_act)
+    return fail(c, "out of device memory (maps, S=%llu)", (unsigned long long)S);
+  {
+    Launch L(c, "m_segmark", (double)N * (8 + 4) + (double)S * (4 + 4 + 8));
+    hipLaunchKernelGGL(k_seg_mark, dim3(T), dim3(256), 0, c->stream, ks,
+                       dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
+                       dev_tab(c, "t_doc_off"), tsb, W, seg_of, seg_start, seg_coll, seg_key);
+  }
+  if (check_launch(c, "m_segmark")) return -1;
+  {
+    Launch L(c, "m_segbuild", (double)N * (4 + 4 + 4 + 8 + 4 + 8 + 1 + 8 + 8 + 1 + 4));
+    hipLaunchKernelGGL(k_seg_build, dim3((N + 255) / 256), dim3(256), 0, c->stream, skey, sval,
+                       mpar, mkind, rank_s, seg_of, seg_coll, dev_tab(c, "t_doc_off"), N, lid,
+                       lcause, lkind, lmap);
+  }
+  if (check_launch(c, "m_segbuild")) return -1;
+  hipLaunchKernelGGL(k_seg_roots, dim3((uint32_t)((S + 255) / 256)), dim3(256), 0, c->stream,
+                     seg_start, (uint32_t)S, lid, lcause, lkind, lmap);
+  if (check_launch(c, "m_segroots")) return -1;
+
+  // key weave s = list document [seg_start[s] + s, seg_start[s+1] + s + 1)
+  std::vector<uint32_t> h_start(S);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(h_start.data(), seg_start, S * 4, hipMemcpyDeviceToHost));
+  uint64_t *loff = res->seg_offsets;
+  for (uint64_t sg = 0; sg < S; sg++) loff[sg] = h_start[sg] + sg;
+  loff[S] = NL;
+  HIPCHK(c, hipMemcpy(seg_off, loff, (S + 1) * 8, hipMemcpyHostToDevice));
+
+  // 4. every key weave is a list weave -- (s/weave-node key-weave ...), map.cljc:40-41
+  std::vector<uint64_t> rel;
+  for (uint64_t s0 = 0; s0 < S;) {
+    uint64_t s1 = s0 + 1;
+    while (s1 < S && s1 - s0 < MAP_CHUNK_DOCS && loff[s1 + 1] - loff[s0] <= MAP_CHUNK_NODES) s1++;
+    rel.resize(s1 - s0 + 1);
+    for (uint64_t sg = s0; sg <= s1; sg++) rel[sg - s0] = loff[sg] - loff[s0];
+    if (ensure_tables(c, s1 - s0, rel.data())) return -1;
+    cw_list_batch lb{};
+    lb.n_docs = s1 - s0;
+    lb.doc_offsets = rel.data();
+    lb.key_bits = key_bits;
+    cw_list_result lr{};
+    lr.weave_perm = lperm + loff[s0];
+    lr.visible_count = lvc + s0;
+    lr.status = lst + s0;
+    if (weave_lists_device(c, &lb, lid + loff[s0], lcause + loff[s0], lkind + loff[s0], &lr))
+      return -1;
+    s0 = s1;
+  }
+
+  // 5. key weaves in collection-local input indices, active-node per key
+  {
+    Launch L(c, "m_segperm", (double)N * (4 + 4 + 8 + 4 + 4) + (double)S * 4);
+    hipLaunchKernelGGL(k_seg_perm, dim3((uint32_t)((NL + 255) / 256)), dim3(256), 0, c->stream,
+                       lperm, lmap, seg_off, seg_of, seg_start, N, (uint32_t)S, seg_perm);
+  }
+  if (check_launch(c, "m_segperm")) return -1;
+  {
+    Launch L(c, "m_active", (double)S * (16 + 4 + 4 + 8 + 3 * 9));
+    hipLaunchKernelGGL(k_seg_active, dim3((uint32_t)((S + 255) / 256)), dim3(256), 0, c->stream,
+                       lperm, lkind, seg_perm, seg_off, seg_coll, lst, (uint32_t)S, seg_act,
+                       status);
+  }
+  if (check_launch(c, "m_active")) return -1;
+
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(res->seg_perm, seg_perm, NL * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(res->seg_coll, seg_coll, S * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(res->seg_key, seg_key, S * 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(res->seg_active, seg_act, S * 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(res->status, status, D * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipDeviceSynchronize());
+  res->n_segs = S;
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -1350,7 +1811,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
   c->min_log2cap = knob("CW_LOG2CAP", 4);
-  c->tree_cfg = knob("CW_TREE", 0);
+  c->tree_cfg = knob("CW_TREE", 1);
   c->join_lds = knob("CW_JOIN_LDS", 0);
 
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
@@ -1415,6 +1876,12 @@ int cw_weave_lists(cw_ctx *c, const cw_list_batch *b, cw_list_result *r, int mem
   c->err.clear();
   if (memspace != CW_MEM_HOST && memspace != CW_MEM_DEVICE) return fail(c, "bad memspace");
   return weave_lists_impl(c, b, r, memspace);
+}
+
+int cw_weave_maps(cw_ctx *c, const cw_map_batch *b, cw_map_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  return weave_maps_impl(c, b, r, memspace);
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <thread>
 #include <vector>
 
@@ -135,9 +136,117 @@ struct DocGen {
   }
 };
 
+struct MapGen {
+  std::vector<uint32_t> ts, site, order, values, idcaused, cnode;
+  std::vector<uint64_t> token;
+  std::vector<uint8_t> cis, kind;
+
+  void run(const cwg_map_params &p, const std::vector<double> &cdf, uint64_t d, uint32_t site_bits,
+           uint64_t *idk, uint64_t *ck, uint8_t *ci, uint8_t *kd) {
+    const uint32_t n = p.nodes_per_coll;
+    ts.assign(n, 0);
+    site.assign(n, 0);
+    cnode.assign(n, 0);
+    token.assign(n, 0);
+    cis.assign(n, 0);
+    kind.assign(n, 0);
+    values.clear();
+    idcaused.clear();
+    Rng rng(mix(p.seed ^ (d * 0x2545F4914F6CDD1Dull)));
+    std::vector<uint32_t> clock(p.n_sites + 1, 0);
+    auto pick_key = [&]() {
+      const double u = rng.uni() * cdf.back();
+      return (uint64_t)(std::lower_bound(cdf.begin(), cdf.end(), u) - cdf.begin());
+    };
+    const double q_id = p.p_hhide + p.p_hshow, q_bad = q_id + p.p_bad, q_hide = q_bad + p.p_hide;
+    for (uint32_t m = 0; m < n; m++) {
+      const uint32_t s = 1 + rng.below(p.n_sites);
+      const double u = rng.uni();
+      uint32_t cts = 0;
+      if (u < q_id && !values.empty()) {
+        const uint32_t c = values[rng.below((uint32_t)values.size())];
+        kind[m] = u < p.p_hhide ? K_HHIDE : K_HSHOW;
+        cis[m] = 1;
+        cnode[m] = c;
+        cts = ts[c];
+        idcaused.push_back(m);
+      } else if (u >= q_id && u < q_bad && !idcaused.empty()) {
+        const uint32_t c = idcaused[rng.below((uint32_t)idcaused.size())];
+        kind[m] = K_HHIDE;
+        cis[m] = 1;
+        cnode[m] = c;
+        cts = ts[c];
+      } else {
+        kind[m] = (u >= q_bad && u < q_hide) ? K_HIDE : K_NORMAL;
+        token[m] = pick_key();
+        if (kind[m] == K_NORMAL) values.push_back(m);
+      }
+      const uint32_t t = std::max(clock[s], cts) + 1;
+      clock[s] = t;
+      ts[m] = t;
+      site[m] = s;
+      if (p.sync_every && (m + 1) % p.sync_every == 0) {
+        uint32_t mx = 0;
+        for (uint32_t x : clock) mx = std::max(mx, x);
+        std::fill(clock.begin(), clock.end(), mx);
+      }
+    }
+    order.resize(n);
+    for (uint32_t i = 0; i < n; i++) order[i] = i;
+    if (p.shuffle && n > 1)
+      for (uint32_t i = n - 1; i > 0; i--) std::swap(order[i], order[rng.below(i + 1)]);
+    for (uint32_t j = 0; j < n; j++) {
+      const uint32_t i = order[j];
+      idk[j] = ((uint64_t)ts[i] << site_bits) | site[i];
+      ck[j] = cis[i] ? (((uint64_t)ts[cnode[i]] << site_bits) | site[cnode[i]]) : token[i];
+      ci[j] = cis[i];
+      kd[j] = kind[i];
+    }
+  }
+};
+
 }  // namespace
 
 extern "C" {
+
+void cwg_map_layout(const cwg_map_params *p, uint32_t *ts_bits, uint32_t *site_bits,
+                    uint32_t *token_bits) {
+  *ts_bits = bits_for(p->nodes_per_coll);
+  *site_bits = bits_for(p->n_sites);
+  *token_bits = std::max<uint32_t>(1, bits_for(p->n_keys ? p->n_keys - 1 : 0));
+}
+
+int cwg_map_generate(const cwg_map_params *p, uint64_t coll_begin, uint64_t coll_end,
+                     uint64_t *id_key, uint64_t *cause, uint8_t *cause_is_id, uint8_t *kind,
+                     int nthreads) {
+  if (!p || coll_end < coll_begin || p->n_sites == 0 || p->n_keys == 0) return -1;
+  uint32_t tsb, sb, tb;
+  cwg_map_layout(p, &tsb, &sb, &tb);
+  std::vector<double> cdf(p->n_keys);
+  double acc = 0;
+  for (uint32_t k = 0; k < p->n_keys; k++) {
+    acc += 1.0 / std::pow((double)(k + 1), p->zipf_s);
+    cdf[k] = acc;
+  }
+  const uint64_t n = p->nodes_per_coll;
+  std::atomic<uint64_t> next{coll_begin};
+  auto work = [&]() {
+    MapGen g;
+    for (;;) {
+      const uint64_t d = next.fetch_add(1);
+      if (d >= coll_end) break;
+      const uint64_t o = (d - coll_begin) * n;
+      g.run(*p, cdf, d, sb, id_key + o, cause + o, cause_is_id + o, kind + o);
+    }
+  };
+  if (nthreads < 1) nthreads = 1;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; t++) th.emplace_back(work);
+  work();
+  for (auto &t : th) t.join();
+  return 0;
+}
+
 
 void cwg_layout(const cwg_params *p, uint32_t *ts_bits, uint32_t *site_bits) {
   *ts_bits = bits_for(p->nodes_per_doc);  // ts <= number of non-root nodes

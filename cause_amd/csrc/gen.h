@@ -41,6 +41,31 @@ void cwg_layout(const cwg_params *p, uint32_t *ts_bits, uint32_t *site_bits);
 int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint64_t *id_key,
                  uint64_t *cause_key, uint8_t *kind, int nthreads);
 
+/* Maps: each collection holds `nodes_per_coll` nodes
+ * typed by `n_sites` sites over `n_keys` key tokens drawn Zipf(zipf_s):
+ *   - key-level :causal/hide (p_hide, cause = the key token, dissoc-)
+ *   - id-caused :causal/h.hide (p_hhide) / :causal/h.show (p_hshow), cause = a
+ *     random earlier value write of the collection (undo/redo)
+ *   - otherwise a value write (cause = the key token, assoc-)
+ *   - p_bad: id-caused nodes whose cause is itself id-caused
+ * cause_is_id[i] says whether cause[i] is a packed id or a key token. */
+typedef struct {
+  uint32_t nodes_per_coll;
+  uint32_t n_sites;
+  uint32_t n_keys;
+  double zipf_s;
+  double p_hide, p_hhide, p_hshow, p_bad;
+  uint32_t sync_every;
+  uint64_t seed;
+  int shuffle;
+} cwg_map_params;
+
+void cwg_map_layout(const cwg_map_params *p, uint32_t *ts_bits, uint32_t *site_bits,
+                    uint32_t *token_bits);
+int cwg_map_generate(const cwg_map_params *p, uint64_t coll_begin, uint64_t coll_end,
+                     uint64_t *id_key, uint64_t *cause, uint8_t *cause_is_id, uint8_t *kind,
+                     int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -169,3 +169,68 @@ def pack_lists(docs) -> PackedBatch:
                          else np.zeros(0, dt))
     return PackedBatch(off, cat("id_key", np.uint64), cat("cause_key", np.uint64),
                        cat("kind", np.uint8), lay, packed)
+
+
+SITE_ID_LENGTH = 13  # shared.cljc:29
+
+
+def valid_id(x) -> bool:
+    """``(spec/valid? ::s/id x)`` (shared.cljc:31-40): [nat site-id nat] with a
+    13-character site-id or "0".  A map cause that is not a valid id is a key
+    (map.cljc:31)."""
+    if not (isinstance(x, tuple) and len(x) == 3):
+        return False
+    ts, site, tx = x
+    nat = lambda v: isinstance(v, int) and not isinstance(v, bool) and v >= 0
+    return nat(ts) and nat(tx) and isinstance(site, str) and (
+        len(site) == SITE_ID_LENGTH or site == "0")
+
+
+@dataclass
+class PackedMaps:
+    offsets: np.ndarray      # uint64 [D+1]
+    id_key: np.ndarray       # uint64 [N]
+    cause: np.ndarray        # uint64 [N] packed id or key token
+    cause_is_id: np.ndarray  # uint8  [N]
+    kind: np.ndarray         # uint8  [N]
+    layout: KeyLayout
+    token_bits: int
+    keys: list               # token -> key value
+    docs: list               # nodes per collection, in the packed order
+    ranks: list              # site rank table per collection
+
+
+def pack_maps(docs) -> PackedMaps:
+    """Pack a batch of map collections (each an iterable of ``(id, cause, value)``
+    nodes; maps have no root node of their own).  Keys get batch-wide tokens in
+    first-appearance order; the virtual root [[0 "0" 0] nil nil] packs to 0, so
+    "0" must be the smallest site-id (true of every u/new-uid, util.cljc:12-23)."""
+    docs = [list(d) for d in docs]
+    lay = layout_for([[(n[0], n[1] if valid_id(n[1]) else None, n[2]) for n in d]
+                      + [((0, "0", 0), None, None)] for d in docs])
+    tok = {}
+    off = np.zeros(len(docs) + 1, np.uint64)
+    N = sum(len(d) for d in docs)
+    idk, ck = np.empty(N, np.uint64), np.empty(N, np.uint64)
+    ci, kd = np.empty(N, np.uint8), np.empty(N, np.uint8)
+    ranks = []
+    j = 0
+    for d, nodes in enumerate(docs):
+        ids = [n[0] for n in nodes] + [n[1] for n in nodes if valid_id(n[1])] + [ROOT_ID]
+        rank = intern_sites(ids)
+        if rank["0"] != 0:
+            raise KeyRangeError('a site-id sorts before "0": the virtual root must pack to 0')
+        ranks.append(rank)
+        for nid, cause, value in nodes:
+            idk[j] = lay.pack(nid[0], rank[nid[1]], nid[2])
+            if valid_id(cause):
+                ck[j] = lay.pack(cause[0], rank[cause[1]], cause[2])
+                ci[j] = 1
+            else:
+                ck[j] = tok.setdefault(cause, len(tok))
+                ci[j] = 0
+            kd[j] = kind_of(value)
+            j += 1
+        off[d + 1] = j
+    token_bits = max(1, _bits(max(len(tok) - 1, 0)))
+    return PackedMaps(off, idk, ck, ci, kd, lay, token_bits, list(tok), docs, ranks)

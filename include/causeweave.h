@@ -45,6 +45,7 @@ extern "C" {
 
 #define CW_ABI_VERSION 1
 #define CW_NIL UINT64_MAX
+#define CW_MAP_ID_KEY (1ull << 63) /* map key weave keyed by an id */
 
 /* Node value class (shared.cljc:21 special-keywords) | CW_KIND_ROOT. */
 enum {
@@ -61,6 +62,8 @@ enum {
   CW_STATUS_DUP = 1u << 1,         /* two nodes share an id (shared.cljc:166-171)          */
   CW_STATUS_ORPHAN = 1u << 2,      /* a cause is not in the document (shared.cljc:175-178) */
   CW_STATUS_NON_LAMPORT = 1u << 3, /* a cause id is not older than its node                */
+  CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits, or a node caused by
+                                      the root id (its key weave mixes children and orphans) */
   CW_STATUS_INTERNAL = 1u << 5     /* consistency check failed inside the pipeline         */
 };
 
@@ -127,6 +130,49 @@ typedef struct {
  * cause_key / kind and every result array live (doc_offsets is always host). */
 int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
                    int memspace);
+
+/* ----------------------------------------------------------------- maps ---- */
+/* Full reweave of a batch of CausalMaps (c.map/weave 1-arity, map.cljc:26-45)
+ * and last-writer-wins per key (active-node, map.cljc:47-59).
+ *
+ * Each node's cause is either a packed id (cause_is_id = 1: (spec/valid? ::s/id
+ * cause), map.cljc:31) or a key token (an opaque key rank, < 2^token_bits).  A
+ * key-caused node is woven under the key's virtual root [[0 "0" 0] nil nil]
+ * (map.cljc:35-40), whose packed id is 0 (site "0" interns to rank 0, ts 0);
+ * an id-caused node lands in the weave of its cause node's key (map.cljc:32-34).
+ * The reference's quirky keys are reproduced: when the cause
+ * node is itself id-caused by X the key is the id X (seg_key = CW_MAP_ID_KEY |
+ * packed X), and when the cause node is absent the key is nil (seg_key =
+ * CW_NIL).  Every key weave is a list weave; the active node is its first
+ * rendered node, blank when the root's first child is a hide.  Key weaves are
+ * returned per collection in ascending seg_key order.  Ids and tokens must fit
+ * 62 bits. */
+typedef struct {
+  uint64_t n_colls;
+  const uint64_t *coll_offsets; /* HOST memory, [n_colls+1]                                */
+  const uint64_t *id_key;       /* [N] packed ids (< 2^63)                                 */
+  const uint64_t *cause;        /* [N] packed cause id, or key token                       */
+  const uint8_t *cause_is_id;   /* [N] 1 = cause is an id                                  */
+  const uint8_t *kind;          /* [N] CW_KIND_* (no root: maps have a virtual root)      */
+  uint32_t key_bits;            /* significant bits of id keys (0 = find on the device)   */
+  uint32_t token_bits;          /* significant bits of key tokens                         */
+} cw_map_batch;
+
+typedef struct {
+  uint64_t cap_segs;      /* IN: capacity of the per-key-weave arrays (N suffices)         */
+  uint64_t n_segs;        /* OUT: number of key weaves                                     */
+  uint64_t *seg_offsets;  /* [cap_segs+1]: key weave s = seg_perm[seg_offsets[s] ..)        */
+  uint32_t *seg_coll;     /* [cap_segs] collection of key weave s                          */
+  uint64_t *seg_key;      /* [cap_segs] key token of key weave s                           */
+  int64_t *seg_active;    /* [cap_segs] collection-local input index of the active node,
+                             -1 = ::blank                                                   */
+  uint32_t *seg_perm;     /* [N + cap_segs] weave order of every key weave: the root
+                             (UINT32_MAX) then collection-local input indices               */
+  uint32_t *status;       /* [n_colls] CW_STATUS_* bits                                     */
+} cw_map_result;
+
+/* Host memory only (memspace must be CW_MEM_HOST in this version). */
+int cw_weave_maps(cw_ctx *ctx, const cw_map_batch *batch, cw_map_result *result, int memspace);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,223 @@
+"""GPU parity of cw_weave_maps (c.map/weave 1-arity + active-node, map.cljc:26-59)
+against the C oracle's literal fold (oracle/weave_oracle.c or_map_fold_literal,
+pinned to the Python restatement and map_test.cljc in test_oracle.py).
+
+Compared per collection and key: the key weave (node order, root first) and
+the active node (LWW, -1 = ::blank), including the reference's quirky keys
+(a key that is an id, or nil).  Collections the library flags
+(duplicate ids, nodes caused by the root id) are out of domain: the flag
+itself is checked against the host's own reading.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from cause_amd import abi, gen
+
+pytestmark = pytest.mark.gpu
+
+NO_ROOT = 0xFFFFFFFF
+ID_KEY = 1 << 63
+NIL = (1 << 64) - 1
+
+
+@pytest.fixture(scope="module")
+def weaver():
+    w = abi.Weaver(0)
+    yield w
+    w.close()
+
+
+def oracle_maps(off, idk, ck, ci, kd):
+    """Per collection: {key: (active, [input idx in weave order])}, keys in the
+    ABI's form (token, ID_KEY | id, or NIL)."""
+    out = []
+    for d in range(len(off) - 1):
+        a, b = int(off[d]), int(off[d + 1])
+        nk, npos, sk, sa = oracle.map_weave(idk[a:b], ck[a:b], ci[a:b], kd[a:b], 0)
+        ids = {int(x): j for j, x in enumerate(idk[a:b])}
+        api = {}
+        for j in range(b - a):
+            k = int(nk[j])
+            if ci[a + j]:
+                c = ids.get(int(ck[a + j]))
+                if c is not None and ci[a + c]:
+                    api[k] = ID_KEY | k        # key = the cause node's cause id
+        order = np.lexsort((npos, nk))
+        groups = {}
+        for j in order:
+            groups.setdefault(int(nk[j]), []).append(int(j))
+        out.append({api.get(int(k), int(k)): (int(act), groups.get(int(k), []))
+                    for k, act in zip(sk, sa)})
+    return out
+
+
+def gpu_maps(res, D):
+    out = [dict() for _ in range(D)]
+    for s in range(len(res.seg_key)):
+        kw = res.key_weave(s)
+        assert kw[0] == NO_ROOT, "key weave must start at its root"
+        out[int(res.seg_coll[s])][int(res.seg_key[s])] = (int(res.seg_active[s]),
+                                                           [int(x) for x in kw[1:]])
+    return out
+
+
+def expected_flags(off, idk, ck, ci):
+    """Host reading of the map domain: duplicate ids, root-id causes."""
+    flags = np.zeros(len(off) - 1, np.uint32)
+    for d in range(len(off) - 1):
+        a, b = int(off[d]), int(off[d + 1])
+        if len(set(idk[a:b].tolist())) != b - a:
+            flags[d] |= abi.STATUS_DUP
+        if ((ci[a:b] == 1) & (ck[a:b] == 0)).any():
+            flags[d] |= abi.STATUS_MAP_KEY
+    return flags
+
+
+def check(weaver, off, idk, ck, ci, kd, token_bits, key_bits=0, flags=None):
+    res = weaver.weave_maps(off, idk, ck, ci, kd, token_bits, key_bits)
+    D = len(off) - 1
+    if flags is None:
+        flags = expected_flags(off, idk, ck, ci)
+    np.testing.assert_array_equal(res.status & (abi.STATUS_MAP_KEY | abi.STATUS_DUP), flags)
+    got, want = gpu_maps(res, D), oracle_maps(off, idk, ck, ci, kd)
+    for d in range(D):
+        if flags[d]:
+            continue
+        assert res.status[d] == 0, (d, res.status[d])
+        assert got[d] == want[d], f"collection {d}"
+    # key weaves come per collection in ascending key order
+    sc, sk = res.seg_coll.astype(np.uint64), res.seg_key
+    assert np.all((sc[1:] > sc[:-1]) | ((sc[1:] == sc[:-1]) & (sk[1:] > sk[:-1])))
+    return res
+
+
+def test_config4_shape(weaver):
+    spec = gen.CONFIG4
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 3000, nthreads=8)
+    res = check(weaver, off, idk, ck, ci, kd, tb)
+    assert (res.status == 0).all()
+
+
+def test_large_collections_few_keys(weaver):
+    # long key weaves: few keys, many writes and id-caused undo/redo per key
+    spec = gen.MapSpec(nodes_per_coll=20_000, n_keys=5, zipf_s=0.5, seed=11)
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 6, nthreads=6)
+    check(weaver, off, idk, ck, ci, kd, tb)
+
+
+def test_many_keys(weaver):
+    spec = gen.MapSpec(nodes_per_coll=3000, n_keys=60_000, zipf_s=0.2, seed=12)
+    _, tb = spec.layout()
+    assert tb == 16
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 20, nthreads=8)
+    check(weaver, off, idk, ck, ci, kd, tb)
+
+
+def test_f8c_id_keys(weaver):
+    """a node whose cause node is itself id-caused lands in a weave
+    keyed by that id, appended there as an orphan."""
+    spec = gen.MapSpec(nodes_per_coll=60, p_bad=0.05, seed=13)
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 400, nthreads=8)
+    res = check(weaver, off, idk, ck, ci, kd, tb)
+    assert (res.status == 0).all()
+    n_id = int(((res.seg_key & np.uint64(ID_KEY)) != 0).sum())
+    assert 50 < n_id < len(res.seg_key)
+
+
+def test_ragged_and_empty_collections(weaver):
+    rng = np.random.default_rng(5)
+    parts = []
+    sizes = [0, 1, 2, 0, 5, 100, 4097, 1, 0, 9000, 33]
+    for d, n in enumerate(sizes):
+        if n == 0:
+            parts.append((np.zeros(0, np.uint64),) * 2 + (np.zeros(0, np.uint8),) * 2)
+            continue
+        spec = gen.MapSpec(nodes_per_coll=n, n_keys=int(rng.integers(1, 300)), seed=100 + d)
+        _, tb = spec.layout()
+        _, i, c, ci, k = gen.generate_maps(spec, d, d + 1, nthreads=1)
+        parts.append((i, c, ci, k))
+    off = np.zeros(len(sizes) + 1, np.uint64)
+    off[1:] = np.cumsum(sizes)
+    idk, ck, ci, kd = (np.concatenate([p[j] for p in parts]) for j in range(4))
+    res = check(weaver, off, idk, ck, ci, kd, 9)
+    assert res.status[0] == 0 and res.status[3] == 0
+
+
+def test_absent_causes_nil_key_and_flags(weaver):
+    spec = gen.MapSpec(nodes_per_coll=50, seed=14)
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 5, nthreads=1)
+    idk, ck, ci = idk.copy(), ck.copy(), ci.copy()
+    # collection 1: id causes that are not in the collection -> the nil key
+    for j in (50 + np.flatnonzero(ci[50:100] == 0)[:3]):
+        ci[j], ck[j] = 1, (1 << 40) | 3
+    # collection 2: a duplicated id
+    idk[101] = idk[100]
+    # collection 3: a node caused by the root id
+    j = 150 + int(np.flatnonzero(ci[150:200] == 0)[0])
+    ci[j], ck[j] = 1, 0
+    res = check(weaver, off, idk, ck, ci, kd, tb)
+    assert res.status[2] & abi.STATUS_DUP and res.status[3] & abi.STATUS_MAP_KEY
+    assert res.status[0] == 0 and res.status[1] == 0 and res.status[4] == 0
+    nil = np.flatnonzero((res.seg_coll == 1) & (res.seg_key == np.uint64(NIL)))
+    assert len(nil) == 1 and len(res.key_weave(int(nil[0]))) == 4
+
+
+def test_assoc_after_dissoc_quirk(weaver):
+    """assoc :a 1, dissoc :a, assoc :a 2 => {} (map.cljc:50-52)."""
+    s = 1  # site bits = 1, one site of rank 1
+    ids = np.array([(1 << s) | 1, (2 << s) | 1, (3 << s) | 1, (4 << s) | 1], np.uint64)
+    cause = np.array([0, 0, 0, 1], np.uint64)        # key tokens :a = 0, :b = 1
+    cis = np.zeros(4, np.uint8)
+    kind = np.array([0, 1, 0, 0], np.uint8)          # 1, hide, 2 on :a; :b -> value
+    res = check(weaver, np.array([0, 4], np.uint64), ids, cause, cis, kind, 1)
+    got = gpu_maps(res, 1)[0]
+    assert got[0][0] == -1          # :a stays hidden
+    assert got[0][1] == [1, 2, 0]   # root, hide, 2 (newest value skips the hide), 1
+    assert got[1] == (3, [3])
+
+
+def test_random_small_maps_match_oracle(weaver):
+    rng = random.Random(21)
+    offs, I, Cs, CI, K = [0], [], [], [], []
+    for d in range(300):
+        n = rng.randint(1, 40)
+        nodes, values = [], []
+        for m in range(n):
+            t = m + 1
+            site = rng.randint(1, 3)
+            idv = (t << 2) | site
+            r = rng.random()
+            if r < 0.55 or not values:
+                nodes.append((idv, rng.randint(0, 5), 0, 0))
+                values.append(idv)
+            elif r < 0.7:
+                nodes.append((idv, rng.randint(0, 5), 0, 1))
+            else:  # mostly undo/redo of a value; sometimes any earlier node (F8c keys)
+                pool = values if rng.random() < 0.8 else [x[0] for x in nodes]
+                nodes.append((idv, rng.choice(pool), 1, rng.choice([1, 2, 3, 0])))
+        rng.shuffle(nodes)
+        for x in nodes:
+            I.append(x[0]); Cs.append(x[1]); CI.append(x[2]); K.append(x[3])
+        offs.append(len(I))
+    check(weaver, np.array(offs, np.uint64), np.array(I, np.uint64), np.array(Cs, np.uint64),
+          np.array(CI, np.uint8), np.array(K, np.uint8), 3)
+
+
+def test_repeat_calls_identical(weaver):
+    spec = gen.CONFIG4
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 10, 510, nthreads=8)
+    a = weaver.weave_maps(off, idk, ck, ci, kd, tb)
+    # a list call in between replaces the cached tables
+    loff, li, lc, lk = gen.generate(gen.GenSpec(nodes_per_doc=300, n_sites=3), 0, 5)
+    weaver.weave_lists(loff, li, lc, lk, gen.GenSpec(nodes_per_doc=300, n_sites=3).layout())
+    b = weaver.weave_maps(off, idk, ck, ci, kd, tb)
+    for f in ("seg_offsets", "seg_coll", "seg_key", "seg_active", "seg_perm", "status"):
+        np.testing.assert_array_equal(getattr(a, f), getattr(b, f))

@@ -114,3 +114,107 @@ def test_insert_errors_mirror_the_reference():
         C.insert(C.list_weave, ct, ((1, "aaaaaaaaaaaaa", 0), C.ROOT_ID, "y"))
     assert e.value.causes == {"append-only", "edits-not-allowed"}
     assert C.insert(C.list_weave, ct, ((1, "aaaaaaaaaaaaa", 0), C.ROOT_ID, "x")) is ct
+
+
+# ------------------------------------------------------------------ map_test.cljc
+MKW = lambda s: C.Keyword(None, s)
+
+
+def _cmap(*kvs):
+    ct = C.new_map_ct(rng=random.Random(5))
+    for k, v in zip(kvs[::2], kvs[1::2]):
+        ct = C.map_assoc(ct, k, v)
+    return ct
+
+
+def test_map_basic():
+    """map_test.cljc:5-15 (a nested list value stays opaque here)."""
+    ct = _cmap(MKW("foo"), "bar")
+    ct = C.map_assoc(ct, MKW("fizz"), "buzz")
+    ct = C.map_assoc(ct, MKW("fizz"), "bang")
+    ct = C.map_dissoc(ct, MKW("foo"))
+    ct = C.map_assoc(ct, MKW("list"), "abc")
+    assert C.causal_map_to_edn(ct) == {MKW("fizz"): "bang", MKW("list"): "abc"}
+
+
+def test_map_hide_and_show():
+    """map_test.cljc:17-31"""
+    foo, fizz = MKW("foo"), MKW("fizz")
+    ct = _cmap(foo, "bar", fizz, "buzz")
+    assert C.causal_map_to_edn(ct) == {foo: "bar", fizz: "buzz"}
+    ct = C.append(C.map_weave, ct, foo, C.HIDE)
+    assert C.causal_map_to_edn(ct) == {fizz: "buzz"}
+    ct = C.append(C.map_weave, ct, foo, C.H_SHOW)
+    assert C.causal_map_to_edn(ct) == {foo: "bar", fizz: "buzz"}
+    ct = C.append(C.map_weave, ct, foo, C.HIDE)
+    assert C.causal_map_to_edn(ct) == {fizz: "buzz"}
+    ct = C.append(C.map_weave, ct, foo, C.H_SHOW)
+    assert C.causal_map_to_edn(ct) == {foo: "bar", fizz: "buzz"}
+    ct = C.append(C.map_weave, ct, foo, "boo")
+    ct = C.append(C.map_weave, ct, foo, C.H_SHOW)
+    ct = C.append(C.map_weave, ct, foo, C.H_SHOW)
+    assert C.causal_map_to_edn(ct) == {foo: "boo", fizz: "buzz"}
+
+
+def test_map_hide_and_show_by_node_id():
+    """map_test.cljc:33-43"""
+    foo = MKW("foo")
+    ct = _cmap(foo, "bar")
+    ct = C.append(C.map_weave, ct, foo, "boo")
+    assert C.causal_map_to_edn(ct) == {foo: "boo"}
+    boo_id = C.causal_map_to_list(ct)[0][0]
+    ct = C.append(C.map_weave, ct, boo_id, C.HIDE)
+    assert C.causal_map_to_edn(ct) == {foo: "bar"}
+    ct = C.append(C.map_weave, ct, boo_id, C.H_SHOW)
+    assert C.causal_map_to_edn(ct) == {foo: "boo"}
+
+
+def test_map_protocol_and_quirk():
+    """map_test.cljc:45-89 and SURVEY F8a."""
+    foo, a = MKW("foo"), MKW("a")
+    assert C.map_count(_cmap()) == 0
+    assert C.map_get(_cmap(foo, "bar"), foo) == "bar"
+    gone = C.map_dissoc(_cmap(foo, "bar"), foo)
+    assert C.map_count(gone) == 0 and C.map_get(gone, foo) is None
+    back = C.append(C.map_weave, gone, foo, C.H_SHOW)
+    assert C.map_count(back) == 1 and C.map_get(back, foo) == "bar"
+    node = ((1, "site-id", 0), MKW("fizz"), "buzz")
+    one = C.insert(C.map_weave, C.new_map_ct(), node)
+    assert C.causal_map_to_list(one) == [node]
+    ct = C.map_assoc(C.map_dissoc(_cmap(a, 1), a), a, 2)
+    assert C.causal_map_to_edn(ct) == {}
+
+
+def test_map_batch_matches_python_restatement():
+    """Many random map histories (incl. F8c id keys) in one GPU call vs causal_ref."""
+    rng = random.Random(99)
+    sites = [C.new_site_id(rng) for _ in range(3)]
+    cts, py = [], []
+    for _ in range(60):
+        nodes, values = [], []
+        for m in range(rng.randint(1, 30)):
+            nid = (m + 1, rng.choice(sites), 0)
+            r = rng.random()
+            if r < 0.55 or not nodes:
+                nd = (nid, f"k{rng.randint(0, 6)}", f"v{m}")
+                values.append(nid)
+            elif r < 0.7:
+                nd = (nid, f"k{rng.randint(0, 6)}", "HIDE")
+            else:
+                pool = values if rng.random() < 0.8 else [x[0] for x in nodes]
+                nd = (nid, rng.choice(pool), rng.choice(["HIDE", "H_HIDE", "H_SHOW", f"w{m}"]))
+            nodes.append(nd)
+        conv = lambda v, M: {"HIDE": M.HIDE, "H_HIDE": M.H_HIDE, "H_SHOW": M.H_SHOW}.get(v, v)
+        ct = C.new_map_ct()
+        ct["nodes"] = {n[0]: (n[1], conv(n[2], C)) for n in nodes}
+        cts.append(ct)
+        p = R.new_map_ct()
+        p["nodes"] = {n[0]: (n[1], conv(n[2], R)) for n in nodes}
+        py.append(R.map_weave(p))
+    got = C.weave_maps(cts)
+    for g, p in zip(got, py):
+        want = {k: [(n[0], n[1], str(n[2])) for n in w] for k, w in p["weave"].items()}
+        have = {k: [(n[0], n[1], str(n[2])) for n in w] for k, w in g["weave"].items()}
+        assert have == want
+        assert {k: str(v) for k, v in C.causal_map_to_edn(g).items()} == \
+            {k: str(v) for k, v in R.causal_map_to_edn(p).items()}
