@@ -398,7 +398,8 @@ __global__ __launch_bounds__(NT) void k_tree(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, uint32_t kbits, uint32_t bm_words,
     uint32_t *__restrict__ epar, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
-    uint32_t *__restrict__ fcN, uint64_t *__restrict__ link, uint32_t *__restrict__ status) {
+    uint32_t *__restrict__ fcN, uint32_t *__restrict__ thr, uint32_t *__restrict__ link,
+    uint32_t *__restrict__ status) {
   constexpr uint32_t IT = TILE_T / NT;
   __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T];
   __shared__ uint32_t wcnt[2][NT / 64][SUB_BINS];
@@ -517,39 +518,80 @@ __global__ __launch_bounds__(NT) void k_tree(
   // the sweep below reads what this workgroup wrote above
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   __syncthreads();
-  for (uint32_t r = tid; r < n; r += NT) {
-    const bool sp = special_at(r);
-    const uint32_t fs = fcS[base + r], fn = fcN[base + r];
-    const uint32_t fc = fs ? fs : fn;
-    uint32_t nx;
-    const uint32_t e = epar[base + r];
-    if (r == 0) {
-      nx = NX_END;
-    } else {
-      uint32_t ns = nsc[base + r];
-      if (!ns && sp) ns = fcN[base + e];  // last special -> newest non-special
-      nx = ns ? ns : (NX_UP | e);
+  // Preorder successor of every node: its first child, else its thread = the
+  // next sibling of the nearest ancestor-or-self that has one (SUCC_END for
+  // the last node).  thr(r) = ns(r) ?: thr(epar(r)), and epar(r) < r, so a
+  // sweep in rank order resolves each tile from earlier tiles' threads (thr,
+  // global) plus pointer jumping over the tile's own parents in LDS.
+  constexpr uint32_t RES = 0x80000000u;
+  uint32_t *T = tkey;
+  for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
+    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+    uint32_t fcr[IT], flg[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid, r = r0 + j;
+      fcr[k] = 0;
+      flg[k] = 0;
+      if (j >= len) continue;
+      const bool sp = special_at(r);
+      const uint32_t fs = fcS[base + r], fn = fcN[base + r];
+      fcr[k] = fs ? fs : fn;
+      uint32_t tv;
+      if (r == 0) {
+        tv = RES | SUCC_END;
+      } else {
+        const uint32_t e = epar[base + r];
+        uint32_t ns = nsc[base + r];
+        if (!ns && sp) ns = fcN[base + e];  // last special -> newest non-special
+        if (ns) tv = RES | ns;
+        else if (e < r0)
+          tv = RES | __hip_atomic_load(&thr[base + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else tv = e - r0;
+      }
+      T[j] = tv;
+      // after a non-special comes its first child, which is its
+      // newest special child when it has one.
+      const bool vis = !sp && r != 0 && !(fs && hide_at(fs));
+      const bool split = r == split_node(d, r >> log2k, log2k, n);
+      flg[k] = (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
     }
-    // after a non-special comes its first child, which is its newest
-    // special child when it has one.
-    const bool vis = !sp && r != 0 && !(fs && hide_at(fs));
-    const bool split = r == split_node(d, r >> log2k, log2k, n);
-    const uint32_t lo = fc | (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
-    link[base + r] = (uint64_t)lo | ((uint64_t)nx << 32);
+    __syncthreads();
+    for (;;) {  // pointer jumping: every value stays an ancestor's thread or pointer
+      bool open = false;
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = k * NT + tid;
+        if (j < len) {
+          const uint32_t t0 = T[j];
+          if (!(t0 & RES)) {
+            const uint32_t t1 = T[t0];
+            T[j] = t1;
+            open |= !(t1 & RES);
+          }
+        }
+      }
+      if (!__syncthreads_or(open)) break;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid, r = r0 + j;
+      if (j >= len) continue;
+      const uint32_t th = T[j] & ~RES;
+      __hip_atomic_store(&thr[base + r], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      link[base + r] = (fcr[k] ? fcr[k] : th) | flg[k];
+    }
+    __syncthreads();
   }
 }
 
-// Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
-// splitter block lw/2's splitter node and follows the tour until the next
-// splitter arc.  Every down arc it crosses gets (walker, local count).
-// Walker lw of document d starts at the down (lw even) or up (lw odd) arc of
-// splitter block lw/2's splitter node and follows the tour to the next splitter
-// arc.  The down arcs it crosses (node rank | renders << 31) are appended to its
-// sublist's slot of `cap` entries; a full slot continues as a new sublist
-// (id >= W, from a per-document counter), so slots are written sequentially
-// by one lane and no per-node scatter is needed.
+// Walker w of document d starts at the splitter node of rank block w and
+// follows preorder successors up to the next splitter (or the end).  The nodes
+// it passes (rank | renders << 31) are appended to its sublist's slot of `cap`
+// entries; a full slot continues as a new sublist (id >= W, from a per-document
+// counter), so slots are written sequentially by one lane, no per-node scatter.
 __global__ __launch_bounds__(1024) void k_walk(
-    const uint64_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
+    const uint32_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
     const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_log2cap,
     const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ doc_Wcap,
@@ -564,54 +606,39 @@ __global__ __launch_bounds__(1024) void k_walk(
   const uint32_t log2cap = doc_log2cap[d], cap = 1u << log2cap;
   const uint32_t f = walk_first[d];
   uint32_t *const sl = slots + slot_first[d];
-  const uint32_t max_steps = 2 * n + 2;
   if (threadIdx.x == 0) next_walker = w0 + blockDim.x;
   __syncthreads();
   for (uint32_t lw = w0 + threadIdx.x; lw < w1; lw = atomicAdd(&next_walker, 1u)) {
-    uint32_t v = split_node(d, lw >> 1, log2k, n);
-    uint32_t dir = lw & 1;  // 0 = down, 1 = up
-    uint32_t x = lw, cnt = 0, nextsub = NX_END;
-    uint64_t L = link[base + v];
-    if (dir == 0) {
-      sl[(size_t)x << log2cap] = v | ((uint32_t)L & LINK_VIS);
-      cnt = 1;
-    }
+    const uint32_t v = split_node(d, lw, log2k, n);
+    uint32_t L = link[base + v];
+    uint32_t x = lw, cnt = 1, nextsub = NX_END;
+    sl[(size_t)x << log2cap] = v | (L & LINK_VIS);
     for (uint32_t steps = 0;; steps++) {
-      uint32_t u, nd;
-      if (dir == 0) {
-        const uint32_t fc = (uint32_t)L & LINK_IDX;
-        if (fc) { u = fc; nd = 0; }
-        else { u = v; nd = 1; }
-      } else {
-        const uint32_t nx = (uint32_t)(L >> 32);
-        if (nx == NX_END) break;
-        if (nx & NX_UP) { u = nx & ~NX_UP; nd = 1; }
-        else { u = nx; nd = 0; }
-      }
-      const uint64_t Lu = (u == v) ? L : link[base + u];
-      if ((uint32_t)Lu & LINK_SPLIT) {
-        nextsub = ((u >> log2k) << 1) | nd;
+      const uint32_t u = L & LINK_IDX;
+      if (u >= n) {  // SUCC_END: the tour is over
+        if (u != SUCC_END) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
       }
-      if (nd == 0) {
-        if (cnt == cap) {  // slot full: continue as a new sublist
-          const uint32_t y = W + atomicAdd(&dyn_ctr[d], 1u);
-          if (y >= Wcap) {
-            atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
-            break;
-          }
-          wcnt[f + x] = cap;
-          wnext[f + x] = y;
-          x = y;
-          cnt = 0;
-        }
-        sl[((size_t)x << log2cap) + cnt] = u | ((uint32_t)Lu & LINK_VIS);
-        cnt++;
+      const uint32_t Lu = link[base + u];
+      if (Lu & LINK_SPLIT) {
+        nextsub = u >> log2k;
+        break;
       }
-      v = u;
-      dir = nd;
+      if (cnt == cap) {  // slot full: continue as a new sublist
+        const uint32_t y = W + atomicAdd(&dyn_ctr[d], 1u);
+        if (y >= Wcap) {
+          atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+          break;
+        }
+        wcnt[f + x] = cap;
+        wnext[f + x] = y;
+        x = y;
+        cnt = 0;
+      }
+      sl[((size_t)x << log2cap) + cnt] = u | (Lu & LINK_VIS);
+      cnt++;
       L = Lu;
-      if (steps > max_steps) {
+      if (steps > n) {
         atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
       }
@@ -1175,15 +1202,14 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
     uint32_t log2k = c->min_log2k, log2cap = c->min_log2cap;
     auto subl = [&]() {
-      return 2 * (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
+      return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
     };
     while (subl() > MAX_SUBLISTS) {
       if (log2k < log2cap) log2k++;
       else log2cap++;
     }
-    const uint32_t S = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;
-    const uint32_t W = 2 * S;
+    const uint32_t W = n ? ((n + (1u << log2k) - 1) >> log2k) : 0;  // one walker per splitter
     const uint32_t Wcap = n ? (uint32_t)subl() : 0;
     t.doc_log2k[d] = log2k;
     t.doc_log2cap[d] = log2cap;
@@ -1375,7 +1401,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint8_t *skind = scratch_t<uint8_t>(c, "skind", N);
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
-  uint64_t *link = scratch_t<uint64_t>(c, "link", N);
+  uint64_t *link = scratch_t<uint64_t>(c, "link", N);  // u32 links; u64 room for the yarn sort
+  uint32_t *thr = scratch_t<uint32_t>(c, "thr", N);
   uint32_t *slots = scratch_t<uint32_t>(c, "slots", t.slots);
   uint32_t *dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
   uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
@@ -1384,7 +1411,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
   uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
   if (!skA || !skB || !svA || !svB || !par || !epar || !skind ||
-      !nsc || !fcS || !fcN || !link || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase || !order)
+      !nsc || !fcS || !fcN || !link || !thr || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase || !order)
     return fail(c, "out of device memory (N=%u)", N);
 
   uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc");
@@ -1429,27 +1456,30 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
       // special/hide bitmaps in LDS for documents up to 2^18 nodes
       const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
-      Launch L(c, "tree", (double)N * (4 + 1 + 8 + 4 + 4 + 8 + 4 + 4 + 4 + 4 + 8));
+      // par, skind, skey in; epar, nsc, last-node tables, thr, link out; sweep 2
+      // reads epar, nsc and the tables back
+      Launch L(c, "tree", (double)N * (4 + 1 + 8 + 4 + 4 + 8 + 4 + 4 + 4 + 8 + 4 + 4));
       if (c->tree_cfg == 2)
         hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
                            (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
+                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
       else if (c->tree_cfg == 1)
         hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
                            (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
+                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
       else
         hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
                            (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, link, out->status);
+                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
     }
     if (check_launch(c, "tree")) return -1;
 
     // 6. Euler walk
     HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
     {
-      Launch L(c, "walk", (double)N * (2 * 8 + 4));
-      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream, link,
+      Launch L(c, "walk", (double)N * (4 + 4));
+      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream,
+                         (const uint32_t *)link,
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
                          dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
                          (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
@@ -1514,7 +1544,7 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
                                         (unsigned long long)N64);
   for (uint64_t d = 0; d < D; d++) {
     if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
-    if (bt->doc_offsets[d + 1] - bt->doc_offsets[d] > LINK_IDX)
+    if (bt->doc_offsets[d + 1] - bt->doc_offsets[d] >= LINK_IDX)
       return fail(c, "document %llu too large (limit 2^30-1 nodes)", (unsigned long long)d);
   }
   if (!res->weave_perm || !res->visible_count || !res->status)
@@ -1600,7 +1630,7 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
                                         (unsigned long long)N64);
   for (uint64_t d = 0; d < D; d++) {
     if (bt->coll_offsets[d + 1] < bt->coll_offsets[d]) return fail(c, "coll_offsets not monotone");
-    if (bt->coll_offsets[d + 1] - bt->coll_offsets[d] >= LINK_IDX)
+    if (bt->coll_offsets[d + 1] - bt->coll_offsets[d] >= LINK_IDX - 1)
       return fail(c, "collection %llu too large", (unsigned long long)d);
   }
   if (!res->seg_offsets || !res->seg_coll || !res->seg_key || !res->seg_active ||

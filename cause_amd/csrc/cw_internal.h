@@ -38,8 +38,8 @@ constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter blo
 constexpr uint32_t LINK_VIS = 0x80000000u;
 constexpr uint32_t LINK_SPLIT = 0x40000000u;
 constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
-constexpr uint32_t NX_UP = 0x80000000u;           // next arc is up(parent)
-constexpr uint32_t NX_END = 0xFFFFFFFFu;          // root's up arc ends the tour
+constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder
+constexpr uint32_t NX_END = 0xFFFFFFFFu;          // last sublist of a document
 
 constexpr uint8_t KIND_CLASS = 3, KIND_ROOT = 4, KIND_HIDE = 1, KIND_HHIDE = 2;
 
