@@ -612,7 +612,9 @@ __global__ __launch_bounds__(1024) void k_walk(
     const uint32_t v = split_node(d, lw, log2k, n);
     uint32_t L = link[base + v];
     uint32_t x = lw, cnt = 1, nextsub = NX_END;
-    sl[(size_t)x << log2cap] = v | (L & LINK_VIS);
+    // entries are buffered four at a time and written as one 16-byte store
+    // (slots are 16-byte aligned: cap >= 4 and every slot start is a multiple)
+    uint4 q = make_uint4(v | (L & LINK_VIS), 0u, 0u, 0u);
     for (uint32_t steps = 0;; steps++) {
       const uint32_t u = L & LINK_IDX;
       if (u >= n) {  // SUCC_END: the tour is over
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(1024) void k_walk(
         nextsub = u >> log2k;
         break;
       }
-      if (cnt == cap) {  // slot full: continue as a new sublist
+      if (cnt == cap) {  // slot full (and flushed): continue as a new sublist
         const uint32_t y = W + atomicAdd(&dyn_ctr[d], 1u);
         if (y >= Wcap) {
           atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
@@ -635,13 +637,27 @@ __global__ __launch_bounds__(1024) void k_walk(
         x = y;
         cnt = 0;
       }
-      sl[((size_t)x << log2cap) + cnt] = u | (Lu & LINK_VIS);
+      const uint32_t e = u | (Lu & LINK_VIS);
+      switch (cnt & 3) {
+        case 0: q.x = e; break;
+        case 1: q.y = e; break;
+        case 2: q.z = e; break;
+        default: q.w = e; break;
+      }
       cnt++;
+      if ((cnt & 3) == 0)
+        *reinterpret_cast<uint4 *>(sl + ((size_t)x << log2cap) + cnt - 4) = q;
       L = Lu;
       if (steps > n) {
         atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
       }
+    }
+    if (cnt & 3) {  // flush the partial group
+      uint32_t *dst = sl + ((size_t)x << log2cap) + (cnt & ~3u);
+      dst[0] = q.x;
+      if ((cnt & 3) > 1) dst[1] = q.y;
+      if ((cnt & 3) > 2) dst[2] = q.z;
     }
     wcnt[f + x] = cnt;
     wnext[f + x] = nextsub;
@@ -735,36 +751,78 @@ __global__ __launch_bounds__(256) void k_emit(
     const uint32_t *__restrict__ doc_log2cap, const uint32_t *__restrict__ doc_off,
     uint32_t *__restrict__ perm, uint8_t *__restrict__ vis8, uint32_t *__restrict__ vcount,
     uint32_t *__restrict__ status) {
+  // The block's sublists are consecutive in tour order, so their entries fill
+  // one contiguous range of weave positions: stage it in LDS, then write it
+  // out coalesced (full lines instead of one 4-byte store per lane and line).
   __shared__ uint32_t wtot[4];
+  __shared__ uint32_t stage_p[EMIT_STAGE];
+  __shared__ uint8_t stage_v[EMIT_STAGE];
+  __shared__ uint32_t P0s;
   const uint32_t b = xcd_tile(blockIdx.x, gridDim.x), d = eblk_doc[b];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, f = walk_first[d];
   const uint32_t Weff = min(doc_W[d] + dyn_ctr[d], walk_first[d + 1] - f);
-  const uint32_t log2cap = doc_log2cap[d];
-  const uint32_t ti = eblk_x0[b] + threadIdx.x;  // tour index: lanes write adjacent ranges
-  uint32_t nvis = 0;
+  const uint32_t log2cap = doc_log2cap[d], cap = 1u << log2cap;
+  const uint32_t ti = eblk_x0[b] + threadIdx.x;  // tour index
+  uint32_t nvis = 0, cnt = 0, p0 = 0;
   bool bad = false;
   const uint32_t x = ti < Weff ? order[f + ti] : 0u;
-  if (ti < Weff && x < Weff) {
-    const uint32_t cnt = wcnt[f + x], p0 = sbase[f + x];
-    const uint32_t *sl = slots + slot_first[d] + ((size_t)x << log2cap);
-    if (p0 + cnt > n || cnt > (1u << log2cap)) {
-      bad = true;
+  const uint4 *sl4 = nullptr;
+  if (ti < Weff) {
+    if (x < Weff) {
+      cnt = wcnt[f + x];
+      p0 = sbase[f + x];
+      sl4 = reinterpret_cast<const uint4 *>(slots + slot_first[d] + ((size_t)x << log2cap));
+      if (p0 + cnt > n || cnt > cap) bad = true;
     } else {
-      for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t e = sl[k];
-        const uint32_t r = e & LINK_IDX;
-        if (r >= n) { bad = true; continue; }
-        const uint32_t v = e >> 31;
-        perm[base + p0 + k] = sval[base + r];
-        vis8[base + p0 + k] = (uint8_t)v;
-        nvis += v;
+      bad = true;
+    }
+  }
+  if (bad) cnt = 0;
+  uint32_t total;
+  const uint32_t off = block_exscan<0>(cnt, wtot, &total);
+  if (threadIdx.x == 0) P0s = p0;  // lane 0 holds the block's first sublist
+  __syncthreads();
+  const uint32_t P0 = P0s;
+  if (cnt && p0 != P0 + off) {  // tour order and sublist bases disagree
+    bad = true;
+    cnt = 0;
+  }
+  const bool staged = total <= EMIT_STAGE && P0 + total <= n;
+  for (uint32_t k0 = 0; k0 < cnt; k0 += 4) {
+    const uint4 q = sl4[k0 >> 2];
+    const uint32_t e4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t k = k0 + u;
+      if (k >= cnt) break;
+      const uint32_t r = e4[u] & LINK_IDX;
+      if (r >= n) {
+        bad = true;
+        continue;
       }
+      const uint32_t v = e4[u] >> 31;
+      const uint32_t pv = sval[base + r];
+      if (staged) {
+        stage_p[off + k] = pv;
+        stage_v[off + k] = (uint8_t)v;
+      } else {
+        perm[base + p0 + k] = pv;
+        vis8[base + p0 + k] = (uint8_t)v;
+      }
+      nvis += v;
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < total; j += 256) {
+      perm[base + P0 + j] = stage_p[j];
+      vis8[base + P0 + j] = stage_v[j];
     }
   }
   if (bad) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
-  uint32_t total;
-  block_exscan<0>(nvis, wtot, &total);
-  if (threadIdx.x == 0 && total) atomicAdd(&vcount[d], total);
+  uint32_t vtotal;
+  block_exscan<0>(nvis, wtot, &vtotal);
+  if (threadIdx.x == 0 && vtotal) atomicAdd(&vcount[d], vtotal);
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
@@ -1840,7 +1898,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 2048));
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
-  c->min_log2cap = knob("CW_LOG2CAP", 4);
+  c->min_log2cap = std::max(2u, knob("CW_LOG2CAP", 4));
   c->tree_cfg = knob("CW_TREE", 1);
   c->join_lds = knob("CW_JOIN_LDS", 0);
 

@@ -38,6 +38,7 @@ constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter blo
 constexpr uint32_t LINK_VIS = 0x80000000u;
 constexpr uint32_t LINK_SPLIT = 0x40000000u;
 constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
+constexpr uint32_t EMIT_STAGE = 4096;          // weave positions staged per emit block
 constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder
 constexpr uint32_t NX_END = 0xFFFFFFFFu;          // last sublist of a document
 
