@@ -245,7 +245,10 @@ def weave_maps(cts):
                 key = _unpack_id(k & ((1 << 63) - 1), pm.layout, pm.ranks[d])
             else:
                 key = pm.keys[k]
-            weave[key] = [ROOT_NODE] + [nodes[p] for p in res.key_weave(s)[1:]]
+            # nodes are woven as [id cause-in-weave v] (map.cljc:35-41)
+            weave[key] = [ROOT_NODE] + [
+                (nodes[p][0], nodes[p][1] if pack.valid_id(nodes[p][1]) else ROOT_ID, nodes[p][2])
+                for p in res.key_weave(s)[1:]]
             a = int(res.seg_active[s])
             active[key] = BLANK if a < 0 else (nodes[a][0], key, nodes[a][2])
         new = dict(ct)

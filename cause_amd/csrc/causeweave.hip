@@ -118,61 +118,67 @@ __global__ __launch_bounds__(1024) void k_radix_scan(uint32_t *__restrict__ hist
       }
 }
 
-// Stable rank of ITEMS striped items per lane (item k of lane t is element
-// k*NT + t) by a sub-digit of sbits (<= 6) bits: returns each item's position
-// inside the tile of `len` elements.
+// Element index of item k of the calling lane when ITEMS items per lane are
+// wave-blocked: wave w owns elements [w*ITEMS*64, (w+1)*ITEMS*64), item k of
+// lane l is element (w*ITEMS + k)*64 + l.
+template <int ITEMS>
+__device__ __forceinline__ uint32_t wb_elem(uint32_t k) {
+  return (((threadIdx.x >> 6) * ITEMS + k) << 6) + (threadIdx.x & 63);
+}
+
+// Stable rank of wave-blocked items (wb_elem) by a sub-digit of sbits (<= 6)
+// bits: returns each item's position inside the tile of `len` elements.  Each
+// wave counts its own items in a private LDS row (LDS ops of one wave execute
+// in order, so no barrier is needed inside the wave); two barriers combine the
+// waves.  wcnt is [NT/64][SUB_BINS], run is [64].
 template <int NT, int ITEMS>
 __device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[ITEMS], uint32_t len,
                                               uint32_t sbits, uint32_t (&pos)[ITEMS],
-                                              uint32_t (*wcnt)[NT / 64][SUB_BINS],
-                                              uint32_t *run) {
+                                              uint32_t (*wcnt)[SUB_BINS], uint32_t *run) {
   constexpr int NW = NT / 64;
-  const uint32_t tid = threadIdx.x, w = tid >> 6, nbin = 1u << sbits;
-  if (tid < SUB_BINS) run[tid] = 0;
-  for (uint32_t i = tid; i < NW * SUB_BINS; i += NT) (&wcnt[0][0][0])[i] = 0;
-  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t *cw = wcnt[w];
+  cw[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
 #pragma unroll
   for (uint32_t k = 0; k < ITEMS; k++) {
-    const bool valid = k * NT + tid < len;
+    const bool valid = wb_elem<ITEMS>(k) < len;
     const uint32_t dd = sd[k];
     uint64_t m = __ballot(valid);
     for (uint32_t bit = 0; bit < sbits; bit++) {
       const bool on = (dd >> bit) & 1u;
-      const uint64_t b = __ballot(on);
-      m &= on ? b : ~b;
+      const uint64_t bb = __ballot(on);
+      m &= on ? bb : ~bb;
     }
     const uint32_t lr = lanes_below(m);
-    const uint32_t buf = k & 1;
-    if (valid && lr == 0) wcnt[buf][w][dd] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (tid < nbin) {
-      uint32_t r = run[tid];
-#pragma unroll
-      for (uint32_t ww = 0; ww < NW; ww++) {
-        const uint32_t c = wcnt[buf][ww][tid];
-        wcnt[buf][ww][tid] = r;
-        r += c;
-        wcnt[buf ^ 1][ww][tid] = 0;
-      }
-      run[tid] = r;
-    }
-    __syncthreads();
-    pos[k] = valid ? wcnt[buf][w][dd] + lr : 0u;
+    const uint32_t before = cw[dd];
+    pos[k] = before + lr;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && lr == 0) cw[dd] = before + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
   }
-  // bin starts (64 bins: one wave)
-  if (tid < 64) {
-    const uint32_t v = tid < nbin ? run[tid] : 0u;
+  __syncthreads();
+  if (threadIdx.x < 64) {  // per bin: wave offsets, then bin starts
+    const uint32_t bn = threadIdx.x;
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ww++) {
+      const uint32_t c = wcnt[ww][bn];
+      wcnt[ww][bn] = tot;
+      tot += c;
+    }
+    const uint32_t v = bn < (1u << sbits) ? tot : 0u;
     uint32_t x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o, 64);
-      if (tid >= (uint32_t)o) x += y;
+      if (bn >= (uint32_t)o) x += y;
     }
-    run[tid] = x - v;
+    run[bn] = x - v;
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < ITEMS; k++) pos[k] += run[sd[k]];
+  for (uint32_t k = 0; k < ITEMS; k++) pos[k] += run[sd[k]] + cw[sd[k]];
   __syncthreads();
 }
 
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   __shared__ K skey[TILE];
   __shared__ uint32_t sval[TILE];
   __shared__ uint32_t soff[MAX_BINS], bstart[MAX_BINS];
-  __shared__ uint32_t wcnt[2][SORT_WAVES][SUB_BINS];
+  __shared__ uint32_t wcnt[SORT_WAVES][SUB_BINS];
   __shared__ uint32_t run[64];
   __shared__ uint32_t wtot[SORT_WAVES];
 
@@ -208,7 +214,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   uint32_t val[SORT_ITEMS], sd[SORT_ITEMS], pos[SORT_ITEMS];
 #pragma unroll
   for (uint32_t k = 0; k < SORT_ITEMS; k++) {
-    const uint32_t j = k * SORT_THREADS + tid;
+    const uint32_t j = wb_elem<SORT_ITEMS>(k);
     const bool valid = j < len;
     key[k] = valid ? keys_in[s + j] : (K)0;
     val[k] = valid ? (vals_in ? vals_in[s + j] : lbase + j) : 0u;
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   if (sub1 > 0) {
 #pragma unroll
     for (uint32_t k = 0; k < SORT_ITEMS; k++)
-      if (k * SORT_THREADS + tid < len) {
+      if (wb_elem<SORT_ITEMS>(k) < len) {
         skey[pos[k]] = key[k];
         sval[pos[k]] = val[k];
       }
@@ -230,7 +236,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     // sub-pass B: high sub-digit, over the tile in sub-pass A order
 #pragma unroll
     for (uint32_t k = 0; k < SORT_ITEMS; k++) {
-      const uint32_t j = k * SORT_THREADS + tid;
+      const uint32_t j = wb_elem<SORT_ITEMS>(k);
       if (j < len) {
         key[k] = skey[j];
         val[k] = sval[j];
@@ -241,7 +247,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 #pragma unroll
   for (uint32_t k = 0; k < SORT_ITEMS; k++)
-    if (k * SORT_THREADS + tid < len) {
+    if (wb_elem<SORT_ITEMS>(k) < len) {
       skey[pos[k]] = key[k];
       sval[pos[k]] = val[k];
     }
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     uint32_t *__restrict__ status) {
   constexpr uint32_t IT = TILE_T / NT;
   __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T];
-  __shared__ uint32_t wcnt[2][NT / 64][SUB_BINS];
+  __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
   __shared__ uint32_t run[64];
   // special / hide bit per rank (LDS when the document fits bm_words words)
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
@@ -440,7 +446,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     uint32_t key[IT], rk[IT], sd[IT], pos[IT];
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
-      const uint32_t j = k * NT + tid, r = r0 + j;
+      const uint32_t j = wb_elem<IT>(k), r = r0 + j;
       key[k] = 0;
       rk[k] = j;
       if (j < len && r > 0) {
@@ -463,14 +469,14 @@ __global__ __launch_bounds__(NT) void k_tree(
       rank_subdigit<NT, IT>(sd, len, min(SUB_BITS, kbits - shift), pos, wcnt, run);
 #pragma unroll
       for (uint32_t k = 0; k < IT; k++)
-        if (k * NT + tid < len) {
+        if (wb_elem<IT>(k) < len) {
           tkey[pos[k]] = key[k];
           trank[pos[k]] = rk[k];
         }
       __syncthreads();
 #pragma unroll
       for (uint32_t k = 0; k < IT; k++) {
-        const uint32_t j = k * NT + tid;
+        const uint32_t j = wb_elem<IT>(k);
         if (j < len) {
           key[k] = tkey[j];
           rk[k] = trank[j];
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     uint32_t prv[IT];
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
-      const uint32_t j = k * NT + tid;
+      const uint32_t j = wb_elem<IT>(k);
       const uint32_t kk = key[k];
       prv[k] = 0;
       if (j < len && kk != 0) {
@@ -498,11 +504,11 @@ __global__ __launch_bounds__(NT) void k_tree(
     }
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++)
-      if (k * NT + tid < len) tns[rk[k]] = prv[k];
+      if (wb_elem<IT>(k) < len) tns[rk[k]] = prv[k];
     __syncthreads();  // every group's old "last" is read before it is replaced
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
-      const uint32_t j = k * NT + tid;
+      const uint32_t j = wb_elem<IT>(k);
       if (j >= len) continue;
       const uint32_t kk = key[k];
       if (kk != 0 && !(j + 1 < len && tkey[j + 1] == kk)) {
@@ -1735,8 +1741,12 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   HIPCHK(c, hipMemsetAsync(status, 0, D * 4, c->stream));
   uint32_t key_bits = bt->key_bits;
   if (key_bits == 0 && find_key_bits(c, id, N, &key_bits)) return -1;
-  if (key_bits > 62) return fail(c, "map ids need %u bits (limit 62)", key_bits);
-  const uint32_t W = std::max(bt->token_bits, key_bits);
+  // id keys are cause ids, which may lie outside the collection
+  uint32_t cause_bits = 0;
+  if (find_key_bits(c, cause, N, &cause_bits)) return -1;
+  if (key_bits > 62 || cause_bits > 62)
+    return fail(c, "map ids need %u bits (limit 62)", std::max(key_bits, cause_bits));
+  const uint32_t W = std::max(std::max(bt->token_bits, key_bits), cause_bits);
 
   // 1. (sort (::s/nodes ct)) per collection -- map.cljc:28
   uint64_t *skey;

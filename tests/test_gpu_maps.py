@@ -32,25 +32,25 @@ def weaver():
 
 def oracle_maps(off, idk, ck, ci, kd):
     """Per collection: {key: (active, [input idx in weave order])}, keys in the
-    ABI's form (token, ID_KEY | id, or NIL)."""
+    ABI's form (token, ID_KEY | id, or NIL).  Tokens go to the oracle with bit
+    63 set so they can never equal a packed id (a keyword is never a vector)."""
     out = []
+    tok = np.uint64(1 << 63)
     for d in range(len(off) - 1):
         a, b = int(off[d]), int(off[d + 1])
-        nk, npos, sk, sa = oracle.map_weave(idk[a:b], ck[a:b], ci[a:b], kd[a:b], 0)
-        ids = {int(x): j for j, x in enumerate(idk[a:b])}
-        api = {}
-        for j in range(b - a):
-            k = int(nk[j])
-            if ci[a + j]:
-                c = ids.get(int(ck[a + j]))
-                if c is not None and ci[a + c]:
-                    api[k] = ID_KEY | k        # key = the cause node's cause id
+        c = np.where(ci[a:b] == 1, ck[a:b], ck[a:b] | tok)
+        nk, npos, sk, sa = oracle.map_weave(idk[a:b], c, ci[a:b], kd[a:b], 0)
+
+        def api(k):
+            if k == NIL:
+                return NIL
+            return k & ~ID_KEY if k & ID_KEY else ID_KEY | k
+
         order = np.lexsort((npos, nk))
         groups = {}
         for j in order:
             groups.setdefault(int(nk[j]), []).append(int(j))
-        out.append({api.get(int(k), int(k)): (int(act), groups.get(int(k), []))
-                    for k, act in zip(sk, sa)})
+        out.append({api(int(k)): (int(act), groups.get(int(k), [])) for k, act in zip(sk, sa)})
     return out
 
 
