@@ -292,17 +292,30 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__
   return lo;
 }
 
-// Every 2^ls-th sorted id of each document, compacted (join's LDS index).
+// Every 2^ls-th sorted id of each document, compacted (join's LDS index),
+// and the duplicate-id check (shared.cljc:166-171): coalesced reads of the
+// sorted ids, neighbours compared across lanes with a shuffle.
 __global__ __launch_bounds__(256) void k_sample(const uint64_t *__restrict__ skey,
                                                 const uint32_t *__restrict__ doc_off,
                                                 const uint32_t *__restrict__ doc_ls,
                                                 const uint32_t *__restrict__ samp_off,
-                                                uint64_t *__restrict__ samples) {
+                                                uint64_t *__restrict__ samples,
+                                                uint32_t *__restrict__ status) {
   const uint32_t d = blockIdx.x, base = doc_off[d], n = doc_off[d + 1] - base;
-  const uint32_t ls = doc_ls[d], ns = samp_off[d + 1] - samp_off[d];
-  for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x)
-    samples[samp_off[d] + j] = skey[base + ((uint64_t)j << ls)];
-  (void)n;
+  const uint32_t ls = doc_ls[d], mask = (1u << ls) - 1, so = samp_off[d];
+  const uint32_t lane = threadIdx.x & 63;
+  bool dup = false;
+  for (uint32_t i0 = threadIdx.x & ~63u; i0 < n; i0 += blockDim.x) {
+    const uint32_t i = i0 + lane;
+    const uint64_t x = i < n ? skey[base + i] : 0ull;
+    uint64_t prev = __shfl_up(x, 1, 64);
+    if (lane == 0 && i > 0) prev = skey[base + i - 1];
+    if (i < n) {
+      if (i > 0) dup |= prev == x;
+      if ((i & mask) == 0) samples[so + (i >> ls)] = x;
+    }
+  }
+  if (__syncthreads_or(dup) && threadIdx.x == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
 }
 
 // Join in sorted order: gather each node's cause id and kind, search the cause
@@ -401,9 +414,9 @@ __global__ __launch_bounds__(1024) void k_join(
 template <int NT, int TILE_T>
 __global__ __launch_bounds__(NT) void k_tree(
     const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
-    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, uint32_t kbits, uint32_t bm_words,
-    uint32_t *__restrict__ epar, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+    uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ fcN, uint32_t *__restrict__ thr, uint32_t *__restrict__ link,
     uint32_t *__restrict__ status) {
   constexpr uint32_t IT = TILE_T / NT;
@@ -440,7 +453,6 @@ __global__ __launch_bounds__(NT) void k_tree(
   auto hide_at = [&](uint32_t r) -> bool {
     return in_lds ? ((hide_bm[r >> 5] >> (r & 31)) & 1u) : is_hide(skind[base + r]);
   };
-  bool dup = false;
   for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
     const uint32_t len = min((uint32_t)TILE_T, n - r0);
     uint32_t key[IT], rk[IT], sd[IT], pos[IT];
@@ -449,17 +461,18 @@ __global__ __launch_bounds__(NT) void k_tree(
       const uint32_t j = wb_elem<IT>(k), r = r0 + j;
       key[k] = 0;
       rk[k] = j;
+      if (j < len) {
+        // this node's own "last child" entries start empty (its children come
+        // later in rank order; the sort's barriers order this before their use)
+        fcS[base + r] = 0;
+        fcN[base + r] = 0;
+      }
       if (j < len && r > 0) {
         const bool sp = special_at(r);
         uint32_t c = par[base + r];
         if (!sp)
           while (c != 0 && special_at(c)) c = par[base + c];
-        epar[base + r] = c;
         key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
-        const uint64_t me = skey[base + r];
-        dup |= me == skey[base + r - 1];
-      } else if (j < len) {
-        epar[base] = 0;
       }
     }
     // stable LDS sort of the tile by group key, 6 bits per sub-pass
@@ -497,14 +510,14 @@ __global__ __launch_bounds__(NT) void k_tree(
           prv[k] = r0 + trank[j - 1];
         } else {
           uint32_t *tab = (kk & 1) ? fcN : fcS;
-          prv[k] = __hip_atomic_load(&tab[base + (kk >> 1) - 1], __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+          prv[k] = tab[base + (kk >> 1) - 1];
         }
       }
     }
+    // nsc = next sibling, or NSC_UP | effective parent for a group's oldest
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++)
-      if (wb_elem<IT>(k) < len) tns[rk[k]] = prv[k];
+      if (wb_elem<IT>(k) < len) tns[rk[k]] = prv[k] ? prv[k] : (NSC_UP | ((key[k] >> 1) - 1));
     __syncthreads();  // every group's old "last" is read before it is replaced
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
@@ -513,20 +526,19 @@ __global__ __launch_bounds__(NT) void k_tree(
       const uint32_t kk = key[k];
       if (kk != 0 && !(j + 1 < len && tkey[j + 1] == kk)) {
         uint32_t *tab = (kk & 1) ? fcN : fcS;
-        __hip_atomic_store(&tab[base + (kk >> 1) - 1], r0 + rk[k], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        tab[base + (kk >> 1) - 1] = r0 + rk[k];
       }
     }
     for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
     __syncthreads();
   }
-  if (dup) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
-  // the sweep below reads what this workgroup wrote above
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // the sweep below reads what this workgroup wrote above: all waves of a
+  // workgroup share one CU and its L1, so the barrier's workgroup-scope
+  // ordering is enough (agent-scope accesses would push every line to L2)
   __syncthreads();
   // Preorder successor of every node: its first child, else its thread = the
   // next sibling of the nearest ancestor-or-self that has one (SUCC_END for
-  // the last node).  thr(r) = ns(r) ?: thr(epar(r)), and epar(r) < r, so a
+  // the last node).  thr(r) = ns(r) ?: thr(e(r)), and e(r) < r, so a
   // sweep in rank order resolves each tile from earlier tiles' threads (thr,
   // global) plus pointer jumping over the tile's own parents in LDS.
   constexpr uint32_t RES = 0x80000000u;
@@ -547,12 +559,14 @@ __global__ __launch_bounds__(NT) void k_tree(
       if (r == 0) {
         tv = RES | SUCC_END;
       } else {
-        const uint32_t e = epar[base + r];
-        uint32_t ns = nsc[base + r];
-        if (!ns && sp) ns = fcN[base + e];  // last special -> newest non-special
+        uint32_t ns = nsc[base + r], e = 0;
+        if (ns & NSC_UP) {
+          e = ns & ~NSC_UP;
+          ns = sp ? fcN[base + e] : 0u;  // last special -> newest non-special
+        }
         if (ns) tv = RES | ns;
         else if (e < r0)
-          tv = RES | __hip_atomic_load(&thr[base + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          tv = RES | thr[base + e];
         else tv = e - r0;
       }
       T[j] = tv;
@@ -584,7 +598,7 @@ __global__ __launch_bounds__(NT) void k_tree(
       const uint32_t j = k * NT + tid, r = r0 + j;
       if (j >= len) continue;
       const uint32_t th = T[j] & ~RES;
-      __hip_atomic_store(&thr[base + r], th, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      thr[base + r] = th;
       link[base + r] = (fcr[k] ? fcr[k] : th) | flg[k];
     }
     __syncthreads();
@@ -1461,7 +1475,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
 
   uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
   uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
-  uint32_t *par = scratch_t<uint32_t>(c, "par", N), *epar = scratch_t<uint32_t>(c, "epar", N);
+  uint32_t *par = scratch_t<uint32_t>(c, "par", N);
   uint8_t *skind = scratch_t<uint8_t>(c, "skind", N);
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
@@ -1474,7 +1488,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
   uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
   uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
-  if (!skA || !skB || !svA || !svB || !par || !epar || !skind ||
+  if (!skA || !skB || !svA || !svB || !par || !skind ||
       !nsc || !fcS || !fcN || !link || !thr || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase || !order)
     return fail(c, "out of device memory (N=%u)", N);
 
@@ -1499,9 +1513,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     uint64_t *samples = scratch_t<uint64_t>(c, "samples", t.Stot);
     if (!samples) return fail(c, "out of device memory (samples)");
     {
-      Launch L(c, "sample", (double)t.Stot * (64 + 8));
+      Launch L(c, "sample", (double)N * 8 + (double)t.Stot * 8);
       hipLaunchKernelGGL(k_sample, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
-                         dev_tab(c, "t_doc_ls"), dev_tab(c, "t_samp_off"), samples);
+                         dev_tab(c, "t_doc_ls"), dev_tab(c, "t_samp_off"), samples, out->status);
     }
     if (check_launch(c, "sample")) return -1;
     {
@@ -1514,27 +1528,25 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (check_launch(c, "join")) return -1;
 
     // 3-5. effective parents, sibling order, links
-    HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
     {
       const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
       // special/hide bitmaps in LDS for documents up to 2^18 nodes
       const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
-      // par, skind, skey in; epar, nsc, last-node tables, thr, link out; sweep 2
-      // reads epar, nsc and the tables back
-      Launch L(c, "tree", (double)N * (4 + 1 + 8 + 4 + 4 + 8 + 4 + 4 + 4 + 8 + 4 + 4));
+      // par, skind in; nsc, last-node tables, thr, link out; sweep 2 reads nsc
+      // and the tables back
+      Launch L(c, "tree", (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
       if (c->tree_cfg == 2)
         hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
-                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
       else if (c->tree_cfg == 1)
         hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
-                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
       else
         hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
-                           (size_t)bm_words * 8, c->stream, par, skind, skey, doc_off, doc_log2k,
-                           kbits, bm_words, epar, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
     }
     if (check_launch(c, "tree")) return -1;
 

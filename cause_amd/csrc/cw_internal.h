@@ -39,6 +39,7 @@ constexpr uint32_t LINK_VIS = 0x80000000u;
 constexpr uint32_t LINK_SPLIT = 0x40000000u;
 constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
 constexpr uint32_t EMIT_STAGE = 4096;          // weave positions staged per emit block
+constexpr uint32_t NSC_UP = 0x80000000u;         // nsc: no next sibling, low bits = eff parent
 constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder
 constexpr uint32_t NX_END = 0xFFFFFFFFu;          // last sublist of a document
 
