@@ -292,61 +292,78 @@ __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__
   return lo;
 }
 
-// Every 2^ls-th sorted id of each document, compacted (join's LDS index),
-// and the duplicate-id check (shared.cljc:166-171): coalesced reads of the
-// sorted ids, neighbours compared across lanes with a shuffle.
-__global__ __launch_bounds__(256) void k_sample(const uint64_t *__restrict__ skey,
-                                                const uint32_t *__restrict__ doc_off,
-                                                const uint32_t *__restrict__ doc_ls,
-                                                const uint32_t *__restrict__ samp_off,
-                                                uint64_t *__restrict__ samples,
-                                                uint32_t *__restrict__ status) {
+// Per document: a bucket index over the sorted ids and the duplicate-id check
+// (shared.cljc:166-171).  With kmin/kmax the smallest/largest id and a shift
+// s chosen so that at most max(n/4, 1) buckets cover [kmin, kmax], entry h of
+// the index is the first rank whose id has (id - kmin) >> s >= h (entry NB =
+// n).  Lamport ids are close to uniform over their range, so a bucket holds a
+// handful of ids: the join finds a cause with two index reads and one short
+// search inside a line of sorted ids.  Coalesced reads; neighbours compared
+// across lanes with a shuffle.
+__device__ __forceinline__ uint32_t bucket_shift(uint64_t range, uint32_t n) {
+  const uint64_t nbmax = max(n >> 2, 1u);
+  uint32_t s = 0;
+  while ((range >> s) > nbmax) s++;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_index(const uint64_t *__restrict__ skey,
+                                               const uint32_t *__restrict__ doc_off,
+                                               const uint32_t *__restrict__ bkt_off,
+                                               uint32_t *__restrict__ bkt,
+                                               uint32_t *__restrict__ status) {
   const uint32_t d = blockIdx.x, base = doc_off[d], n = doc_off[d + 1] - base;
-  const uint32_t ls = doc_ls[d], mask = (1u << ls) - 1, so = samp_off[d];
+  if (n == 0) return;
+  const uint64_t kmin = skey[base], kmax = skey[base + n - 1];
+  const uint32_t sh = bucket_shift(kmax - kmin, n);
+  const uint32_t nb = (uint32_t)((kmax - kmin) >> sh) + 1;
+  uint32_t *B = bkt + bkt_off[d];
   const uint32_t lane = threadIdx.x & 63;
   bool dup = false;
   for (uint32_t i0 = threadIdx.x & ~63u; i0 < n; i0 += blockDim.x) {
     const uint32_t i = i0 + lane;
-    const uint64_t x = i < n ? skey[base + i] : 0ull;
+    const uint64_t x = i < n ? skey[base + i] : kmax;
     uint64_t prev = __shfl_up(x, 1, 64);
-    if (lane == 0 && i > 0) prev = skey[base + i - 1];
+    if (lane == 0 && i > 0 && i < n) prev = skey[base + i - 1];
     if (i < n) {
-      if (i > 0) dup |= prev == x;
-      if ((i & mask) == 0) samples[so + (i >> ls)] = x;
+      const uint32_t h = (uint32_t)((x - kmin) >> sh);
+      uint32_t h0 = 0;
+      if (i > 0) {
+        dup |= prev == x;
+        h0 = (uint32_t)((prev - kmin) >> sh) + 1;
+      }
+      for (uint32_t hh = h0; hh <= h; hh++) B[hh] = i;
     }
   }
+  if (threadIdx.x == 0) B[nb] = n;
   if (__syncthreads_or(dup) && threadIdx.x == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
 }
 
-// Join in sorted order: gather each node's cause id and kind, search the cause
-// among the document's sorted ids: a branchless search of the LDS sample
-// (every 2^ls-th id), then one 2^ls-key span of global memory.  Each lane
-// handles JOIN_ITEMS nodes with their loads and searches interleaved.
+// Join in sorted order: gather each node's cause id and kind, find the cause
+// among the document's sorted ids through the bucket index (k_index).  Each
+// lane handles JOIN_ITEMS nodes with their loads and searches interleaved.
 __global__ __launch_bounds__(1024) void k_join(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
-    const uint64_t *__restrict__ samples, const uint32_t *__restrict__ samp_off,
-    const uint32_t *__restrict__ doc_ls, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ bkt, const uint32_t *__restrict__ bkt_off,
+    const uint32_t *__restrict__ tile_start,
     const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ doc_off,
     uint32_t *__restrict__ par, uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
   constexpr int IT = JOIN_ITEMS;
-  extern __shared__ __attribute__((aligned(16))) uint64_t S[];  // <= MAX_SAMPLES
   __shared__ uint32_t bst;
   const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t];
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
-  const uint32_t ls = doc_ls[d], s0 = samp_off[d], ns = samp_off[d + 1] - s0;
-  for (uint32_t j = threadIdx.x; j < ns; j += blockDim.x) S[j] = samples[s0 + j];
+  const uint64_t kmin = skey[base], kmax = skey[base + n - 1];
+  const uint32_t sh = bucket_shift(kmax - kmin, n);
+  const uint32_t *B = bkt + bkt_off[d];
   if (threadIdx.x == 0) bst = 0;
   __syncthreads();
-  uint32_t top = 1;
-  while (top <= ns) top <<= 1;
   const uint32_t ts = tile_start[t], te = tile_start[t + 1];
   uint32_t st = 0;
   for (uint32_t i0 = ts + threadIdx.x; i0 < te; i0 += IT * blockDim.x) {
-    uint32_t gi[IT];
+    uint32_t gi[IT], lo[IT], hi[IT];
     uint8_t kd[IT];
     uint64_t ck[IT];
-    uint32_t lo[IT];
     bool v[IT];
 #pragma unroll
     for (int k = 0; k < IT; k++) {
@@ -358,14 +375,26 @@ __global__ __launch_bounds__(1024) void k_join(
     for (int k = 0; k < IT; k++) {
       kd[k] = v[k] ? kind[gi[k]] : 0;
       ck[k] = v[k] ? cause_key[gi[k]] : 0;
-      lo[k] = 0;
     }
-    // lo = number of samples <= ck (branchless, interleaved)
-    for (uint32_t bstep = top >> 1; bstep; bstep >>= 1) {
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      lo[k] = hi[k] = 0;
+      if (v[k] && ck[k] >= kmin && ck[k] <= kmax) {
+        const uint32_t h = (uint32_t)((ck[k] - kmin) >> sh);
+        lo[k] = B[h];
+        hi[k] = B[h + 1];
+      }
+    }
+    // search inside the bucket (a few ids, usually one line)
+    for (bool more = true; more;) {
+      more = false;
 #pragma unroll
       for (int k = 0; k < IT; k++) {
-        const uint32_t q = lo[k] + bstep;
-        if (q <= ns && S[q - 1] <= ck[k]) lo[k] = q;
+        if (lo[k] < hi[k]) {
+          const uint32_t m = (lo[k] + hi[k]) >> 1;
+          if (skey[base + m] < ck[k]) lo[k] = m + 1; else hi[k] = m;
+          more |= lo[k] < hi[k];
+        }
       }
     }
 #pragma unroll
@@ -378,17 +407,9 @@ __global__ __launch_bounds__(1024) void k_join(
         if (!(kd[k] & KIND_ROOT)) st |= CW_STATUS_ROOT;
       } else {
         if (kd[k] & KIND_ROOT) st |= CW_STATUS_ROOT;
-        uint32_t c = n;
-        if (lo[k] > 0) {
-          uint32_t a0 = (lo[k] - 1) << ls;
-          uint32_t b0 = min(a0 + (1u << ls), n);
-          while (a0 < b0) {
-            const uint32_t m = (a0 + b0) >> 1;
-            if (skey[base + m] < ck[k]) a0 = m + 1; else b0 = m;
-          }
-          c = a0;
-        }
-        if (c >= n || skey[base + c] != ck[k]) st |= CW_STATUS_ORPHAN;
+        const uint32_t c = lo[k];
+        if (ck[k] < kmin || ck[k] > kmax || c >= n || skey[base + c] != ck[k])
+          st |= CW_STATUS_ORPHAN;
         else if (c >= r) st |= CW_STATUS_NON_LAMPORT;
         else p = c;
       }
@@ -1127,15 +1148,15 @@ struct cw_ctx {
   std::vector<uint64_t> last_off;
   struct Tables {
     std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
-        wblk_doc, wblk_w0, doc_ls, samp_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0;
+        wblk_doc, wblk_w0, bkt_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0;
     std::vector<uint64_t> slot_first;
-    uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Stot = 0, Wmax = 0, Smax = 0;
+    uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Btot = 0, Wmax = 0;
     uint64_t slots = 0;
   } tab;
   bool tab_on_device = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
   uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
-           join_lds = 0, max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
+           max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
 };
 
 namespace {
@@ -1261,12 +1282,10 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.doc_Wcap.resize(D);
   t.slot_first.resize(D + 1);
   uint64_t slots = 0;
-  t.doc_ls.resize(D);
-  t.samp_off.resize(D + 1);
+  t.bkt_off.resize(D + 1);
   uint32_t wtot = 0, stot = 0;
   t.nmax = 0;
   t.Wmax = 0;
-  t.Smax = 0;
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
     t.doc_off[d] = b;
@@ -1306,14 +1325,9 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
       t.eblk_x0.push_back(x0);
     }
     wtot += Wcap;
-    // join samples: every 2^ls-th sorted id, at most MAX_SAMPLES per document
-    const uint32_t ls =
-        std::max(MIN_LOG2_STRIDE, ceil_log2((n + MAX_SAMPLES - 1) / MAX_SAMPLES));
-    t.doc_ls[d] = ls;
-    t.samp_off[d] = stot;
-    const uint32_t ns = n ? ((n - 1) >> ls) + 1 : 0;
-    t.Smax = std::max(t.Smax, ns);
-    stot += ns;
+    // join bucket index: <= max(n/4, 1) buckets + 1 end entry (k_index)
+    t.bkt_off[d] = stot;
+    stot += n ? std::max(n >> 2, 1u) + 2 : 0;
   }
   t.doc_off[D] = (uint32_t)off[D];
   t.tile_first[D] = (uint32_t)t.tile_start.size();
@@ -1321,8 +1335,8 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.slot_first[D] = slots;
   t.slots = slots;
   t.Be = (uint32_t)t.eblk_doc.size();
-  t.samp_off[D] = stot;
-  t.Stot = stot;
+  t.bkt_off[D] = stot;
+  t.Btot = stot;
   t.T = (uint32_t)t.tile_doc.size();
   t.tile_start.push_back((uint32_t)off[D]);
   t.Wtot = wtot;
@@ -1335,7 +1349,7 @@ int upload_tables(cw_ctx *c) {
       {"t_doc_off", &t.doc_off},   {"t_tile_start", &t.tile_start}, {"t_tile_doc", &t.tile_doc},
       {"t_tile_first", &t.tile_first}, {"t_doc_log2k", &t.doc_log2k}, {"t_doc_W", &t.doc_W},
       {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0},
-      {"t_doc_ls", &t.doc_ls},     {"t_samp_off", &t.samp_off}, {"t_doc_log2cap", &t.doc_log2cap},
+      {"t_bkt_off", &t.bkt_off}, {"t_doc_log2cap", &t.doc_log2cap},
       {"t_doc_Wcap", &t.doc_Wcap}, {"t_eblk_doc", &t.eblk_doc}, {"t_eblk_x0", &t.eblk_x0}};
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still be read
   size_t total = (t.slot_first.size() + 64) * 8;
@@ -1510,20 +1524,19 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       return -1;
 
     // 2. join
-    uint64_t *samples = scratch_t<uint64_t>(c, "samples", t.Stot);
-    if (!samples) return fail(c, "out of device memory (samples)");
+    uint32_t *bkt = scratch_t<uint32_t>(c, "bkt", t.Btot);
+    if (!bkt) return fail(c, "out of device memory (bucket index)");
     {
-      Launch L(c, "sample", (double)N * 8 + (double)t.Stot * 8);
-      hipLaunchKernelGGL(k_sample, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
-                         dev_tab(c, "t_doc_ls"), dev_tab(c, "t_samp_off"), samples, out->status);
+      Launch L(c, "index", (double)N * 8 + (double)t.Btot * 4);
+      hipLaunchKernelGGL(k_index, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
+                         dev_tab(c, "t_bkt_off"), bkt, out->status);
     }
-    if (check_launch(c, "sample")) return -1;
+    if (check_launch(c, "index")) return -1;
     {
       Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1));
-      hipLaunchKernelGGL(k_join, GT, TB, (size_t)t.Smax * 8 + c->join_lds, c->stream, skey, sval,
-                         cause_key, kind, samples,
-                         dev_tab(c, "t_samp_off"), dev_tab(c, "t_doc_ls"), tile_start, tile_doc,
-                         doc_off, par, skind, out->status);
+      hipLaunchKernelGGL(k_join, GT, TB, 0, c->stream, skey, sval, cause_key, kind, bkt,
+                         dev_tab(c, "t_bkt_off"), tile_start, tile_doc, doc_off, par, skind,
+                         out->status);
     }
     if (check_launch(c, "join")) return -1;
 
@@ -1922,7 +1935,6 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
   c->min_log2cap = std::max(2u, knob("CW_LOG2CAP", 4));
   c->tree_cfg = knob("CW_TREE", 1);
-  c->join_lds = knob("CW_JOIN_LDS", 0);
 
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
   *out = c;

@@ -21,8 +21,6 @@ constexpr uint32_t TREE_TILE = 4096;
 
 // Join: per-document sample of the sorted ids (every 2^ls-th key, <= MAX_SAMPLES)
 // staged in LDS so the cause search touches global memory only at the end.
-constexpr uint32_t MAX_SAMPLES = 8192;             // 64 KiB of LDS
-constexpr uint32_t MIN_LOG2_STRIDE = 3;
 constexpr int JOIN_ITEMS = 4;
 
 // Euler walk: one walker per splitter arc; <= MAX_SUBLISTS sublists per document
