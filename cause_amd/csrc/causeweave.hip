@@ -422,6 +422,280 @@ __global__ __launch_bounds__(1024) void k_join(
   if (threadIdx.x == 0 && bst) atomicOr(&status[d], bst);
 }
 
+// --- front end by rank directory: id order and cause join without a sort ---------
+// Lamport ids are dense: a document of n nodes from s sites has ids inside a
+// range of about (max ts) * 2^site_bits keys.  A bitmap over [kmin, kmax]
+// with a running popcount gives each id its rank in (sort ::nodes) directly
+// (list.cljc:28) and each cause its parent rank (the join), so the two radix
+// passes, the bucket index and the search disappear.  Directory layout, per
+// group of 96 key values: uint4 {ones before the group, bits 0-31, 32-63,
+// 64-95}; one 16-byte LDS read answers "present?" and "rank".
+constexpr uint32_t FR_GROUP_BITS = 96;
+constexpr uint32_t FR_BIG = 0xFFFFFFFFu;  // dgroups[d]: range too wide for a slot
+
+__device__ __forceinline__ uint32_t fr_word(const uint4 &q, uint32_t w) {
+  return w == 0 ? q.y : (w == 1 ? q.z : q.w);
+}
+
+// x = key - kmin < groups * 96.  present: bit x is set; returns the rank.
+__device__ __forceinline__ uint32_t fr_rank(const uint4 *__restrict__ dir, uint32_t x,
+                                            bool *present) {
+  const uint32_t g = x / FR_GROUP_BITS, b = x - g * FR_GROUP_BITS, w = b >> 5, m = 1u << (b & 31);
+  const uint4 q = dir[g];
+  const uint32_t wv = fr_word(q, w);
+  *present = (wv & m) != 0;
+  return q.x + (w > 0 ? __popc(q.y) : 0u) + (w > 1 ? __popc(q.z) : 0u) + __popc(wv & (m - 1));
+}
+
+// One workgroup per document: key range (min/max), bitmap in LDS (a bit set
+// twice is a duplicate id, shared.cljc:166-171), group prefix counts, copy to
+// the document's directory slot.  Also ::lamport-ts = max ts (refresh-ts,
+// shared.cljc:243-249).  A range wider than a slot marks the document FR_BIG
+// and counts it in big[0]; big[1] = the largest group count.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key,
+                                             const uint32_t *__restrict__ doc_off,
+                                             uint32_t slot_groups, uint4 *__restrict__ dir,
+                                             uint64_t *__restrict__ dkmin,
+                                             uint32_t *__restrict__ dgroups,
+                                             uint64_t *__restrict__ max_ts, uint32_t ts_shift,
+                                             uint32_t *__restrict__ status,
+                                             uint32_t *__restrict__ big) {
+  extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
+  __shared__ uint64_t rmin[NT / 64], rmax[NT / 64];
+  __shared__ uint32_t wtot[NT / 64];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x, base = doc_off[d];
+  const uint32_t n = doc_off[d + 1] - base;
+  if (n == 0) {
+    if (tid == 0) dgroups[d] = 0;
+    return;
+  }
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint32_t i = tid; i < n; i += NT) {
+    const uint64_t k = id_key[base + i];
+    mn = min(mn, k);
+    mx = max(mx, k);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mn = min(mn, (uint64_t)__shfl_xor(mn, o, 64));
+    mx = max(mx, (uint64_t)__shfl_xor(mx, o, 64));
+  }
+  if ((tid & 63) == 0) {
+    rmin[tid >> 6] = mn;
+    rmax[tid >> 6] = mx;
+  }
+  __syncthreads();
+  mn = rmin[0];
+  mx = rmax[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; w++) {
+    mn = min(mn, rmin[w]);
+    mx = max(mx, rmax[w]);
+  }
+  if (tid == 0 && max_ts) max_ts[d] = mx >> ts_shift;
+  const uint64_t span = mx - mn;  // R - 1
+  if (span >= (uint64_t)slot_groups * FR_GROUP_BITS) {
+    if (tid == 0) {
+      dgroups[d] = FR_BIG;
+      atomicAdd(&big[0], 1u);
+    }
+    return;
+  }
+  const uint32_t G = (uint32_t)(span / FR_GROUP_BITS) + 1;
+  if (tid == 0) {
+    dkmin[d] = mn;
+    dgroups[d] = G;
+    atomicMax(&big[1], G);
+  }
+  for (uint32_t g = tid; g < G; g += NT) sdir[g] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
+  bool dup = false;
+  for (uint32_t i = tid; i < n; i += NT) {
+    const uint32_t x = (uint32_t)(id_key[base + i] - mn);
+    const uint32_t g = x / FR_GROUP_BITS, b = x - g * FR_GROUP_BITS, m = 1u << (b & 31);
+    const uint32_t old = atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
+    dup |= (old & m) != 0;
+  }
+  __syncthreads();
+  // group prefix counts: each thread owns a contiguous run of groups
+  const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
+  uint32_t cnt = 0;
+  for (uint32_t g = g0; g < g1; g++) {
+    const uint4 q = sdir[g];
+    cnt += __popc(q.y) + __popc(q.z) + __popc(q.w);
+  }
+  uint32_t run = block_exscan<NT>(cnt, wtot, nullptr);
+  for (uint32_t g = g0; g < g1; g++) {
+    const uint4 q = sdir[g];
+    sw[g * 4] = run;
+    run += __popc(q.y) + __popc(q.z) + __popc(q.w);
+  }
+  __syncthreads();
+  uint4 *out = dir + (size_t)d * slot_groups;
+  for (uint32_t g = tid; g < G; g += NT) out[g] = sdir[g];
+  if (__syncthreads_or(dup) && tid == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
+}
+
+// Pass 1, per tile (XCD-contiguous like the sort tiles): stage the document's
+// directory in LDS, rank every node and its cause, and do the domain checks
+// of s/insert (shared.cljc:163-178): root at rank 0 only, cause present
+// (orphan), cause older than the node (lamport).  A random 4-byte store per
+// node into the rank-ordered arrays would cost a partial line each, so the
+// tile is sorted in LDS by rank window (rank >> 12, a window = the ranks of
+// one tile) and written out coalesced as records: meta = rank & 4095 |
+// (tile-local index) << 12 | class << 24, and the cause rank.  woff[t][w] =
+// start of window w's records inside tile t.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_frank(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ tile_start,
+    const uint32_t *__restrict__ tile_doc, const uint32_t *__restrict__ tile_first,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ woff_base,
+    const uint4 *__restrict__ dir, uint32_t slot_groups, const uint64_t *__restrict__ dkmin,
+    const uint32_t *__restrict__ dgroups, uint32_t *__restrict__ rec_meta,
+    uint32_t *__restrict__ rec_par, uint32_t *__restrict__ woff, uint32_t *__restrict__ status) {
+  constexpr uint32_t IT = TILE / NT;
+  extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
+  __shared__ uint32_t st_meta[TILE], st_par[TILE];
+  __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
+  __shared__ uint32_t run[64];
+  __shared__ uint32_t bst;
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t], tid = threadIdx.x;
+  const uint32_t nwin = tile_first[d + 1] - tile_first[d];
+  const uint32_t wbits = nwin <= 1 ? 0u : 32u - __clz(nwin - 1);  // <= 6
+  const uint32_t G = dgroups[d];
+  const uint64_t kmin = dkmin[d], xend = (uint64_t)G * FR_GROUP_BITS;
+  const uint4 *src = dir + (size_t)d * slot_groups;
+  for (uint32_t g = tid; g < G; g += NT) sdir[g] = src[g];
+  if (tid == 0) bst = 0;
+  __syncthreads();
+  const uint32_t s = tile_start[t], len = tile_start[t + 1] - s;
+  uint64_t k[IT], c[IT];
+  uint8_t kd[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t j = wb_elem<IT>(u);
+    k[u] = j < len ? id_key[s + j] : kmin;
+    c[u] = j < len ? cause_key[s + j] : 0;
+    kd[u] = j < len ? kind[s + j] : 0;
+  }
+  uint32_t st = 0, meta[IT], pr[IT], sd[IT], pos[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t j = wb_elem<IT>(u);
+    bool pres;
+    const uint32_t r = fr_rank(sdir, (uint32_t)(k[u] - kmin), &pres);
+    uint32_t p = 0;
+    if (j < len) {
+      if (r == 0) {
+        if (!(kd[u] & KIND_ROOT)) st |= CW_STATUS_ROOT;
+      } else {
+        if (kd[u] & KIND_ROOT) st |= CW_STATUS_ROOT;
+        const uint64_t cx = c[u] - kmin;
+        bool cp = false;
+        uint32_t cr = 0;
+        if (c[u] >= kmin && cx < xend) cr = fr_rank(sdir, (uint32_t)cx, &cp);
+        if (!cp) st |= CW_STATUS_ORPHAN;
+        else if (c[u] >= k[u]) st |= CW_STATUS_NON_LAMPORT;
+        else p = cr;
+      }
+    }
+    meta[u] = (r & (TILE - 1)) | (j << 12) | ((uint32_t)(kd[u] & KIND_CLASS) << 24);
+    pr[u] = p;
+    sd[u] = min(r >> 12, nwin - 1);  // duplicates can push ranks past the end
+  }
+  if (wbits) {
+    rank_subdigit<NT, IT>(sd, len, wbits, pos, wcnt, run);
+  } else {
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) pos[u] = wb_elem<IT>(u);
+    if (tid == 0) run[0] = 0;
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++)
+    if (wb_elem<IT>(u) < len) {
+      st_meta[pos[u]] = meta[u];
+      st_par[pos[u]] = pr[u];
+    }
+  if (st) atomicOr(&bst, st);
+  __syncthreads();
+  uint32_t *wo = woff + woff_base[t];
+  for (uint32_t w = tid; w <= nwin; w += NT) wo[w] = w < nwin ? (wbits ? run[w] : 0u) : len;
+  for (uint32_t j = tid; j < len; j += NT) {
+    rec_meta[s + j] = st_meta[j];
+    rec_par[s + j] = st_par[j];
+  }
+  if (tid == 0 && bst) atomicOr(&status[d], bst);
+}
+
+// Pass 2, one block per window (window w of document d covers ranks
+// [4096 w, 4096 (w+1)), the ranks of tile w): gather the window's records from
+// every tile of the document (one contiguous run each), place them by rank in
+// LDS and write sval (input index), par (cause rank), skind and, for the yarn
+// sort, skey in rank order, coalesced.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fplace(
+    const uint32_t *__restrict__ rec_meta, const uint32_t *__restrict__ rec_par,
+    const uint32_t *__restrict__ woff, const uint32_t *__restrict__ woff_base,
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ tile_first, const uint32_t *__restrict__ doc_off,
+    const uint64_t *__restrict__ id_key, uint32_t *__restrict__ sval, uint32_t *__restrict__ par,
+    uint8_t *__restrict__ skind, uint64_t *__restrict__ skey) {
+  __shared__ uint32_t s_val[TILE], s_par[TILE];
+  __shared__ uint8_t s_kind[TILE];
+  __shared__ uint32_t s_run[65], s_src[64];
+  const uint32_t t = xcd_tile(blockIdx.x, gridDim.x), d = tile_doc[t], tid = threadIdx.x;
+  const uint32_t t0 = tile_first[d], ntile = tile_first[d + 1] - t0, w = t - t0;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  const uint32_t r0 = w << 12, wlen = min(TILE, n - r0);
+  if (tid < 64) {  // run lengths of this window in every tile, prefix in LDS
+    uint32_t a = 0, l = 0;
+    if (tid < ntile) {
+      const uint32_t *wo = woff + woff_base[t0 + tid];
+      a = wo[w];
+      l = wo[w + 1] - a;
+      s_src[tid] = tile_start[t0 + tid] + a;
+    }
+    uint32_t x = l;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (tid >= (uint32_t)o) x += y;
+    }
+    s_run[tid + 1] = x;
+    if (tid == 0) s_run[0] = 0;
+  }
+  for (uint32_t j = tid; j < wlen; j += NT) {
+    s_val[j] = 0;
+    s_par[j] = 0;
+    s_kind[j] = 0;
+  }
+  __syncthreads();
+  const uint32_t total = min(s_run[ntile], wlen);
+  for (uint32_t j = tid; j < total; j += NT) {
+    uint32_t lo = 0, hi = ntile;  // last tile whose run starts at or before j
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (s_run[m] <= j) lo = m; else hi = m;
+    }
+    const uint32_t g = s_src[lo] + (j - s_run[lo]);
+    const uint32_t meta = rec_meta[g], rr = meta & (TILE - 1);
+    s_val[rr] = (lo << 12) | ((meta >> 12) & (TILE - 1));
+    s_par[rr] = rec_par[g];
+    s_kind[rr] = (uint8_t)(meta >> 24);
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < wlen; j += NT) {
+    const uint32_t v = s_val[j];
+    sval[base + r0 + j] = v;
+    par[base + r0 + j] = s_par[j];
+    skind[base + r0 + j] = s_kind[j];
+    if (skey) skey[base + r0 + j] = id_key[base + (v < n ? v : 0u)];
+  }
+}
+
 // --- tree: effective parents, sibling order, links (one workgroup per document) --
 // Effective parent: a special keeps its cause, a non-special climbs
 // through special causes.  Siblings are ordered specials by descending id, then
@@ -490,9 +764,15 @@ __global__ __launch_bounds__(NT) void k_tree(
       }
       if (j < len && r > 0) {
         const bool sp = special_at(r);
+        // causes are older (c < r); the clamps only keep out-of-domain
+        // documents (duplicate ids leave ranks unwritten) in bounds
         uint32_t c = par[base + r];
+        c = c < r ? c : 0u;
         if (!sp)
-          while (c != 0 && special_at(c)) c = par[base + c];
+          while (c != 0 && special_at(c)) {
+            const uint32_t pc = par[base + c];
+            c = pc < c ? pc : 0u;
+          }
         key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
       }
     }
@@ -1148,15 +1428,18 @@ struct cw_ctx {
   std::vector<uint64_t> last_off;
   struct Tables {
     std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
-        wblk_doc, wblk_w0, bkt_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0;
+        wblk_doc, wblk_w0, bkt_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0, woff_base;
     std::vector<uint64_t> slot_first;
-    uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Btot = 0, Wmax = 0;
+    uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Btot = 0, Wmax = 0, Wofftot = 0;
     uint64_t slots = 0;
   } tab;
   bool tab_on_device = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
   uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
+  // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
+  uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
+  uint32_t *pin_small = nullptr;  // pinned 16-byte readback
 };
 
 namespace {
@@ -1278,6 +1561,8 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.wblk_w0.clear();
   t.eblk_doc.clear();
   t.eblk_x0.clear();
+  t.woff_base.clear();
+  uint32_t wofft = 0;
   t.doc_log2cap.resize(D);
   t.doc_Wcap.resize(D);
   t.slot_first.resize(D + 1);
@@ -1291,9 +1576,12 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
     t.doc_off[d] = b;
     t.nmax = std::max(t.nmax, n);
     t.tile_first[d] = (uint32_t)t.tile_start.size();
+    const uint32_t ntile = (n + TILE - 1) / TILE;
     for (uint32_t s = 0; s < n; s += TILE) {
       t.tile_start.push_back(b + s);
       t.tile_doc.push_back((uint32_t)d);
+      t.woff_base.push_back(wofft);  // rank-window table of this tile: ntile + 1 entries
+      wofft += ntile + 1;
     }
     // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
@@ -1335,6 +1623,7 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.slot_first[D] = slots;
   t.slots = slots;
   t.Be = (uint32_t)t.eblk_doc.size();
+  t.Wofftot = wofft;
   t.bkt_off[D] = stot;
   t.Btot = stot;
   t.T = (uint32_t)t.tile_doc.size();
@@ -1350,7 +1639,8 @@ int upload_tables(cw_ctx *c) {
       {"t_tile_first", &t.tile_first}, {"t_doc_log2k", &t.doc_log2k}, {"t_doc_W", &t.doc_W},
       {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0},
       {"t_bkt_off", &t.bkt_off}, {"t_doc_log2cap", &t.doc_log2cap},
-      {"t_doc_Wcap", &t.doc_Wcap}, {"t_eblk_doc", &t.eblk_doc}, {"t_eblk_x0", &t.eblk_x0}};
+      {"t_doc_Wcap", &t.doc_Wcap}, {"t_eblk_doc", &t.eblk_doc}, {"t_eblk_x0", &t.eblk_x0},
+      {"t_woff_base", &t.woff_base}};
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still be read
   size_t total = (t.slot_first.size() + 64) * 8;
   for (auto &it : items) total += (it.second->size() + 64) * 4;
@@ -1516,9 +1806,59 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     return fail(c, "batch too large for one dispatch (split the batch)");
 
   if (N) {
+    uint64_t *skey = nullptr;
+    uint32_t *sval = nullptr;
+    const bool want_yarns = out->yarn_perm && bt->site_bits;
+    // 1-2 (dense ids). id order and join through per-document rank directories
+    bool front_done = false;
+    if (c->front && N >= (uint64_t)c->front_min_avg * D && t.nmax <= 64 * TILE) {
+      const uint32_t SG = c->front_slot_groups;
+      uint4 *dir = scratch_t<uint4>(c, "fr_dir", (size_t)D * SG);
+      uint64_t *dkmin = scratch_t<uint64_t>(c, "fr_kmin", D);
+      uint32_t *dgroups = scratch_t<uint32_t>(c, "fr_groups", D);
+      uint32_t *big = scratch_t<uint32_t>(c, "fr_big", 4);
+      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+      if (!dir || !dkmin || !dgroups || !big) return fail(c, "out of device memory (rank directory)");
+      HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
+      {
+        Launch L(c, "fdir", (double)N * 16 + (double)N / 6.0 * 1.0);
+        hipLaunchKernelGGL(k_fdir<1024>, dim3((uint32_t)D), dim3(1024), (size_t)SG * 16, c->stream,
+                           id_key, doc_off, SG, dir, dkmin, dgroups, out->max_ts, bt->ts_shift,
+                           out->status, big);
+      }
+      if (check_launch(c, "fdir")) return -1;
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, big, 8, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      const uint32_t nbig = c->pin_small[0], gmax = c->pin_small[1];
+      if (nbig == 0) {
+        skey = want_yarns ? skA : nullptr;
+        sval = svA;
+        uint32_t *rec_meta = svB, *rec_par = (uint32_t *)skB;  // free until the yarn sort
+        uint32_t *woff = scratch_t<uint32_t>(c, "fr_woff", t.Wofftot);
+        if (!woff) return fail(c, "out of device memory (window table)");
+        {
+          Launch L(c, "frank", (double)N * (8 + 8 + 1 + 4 + 4));
+          hipLaunchKernelGGL((k_frank<512>), GT, dim3(512), (size_t)std::max(gmax, 1u) * 16,
+                             c->stream, id_key, cause_key, kind, tile_start, tile_doc,
+                             dev_tab(c, "t_tile_first"), doc_off, dev_tab(c, "t_woff_base"), dir,
+                             SG, dkmin, dgroups, rec_meta, rec_par, woff, out->status);
+        }
+        if (check_launch(c, "frank")) return -1;
+        {
+          Launch L(c, "fplace", (double)N * (4 + 4 + 4 + 4 + 1 + (skey ? 16 : 0)));
+          hipLaunchKernelGGL((k_fplace<512>), GT, dim3(512), 0, c->stream, rec_meta, rec_par,
+                             woff, dev_tab(c, "t_woff_base"), tile_start, tile_doc,
+                             dev_tab(c, "t_tile_first"), doc_off, id_key, sval, par, skind, skey);
+        }
+        if (check_launch(c, "fplace")) return -1;
+        front_done = true;
+      } else {
+        // some document's ids are too sparse for a slot: general path for the batch
+        HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
+      }
+    }
+    if (!front_done) {
     // 1. id sort
-    uint64_t *skey;
-    uint32_t *sval;
     if (radix_sort<uint64_t>(c, "idsort", id_key, nullptr, skA, svA, skB, svB, key_bits, 0, N,
                              &skey, &sval))
       return -1;
@@ -1539,6 +1879,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                          out->status);
     }
     if (check_launch(c, "join")) return -1;
+    }  // general front end
 
     // 3-5. effective parents, sibling order, links
     {
@@ -1581,7 +1922,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       Launch L(c, "rank", (double)t.Wtot * 12);
       hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
                          wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, bt->ts_shift, sbase,
-                         order, out->max_ts, out->status);
+                         order, front_done ? nullptr : out->max_ts, out->status);
     }
     if (check_launch(c, "rank")) return -1;
 
@@ -1606,7 +1947,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (check_launch(c, "packbits")) return -1;
 
     // 10. yarns: stable partition of the id order by site rank
-    if (out->yarn_perm && bt->site_bits) {
+    if (want_yarns) {
       uint64_t *yk;
       uint32_t *yv;
       uint64_t *ykA = skey == skA ? skB : skA;
@@ -1937,6 +2278,9 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_cfg = knob("CW_TREE", 1);
 
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
+  c->front = knob("CW_FRONT", 1);
+  c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
+  c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;
   return 0;
 }
@@ -1948,6 +2292,7 @@ void cw_ctx_destroy(cw_ctx *c) {
   for (auto &kv : c->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (c->pinned) (void)hipHostFree(c->pinned);
+  if (c->pin_small) (void)hipHostFree(c->pin_small);
   for (auto &p : c->pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);

@@ -19,9 +19,26 @@ from tests import refgen as G
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def weaver():
-    with abi.Weaver(0) as w:
+# Front ends: "front" = rank directories for every document (CW_FRONT_MIN_AVG=0
+# also sends tiny documents through it), "radix" = segmented radix sort + join.
+FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"}, "radix": {"CW_FRONT": "0"}}
+
+
+@pytest.fixture(scope="module", params=sorted(FRONTS))
+def weaver(request):
+    import os
+
+    old = {k: os.environ.get(k) for k in FRONTS[request.param]}
+    os.environ.update(FRONTS[request.param])
+    try:
+        w = abi.Weaver(0)  # knobs are read when the context is created
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    with w:
         yield w
 
 
@@ -185,8 +202,44 @@ def test_key_bits_found_on_device(weaver):
     assert np.array_equal(a.weave_perm, b.weave_perm)
 
 
+def test_sparse_document_falls_back(weaver):
+    """A document whose ids are too sparse for a rank-directory slot (ts gaps
+    of 2^20) sends the whole batch through the radix front end."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000)
+    off, idk, ck, kd = gen.generate(spec, 0, 6)
+    lay = spec.layout()
+    b, e = int(off[2]), int(off[3])
+    sh = np.uint64(lay.ts_shift)
+    stretch = lambda k: np.where(k == np.uint64(pack.NIL), k,
+                                 ((k >> sh) * np.uint64(1 << 20) << sh) | (k & ((np.uint64(1) << sh) - np.uint64(1))))
+    idk, ck = idk.copy(), ck.copy()
+    idk[b:e], ck[b:e] = stretch(idk[b:e]), stretch(ck[b:e])
+    wide = pack.KeyLayout(lay.ts_bits + 20, lay.site_bits, lay.tx_bits)
+    check_batch(weaver, off, idk, ck, kd, wide, method=oracle.METHOD_EFF)
+
+
+def test_duplicate_ids_beside_clean_documents(weaver):
+    """A duplicated id (shared.cljc:166-171) flags its document only; the
+    documents around it still weave exactly."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000)
+    off, idk, ck, kd = gen.generate(spec, 0, 5)
+    idk = idk.copy()
+    b = int(off[1])
+    idk[b + 10] = idk[b + 11] if idk[b + 11] != idk[b] else idk[b + 12]
+    res = weaver.weave_lists(off, idk, ck, kd, spec.layout())
+    perm, vis, st = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF)
+    assert res.status[1] & abi.STATUS_DUP and st[1] & abi.STATUS_DUP
+    assert not res.status[[0, 2, 3, 4]].any()
+    gvis = res.visible()
+    for d in (0, 2, 3, 4):
+        b, e = int(off[d]), int(off[d + 1])
+        assert np.array_equal(res.weave_perm[b:e], perm[b:e])
+        assert np.array_equal(gvis[b:e], vis[b:e])
+
+
 KNOBS = [{}, {"CW_LOG2CAP": "5"}, {"CW_LOG2K": "4", "CW_LOG2CAP": "5"},
-         {"CW_MAX_DIGIT": "8"}, {"CW_WALK_THREADS": "256", "CW_WALK_SPAN": "512"}]
+         {"CW_MAX_DIGIT": "8"}, {"CW_WALK_THREADS": "256", "CW_WALK_SPAN": "512"},
+         {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"}]
 
 
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
