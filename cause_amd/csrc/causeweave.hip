@@ -713,9 +713,19 @@ __global__ __launch_bounds__(NT) void k_tree(
     const uint32_t *__restrict__ doc_log2k, uint32_t kbits, uint32_t bm_words,
     uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ fcN, uint32_t *__restrict__ thr, uint32_t *__restrict__ link,
-    uint32_t *__restrict__ status) {
+    uint32_t *__restrict__ status, unsigned long long *__restrict__ tprof) {
   constexpr uint32_t IT = TILE_T / NT;
-  __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T];
+  // diagnostic phase stamps (tprof != nullptr only under CW_TREE_PROF)
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto stamp = [&](int ph) {
+    if (tprof) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tacc[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  stamp(-1);
+  __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T], ptab[TILE_T];
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
   __shared__ uint32_t run[64];
   // special / hide bit per rank (LDS when the document fits bm_words words)
@@ -725,23 +735,34 @@ __global__ __launch_bounds__(NT) void k_tree(
   const bool in_lds = ((n + 31) >> 5) <= bm_words;
   uint32_t *spec_bm = bm, *hide_bm = bm + bm_words;
   if (in_lds) {
-    // one ballot per wave per 64 ranks: bit r of the bitmap = special(rank r)
-    for (uint32_t r0 = (tid >> 6) << 6; r0 < n; r0 += NT) {
-      const uint32_t r = r0 + (tid & 63);
-      const uint8_t kd = r < n ? skind[base + r] : 0;
-      const uint64_t sm = __ballot(r < n && is_special(kd));
-      const uint64_t hm = __ballot(r < n && is_hide(kd));
-      if ((tid & 63) == 0) {
-        spec_bm[r0 >> 5] = (uint32_t)sm;
-        hide_bm[r0 >> 5] = (uint32_t)hm;
-        if ((r0 >> 5) + 1 < bm_words) {
-          spec_bm[(r0 >> 5) + 1] = (uint32_t)(sm >> 32);
-          hide_bm[(r0 >> 5) + 1] = (uint32_t)(hm >> 32);
+    // one ballot per wave per 64 ranks: bit r of the bitmap = special(rank r);
+    // eight loads in flight per lane
+    constexpr uint32_t BU = 8;
+    for (uint32_t rb = (tid >> 6) << 6; rb < n; rb += NT * BU) {
+      uint8_t kd[BU];
+#pragma unroll
+      for (uint32_t u = 0; u < BU; u++) {
+        const uint32_t r = rb + u * NT + (tid & 63);
+        kd[u] = r < n ? skind[base + r] : 0;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < BU; u++) {
+        const uint32_t r0 = rb + u * NT, r = r0 + (tid & 63);
+        const uint64_t sm = __ballot(r < n && is_special(kd[u]));
+        const uint64_t hm = __ballot(r < n && is_hide(kd[u]));
+        if ((tid & 63) == 0 && r0 < n) {
+          spec_bm[r0 >> 5] = (uint32_t)sm;
+          hide_bm[r0 >> 5] = (uint32_t)hm;
+          if ((r0 >> 5) + 1 < bm_words) {
+            spec_bm[(r0 >> 5) + 1] = (uint32_t)(sm >> 32);
+            hide_bm[(r0 >> 5) + 1] = (uint32_t)(hm >> 32);
+          }
         }
       }
     }
     __syncthreads();
   }
+  stamp(0);
   auto special_at = [&](uint32_t r) -> bool {
     return in_lds ? ((spec_bm[r >> 5] >> (r & 31)) & 1u) : is_special(skind[base + r]);
   };
@@ -776,6 +797,17 @@ __global__ __launch_bounds__(NT) void k_tree(
         key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
       }
     }
+    // the group's last node of earlier tiles, loaded now so the load overlaps
+    // the sort (earlier tiles' updates are complete: barrier at tile end); a
+    // parent inside this tile has no children in earlier tiles (and its
+    // entries were only just cleared above)
+    uint32_t ptv[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t kk = key[k], e = (kk >> 1) - 1;
+      ptv[k] = (kk && e < r0) ? ((kk & 1) ? fcN : fcS)[base + e] : 0u;
+    }
+    stamp(1);
     // stable LDS sort of the tile by group key, 6 bits per sub-pass
     for (uint32_t shift = 0; shift < kbits; shift += SUB_BITS) {
 #pragma unroll
@@ -787,6 +819,10 @@ __global__ __launch_bounds__(NT) void k_tree(
           tkey[pos[k]] = key[k];
           trank[pos[k]] = rk[k];
         }
+      if (shift + SUB_BITS >= kbits) {
+#pragma unroll
+        for (uint32_t k = 0; k < IT; k++) ptab[wb_elem<IT>(k)] = ptv[k];
+      }
       __syncthreads();
 #pragma unroll
       for (uint32_t k = 0; k < IT; k++) {
@@ -798,6 +834,7 @@ __global__ __launch_bounds__(NT) void k_tree(
       }
       __syncthreads();
     }
+    stamp(2);
     // next sibling inside the class: previous node of the group; a group's
     // first node in the tile takes the group's last node of earlier tiles
     uint32_t prv[IT];
@@ -810,8 +847,7 @@ __global__ __launch_bounds__(NT) void k_tree(
         if (j > 0 && tkey[j - 1] == kk) {
           prv[k] = r0 + trank[j - 1];
         } else {
-          uint32_t *tab = (kk & 1) ? fcN : fcS;
-          prv[k] = tab[base + (kk >> 1) - 1];
+          prv[k] = ptab[rk[k]];
         }
       }
     }
@@ -832,6 +868,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     }
     for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
     __syncthreads();
+    stamp(3);
   }
   // the sweep below reads what this workgroup wrote above: all waves of a
   // workgroup share one CU and its L1, so the barrier's workgroup-scope
@@ -843,41 +880,62 @@ __global__ __launch_bounds__(NT) void k_tree(
   // sweep in rank order resolves each tile from earlier tiles' threads (thr,
   // global) plus pointer jumping over the tile's own parents in LDS.
   constexpr uint32_t RES = 0x80000000u;
-  uint32_t *T = tkey;
+  // T: this tile's threads (pointer jumping); P: the previous tile's resolved
+  // threads, so a parent in the previous tile needs no global read.  The next
+  // tile's fcS/fcN/nsc are loaded while this tile is resolved.
+  uint32_t *T = tkey, *P = trank;
+  uint32_t qfs[IT], qfn[IT], qns[IT];
+  auto load_tile = [&](uint32_t r0) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t r = r0 + k * NT + tid;
+      const bool ok = r < n;
+      qfs[k] = ok ? fcS[base + r] : 0u;
+      qfn[k] = ok ? fcN[base + r] : 0u;
+      qns[k] = ok ? nsc[base + r] : 0u;
+    }
+  };
+  load_tile(0);
   for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
     const uint32_t len = min((uint32_t)TILE_T, n - r0);
-    uint32_t fcr[IT], flg[IT];
+    uint32_t fs4[IT], ns4[IT], fcr[IT], flg[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      fs4[k] = qfs[k];
+      fcr[k] = qfs[k] ? qfs[k] : qfn[k];
+      ns4[k] = qns[k];
+    }
+    if (r0 + TILE_T < n) load_tile(r0 + TILE_T);
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = k * NT + tid, r = r0 + j;
-      fcr[k] = 0;
       flg[k] = 0;
       if (j >= len) continue;
       const bool sp = special_at(r);
-      const uint32_t fs = fcS[base + r], fn = fcN[base + r];
-      fcr[k] = fs ? fs : fn;
       uint32_t tv;
       if (r == 0) {
         tv = RES | SUCC_END;
       } else {
-        uint32_t ns = nsc[base + r], e = 0;
+        uint32_t ns = ns4[k], e = 0;
         if (ns & NSC_UP) {
           e = ns & ~NSC_UP;
           ns = sp ? fcN[base + e] : 0u;  // last special -> newest non-special
         }
         if (ns) tv = RES | ns;
-        else if (e < r0)
-          tv = RES | thr[base + e];
-        else tv = e - r0;
+        else if (e >= r0) tv = e - r0;
+        else if (e + TILE_T >= r0) tv = P[e + TILE_T - r0];
+        else tv = RES | thr[base + e];
       }
       T[j] = tv;
       // after a non-special comes its first child, which is its
       // newest special child when it has one.
+      const uint32_t fs = fs4[k];
       const bool vis = !sp && r != 0 && !(fs && hide_at(fs));
       const bool split = r == split_node(d, r >> log2k, log2k, n);
       flg[k] = (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
     }
     __syncthreads();
+    stamp(4);
     for (;;) {  // pointer jumping: every value stays an ancestor's thread or pointer
       bool open = false;
 #pragma unroll
@@ -894,6 +952,7 @@ __global__ __launch_bounds__(NT) void k_tree(
       }
       if (!__syncthreads_or(open)) break;
     }
+    stamp(5);
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = k * NT + tid, r = r0 + j;
@@ -903,7 +962,13 @@ __global__ __launch_bounds__(NT) void k_tree(
       link[base + r] = (fcr[k] ? fcr[k] : th) | flg[k];
     }
     __syncthreads();
+    stamp(6);
+    uint32_t *x = T;  // this tile's resolved threads become the previous tile's
+    T = P;
+    P = x;
   }
+  if (tprof && tid == 0)
+    for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
 }
 
 // Walker w of document d starts at the splitter node of rank block w and
@@ -1440,6 +1505,7 @@ struct cw_ctx {
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
+  uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
 };
 
 namespace {
@@ -1888,21 +1954,37 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
       // par, skind in; nsc, last-node tables, thr, link out; sweep 2 reads nsc
       // and the tables back
+      unsigned long long *tprof = nullptr;
+      if (c->tree_prof) {
+        tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 8);
+        HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
+      }
       Launch L(c, "tree", (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
       if (c->tree_cfg == 2)
         hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
       else if (c->tree_cfg == 1)
         hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
       else
         hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
     }
     if (check_launch(c, "tree")) return -1;
+    if (c->tree_prof) {
+      std::vector<unsigned long long> h((size_t)D * 8);
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 64, hipMemcpyDeviceToHost));
+      double acc[8] = {0};
+      for (uint64_t d = 0; d < D; d++)
+        for (int ph = 0; ph < 8; ph++) acc[ph] += (double)h[d * 8 + ph];
+      fprintf(stderr, "tree phases (memtime ticks per doc): bitmap %.0f climb %.0f sort %.0f prv %.0f "
+              "s2load %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
+              acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
+    }
 
     // 6. Euler walk
     HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
@@ -2275,10 +2357,11 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
   c->min_log2cap = std::max(2u, knob("CW_LOG2CAP", 4));
-  c->tree_cfg = knob("CW_TREE", 1);
+  c->tree_cfg = knob("CW_TREE", 2);
 
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
   c->front = knob("CW_FRONT", 1);
+  c->tree_prof = knob("CW_TREE_PROF", 0);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;
