@@ -47,6 +47,16 @@ class CwMapResult(C.Structure):
                 ("seg_perm", C.c_void_p), ("status", C.c_void_p)]
 
 
+class CwMergeBatch(C.Structure):
+    _fields_ = [("a", CwListBatch), ("a_value", C.c_void_p), ("b", CwListBatch),
+                ("b_value", C.c_void_p)]
+
+
+class CwMergeResult(C.Structure):
+    _fields_ = [("merged_offsets", C.POINTER(C.c_uint64)), ("merged_src", C.c_void_p),
+                ("weave", CwListResult)]
+
+
 class CwKernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double),
                 ("bytes_alg", C.c_double)]
@@ -91,6 +101,9 @@ def lib():
         L.cw_weave_maps.argtypes = [C.c_void_p, C.POINTER(CwMapBatch), C.POINTER(CwMapResult),
                                     C.c_int]
         L.cw_weave_maps.restype = C.c_int
+        L.cw_merge_lists.argtypes = [C.c_void_p, C.POINTER(CwMergeBatch),
+                                     C.POINTER(CwMergeResult), C.c_int]
+        L.cw_merge_lists.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -109,6 +122,22 @@ class ListResult:
         n = len(self.weave_perm)
         b = np.unpackbits(self.visible_bits.view(np.uint8), bitorder="little")
         return b[:n]
+
+
+@dataclass
+class MergeResult:
+    """Union of two node bags per document and its weave (cw_merge_lists)."""
+    offsets: np.ndarray      # uint64[D+1] merged documents
+    src: np.ndarray          # uint32[M] merged nodes in id order: < na_d -> a, else b (- na_d)
+    weave: ListResult        # weave_perm holds doc-local merged indices (into src)
+
+    def weave_src(self) -> np.ndarray:
+        """uint32[M]: source index (as in src) of every weave position."""
+        out = np.empty_like(self.weave.weave_perm)
+        for d in range(len(self.offsets) - 1):
+            lo, hi = int(self.offsets[d]), int(self.offsets[d + 1])
+            out[lo:hi] = self.src[lo:hi][self.weave.weave_perm[lo:hi]]
+        return out
 
 
 @dataclass
@@ -224,6 +253,42 @@ class Weaver:
                          g("status"), g("yarn_perm"))
         self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
                     "cw_weave_lists")
+
+    def merge_lists(self, a, b, layout, yarns=True) -> MergeResult:
+        """Host-memory call of cw_merge_lists.  a, b: (offsets, id_key, cause_key,
+        kind, value_token) per side, with the same number of documents."""
+        def side(t):
+            off, i, c, k, v = t
+            off = np.ascontiguousarray(off, np.uint64)
+            arrs = (np.ascontiguousarray(i, np.uint64), np.ascontiguousarray(c, np.uint64),
+                    np.ascontiguousarray(k, np.uint8), np.ascontiguousarray(v, np.uint64))
+            if int(off[-1]) != len(arrs[0]):
+                raise ValueError("offsets[-1] != number of nodes")
+            return off, arrs
+        ao, (ai, ac, ak, av) = side(a)
+        bo, (bi, bc, bk, bv) = side(b)
+        if len(ao) != len(bo):
+            raise ValueError("a and b must have the same number of documents")
+        D, NC = len(ao) - 1, len(ai) + len(bi)
+        ba, _ = self._batch(ao, _ptr(ai), _ptr(ac), _ptr(ak), layout)
+        bb, _ = self._batch(bo, _ptr(bi), _ptr(bc), _ptr(bk), layout)
+        mb = CwMergeBatch(ba, _ptr(av), bb, _ptr(bv))
+        mo = np.zeros(D + 1, np.uint64)
+        src = np.zeros(max(NC, 1), np.uint32)
+        w = ListResult(np.zeros(max(NC, 1), np.uint32), np.zeros((NC + 31) // 32 + 1, np.uint32),
+                       np.zeros(max(D, 1), np.uint32), np.zeros(max(D, 1), np.uint64),
+                       np.zeros(max(D, 1), np.uint32),
+                       np.zeros(max(NC, 1), np.uint32) if (yarns and layout.site_bits) else None)
+        r = CwMergeResult(mo.ctypes.data_as(C.POINTER(C.c_uint64)), _ptr(src),
+                          CwListResult(_ptr(w.weave_perm), _ptr(w.visible_bits),
+                                       _ptr(w.visible_count), _ptr(w.max_ts), _ptr(w.status),
+                                       _ptr(w.yarn_perm)))
+        self._check(self._L.cw_merge_lists(self._h, C.byref(mb), C.byref(r), CW_MEM_HOST),
+                    "cw_merge_lists")
+        M = int(mo[-1])
+        w = ListResult(w.weave_perm[:M], w.visible_bits[:(M + 31) // 32], w.visible_count[:D],
+                       w.max_ts[:D], w.status[:D], None if w.yarn_perm is None else w.yarn_perm[:M])
+        return MergeResult(mo, src[:M], w)
 
     def weave_maps(self, offsets, id_key, cause, cause_is_id, kind, token_bits,
                    key_bits=0) -> MapResult:

@@ -7,7 +7,8 @@ Every ``weave`` arity is a full reweave on the MI355X through the C ABI
 (cw_weave_lists) -- exact by SURVEY F7 (incremental insertion in any causal
 order equals the full reweave).  There is no CPU weave in this module.
 
-    shared.cljc:151-192   insert / append           -> insert, append
+    shared.cljc:151-192   insert / append           -> insert, append, insert_bulk
+    shared.cljc:300-314   merge-trees               -> merge_trees / merge_lists (cw_merge_lists)
     shared.cljc:259-266   refresh-caches            -> refresh_caches
     list.cljc:20-34       weave (all arities)       -> list_weave / weave_lists
     list.cljc:36-43       conj- / cons-             -> list_conj / list_cons
@@ -166,6 +167,95 @@ def insert(weave_fn, ct, node, more=None):
     woven = dict(woven)
     woven["lamport_ts"] = out["lamport_ts"]
     return woven
+
+
+class _Tokens:
+    """Value identity for the merge's body check (equal values <=> equal token)."""
+
+    def __init__(self):
+        self.t = {}
+
+    def __call__(self, v):
+        try:
+            key = ("h", type(v).__name__, v)
+            hash(key)
+        except TypeError:
+            key = ("r", repr(v))
+        return self.t.setdefault(key, len(self.t))
+
+
+def merge_lists(pairs):
+    """s/merge-trees (shared.cljc:300-314) for many (ct1, ct2) list pairs in ONE
+    GPU call (cw_merge_lists): the union of the two ::nodes maps, deduplicated,
+    then the full reweave.  Same checks and ex-info causes as the
+    reference; see include/causeweave.h for the one divergence (the reference
+    can also throw :cause-must-exist because of its hash-map insertion order)."""
+    for ct1, ct2 in pairs:
+        if ct1["type"] != ct2["type"]:
+            raise CauseError("Causal type missmatch. Merge not allowed.", {"type-missmatch"})
+        if ct1["uuid"] != ct2["uuid"]:
+            raise CauseError("Causal UUID missmatch. Merge not allowed.", {"uuid-missmatch"})
+    da = [[(i, b[0], b[1]) for i, b in ct1["nodes"].items()] for ct1, _ in pairs]
+    db = [[(i, b[0], b[1]) for i, b in ct2["nodes"].items()] for _, ct2 in pairs]
+    pk = pack.pack_lists([a + b for a, b in zip(da, db)])  # one site ranking per pair
+    tok = _Tokens()
+    ia, ib = [], []
+    for d, (a, b) in enumerate(zip(da, db)):
+        lo = int(pk.offsets[d])
+        ia.append(np.arange(lo, lo + len(a)))
+        ib.append(np.arange(lo + len(a), lo + len(a) + len(b)))
+    ia = np.concatenate(ia) if ia else np.zeros(0, np.int64)
+    ib = np.concatenate(ib) if ib else np.zeros(0, np.int64)
+    vals = np.array([tok(n[2]) for d in pk.docs for n in d.nodes], np.uint64)
+    off_a = np.zeros(len(pairs) + 1, np.uint64)
+    off_a[1:] = np.cumsum([len(a) for a in da])
+    off_b = np.zeros(len(pairs) + 1, np.uint64)
+    off_b[1:] = np.cumsum([len(b) for b in db])
+    side = lambda idx, off: (off, pk.id_key[idx], pk.cause_key[idx], pk.kind[idx], vals[idx])
+    res = weaver().merge_lists(side(ia, off_a), side(ib, off_b), pk.layout)
+    vis = res.weave.visible()
+    out = []
+    for d, ((ct1, ct2), a, b) in enumerate(zip(pairs, da, db)):
+        st = int(res.weave.status[d])
+        if st & abi.STATUS_DUP:
+            raise CauseError("This node is already in the tree and can't be changed.",
+                             {"append-only", "edits-not-allowed"})
+        if st & abi.STATUS_ORPHAN:
+            raise CauseError("The cause of this node is not in the tree.", {"cause-must-exist"})
+        if st:
+            raise CauseError(f"document outside the weave's domain (status {st})", {"weave-domain"})
+        lo, hi = int(res.offsets[d]), int(res.offsets[d + 1])
+        src = res.src[lo:hi]
+        node_of = lambda s: a[s] if s < len(a) else b[s - len(a)]
+        merged = [node_of(int(s)) for s in src]
+        new = dict(ct1)
+        new["nodes"] = {n[0]: (n[1], n[2]) for n in merged}
+        new["weave"] = [merged[p] for p in res.weave.weave_perm[lo:hi]]
+        new["_visible"] = [bool(v) for v in vis[lo:hi]]
+        yarns = {}
+        for p in res.weave.yarn_perm[lo:hi]:
+            nd = merged[p]
+            yarns.setdefault(nd[0][1], []).append(nd)
+        new["yarns"] = yarns
+        # insert fast-forwards ::lamport-ts to every newly inserted node (shared.cljc:179-181)
+        fresh = [merged[i][0][0] for i, s in enumerate(src) if s >= len(a)]
+        new["lamport_ts"] = max([ct1["lamport_ts"]] + fresh)
+        new["_max_ts"] = int(res.weave.max_ts[d])
+        out.append(new)
+    return out
+
+
+def merge_trees(weave_fn, ct1, ct2):
+    """shared.cljc:300-314 (lists; the weave-fn is the GPU weave)."""
+    return merge_lists([(ct1, ct2)])[0]
+
+
+def insert_bulk(ct, nodes):
+    """Many s/insert calls (shared.cljc:151-184) in causal order, as one GPU
+    merge of ``nodes`` into ``ct``."""
+    ct2 = dict(ct)
+    ct2["nodes"] = {n[0]: (n[1], n[2]) for n in nodes}
+    return merge_trees(list_weave, ct, ct2)
 
 
 def append(weave_fn, ct, cause, value):

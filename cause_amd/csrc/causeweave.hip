@@ -1453,6 +1453,89 @@ __global__ __launch_bounds__(256) void k_seg_active(
 }
 
 // ============================================================================
+// Merge (s/merge-trees, shared.cljc:300-314; bulk s/insert, :151-184): union
+// of two node bags per document, deduplicated by id, then the list pipeline.
+// ============================================================================
+// Document d's a-nodes then b-nodes into one capacity slot [coff[d], coff[d+1]).
+__global__ __launch_bounds__(256) void k_merge_concat(
+    const uint64_t *__restrict__ aid, const uint64_t *__restrict__ acause,
+    const uint8_t *__restrict__ akind, const uint64_t *__restrict__ aval,
+    const uint64_t *__restrict__ bid, const uint64_t *__restrict__ bcause,
+    const uint8_t *__restrict__ bkind, const uint64_t *__restrict__ bval,
+    const uint32_t *__restrict__ aoff, const uint32_t *__restrict__ boff,
+    const uint32_t *__restrict__ coff, uint64_t *__restrict__ cid,
+    uint64_t *__restrict__ ccause, uint8_t *__restrict__ ckind, uint64_t *__restrict__ cval) {
+  const uint32_t d = blockIdx.x;
+  const uint32_t a0 = aoff[d], na = aoff[d + 1] - a0, b0 = boff[d], nb = boff[d + 1] - b0;
+  const uint32_t c0 = coff[d];
+  for (uint32_t i = threadIdx.x; i < na + nb; i += blockDim.x) {
+    const bool fa = i < na;
+    const uint32_t g = fa ? a0 + i : b0 + (i - na);
+    cid[c0 + i] = fa ? aid[g] : bid[g];
+    ccause[c0 + i] = fa ? acause[g] : bcause[g];
+    ckind[c0 + i] = fa ? akind[g] : bkind[g];
+    cval[c0 + i] = fa ? aval[g] : bval[g];
+  }
+}
+
+// Walks document d's id-sorted capacity slot: a node is kept when its id
+// differs from its predecessor's; a repeated id must repeat the body (cause,
+// kind, value token) or the document gets CW_STATUS_DUP.  pass 0 counts the
+// kept nodes (mcount[d]); pass 1 writes them at moff[d] (ids in order, causes,
+// kinds and source indices).
+template <int NT>
+__global__ __launch_bounds__(NT) void k_merge_dedup(
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ ccause, const uint8_t *__restrict__ ckind,
+    const uint64_t *__restrict__ cval, const uint32_t *__restrict__ coff, int pass,
+    uint32_t *__restrict__ mcount, const uint32_t *__restrict__ moff,
+    uint64_t *__restrict__ mid, uint64_t *__restrict__ mcause, uint8_t *__restrict__ mkind,
+    uint32_t *__restrict__ msrc, uint32_t *__restrict__ mstatus) {
+  __shared__ uint32_t wtot[NT / 64];
+  const uint32_t d = blockIdx.x, c0 = coff[d], n = coff[d + 1] - c0;
+  uint32_t run = 0;
+  bool conflict = false;
+  for (uint32_t i0 = 0; i0 < n; i0 += NT) {
+    const uint32_t i = i0 + threadIdx.x;
+    bool keep = false;
+    uint64_t k = 0;
+    uint32_t v = 0;
+    if (i < n) {
+      k = skey[c0 + i];
+      v = sval[c0 + i];
+      keep = i == 0 || skey[c0 + i - 1] != k;
+      if (!keep && pass == 0) {
+        const uint32_t u = sval[c0 + i - 1];
+        conflict |= ccause[c0 + u] != ccause[c0 + v] || ckind[c0 + u] != ckind[c0 + v] ||
+                    cval[c0 + u] != cval[c0 + v];
+      }
+    }
+    uint32_t tot;
+    const uint32_t pos = run + block_exscan<NT>(keep ? 1u : 0u, wtot, &tot);
+    if (pass == 1 && keep) {
+      const uint32_t o = moff[d] + pos;
+      mid[o] = k;
+      mcause[o] = ccause[c0 + v];
+      mkind[o] = ckind[c0 + v];
+      msrc[o] = v;
+    }
+    run += tot;
+  }
+  if (pass == 0) {
+    if (__syncthreads_or(conflict) && threadIdx.x == 0) mstatus[d] = CW_STATUS_DUP;
+    else if (threadIdx.x == 0) mstatus[d] = 0;
+    if (threadIdx.x == 0) mcount[d] = run;
+  }
+}
+
+// merged weave positions -> doc-local merged index is what the list pipeline
+// returns already; status of the union (conflicts) joins the weave's.
+__global__ void k_or_status(const uint32_t *__restrict__ a, uint32_t *__restrict__ b, uint32_t D) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d < D) b[d] |= a[d];
+}
+
+// ============================================================================
 // Host side
 // ============================================================================
 
@@ -2324,6 +2407,151 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   return 0;
 }
 
+int merge_lists_impl(cw_ctx *c, const cw_merge_batch *bt, cw_merge_result *res, int memspace) {
+  if (!bt || !res) return fail(c, "null batch/result");
+  if (memspace != CW_MEM_HOST) return fail(c, "cw_merge_lists: only CW_MEM_HOST is supported");
+  const uint64_t D = bt->a.n_docs;
+  if (bt->b.n_docs != D) return fail(c, "a and b must have the same number of documents");
+  const uint64_t *ao = bt->a.doc_offsets, *bo = bt->b.doc_offsets;
+  if (!ao || !bo || ao[0] != 0 || bo[0] != 0) return fail(c, "doc_offsets must start at 0");
+  const uint64_t Na = ao[D], Nb = bo[D], NC = Na + Nb;
+  if (NC >= 0x7FFFFFFFull) return fail(c, "merge too large: %llu nodes", (unsigned long long)NC);
+  std::vector<uint32_t> h_ao(D + 1), h_bo(D + 1), h_co(D + 1);
+  std::vector<uint64_t> cap(D + 1);
+  for (uint64_t d = 0; d <= D; d++) {
+    if (d < D && (ao[d + 1] < ao[d] || bo[d + 1] < bo[d])) return fail(c, "doc_offsets not monotone");
+    h_ao[d] = (uint32_t)ao[d];
+    h_bo[d] = (uint32_t)bo[d];
+    cap[d] = ao[d] + bo[d];
+    h_co[d] = (uint32_t)cap[d];
+  }
+  for (uint64_t d = 0; d < D; d++)
+    if (cap[d + 1] - cap[d] >= LINK_IDX) return fail(c, "document %llu too large", (unsigned long long)d);
+  cw_list_result &W = res->weave;
+  if (!res->merged_offsets || !res->merged_src || !W.weave_perm || !W.visible_count || !W.status)
+    return fail(c, "merged_offsets, merged_src, weave_perm, visible_count and status are required");
+  if ((Na && (!bt->a.id_key || !bt->a.cause_key || !bt->a.kind || !bt->a_value)) ||
+      (Nb && (!bt->b.id_key || !bt->b.cause_key || !bt->b.kind || !bt->b_value)))
+    return fail(c, "null input arrays");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t NCs = std::max<uint64_t>(NC, 1);
+  uint64_t *aid = scratch_t<uint64_t>(c, "g_aid", std::max<uint64_t>(Na, 1)),
+           *aca = scratch_t<uint64_t>(c, "g_aca", std::max<uint64_t>(Na, 1)),
+           *ava = scratch_t<uint64_t>(c, "g_ava", std::max<uint64_t>(Na, 1));
+  uint64_t *bid = scratch_t<uint64_t>(c, "g_bid", std::max<uint64_t>(Nb, 1)),
+           *bca = scratch_t<uint64_t>(c, "g_bca", std::max<uint64_t>(Nb, 1)),
+           *bva = scratch_t<uint64_t>(c, "g_bva", std::max<uint64_t>(Nb, 1));
+  uint8_t *akd = scratch_t<uint8_t>(c, "g_akd", std::max<uint64_t>(Na, 1)),
+          *bkd = scratch_t<uint8_t>(c, "g_bkd", std::max<uint64_t>(Nb, 1));
+  uint32_t *dao = scratch_t<uint32_t>(c, "g_aoff", D + 1), *dbo = scratch_t<uint32_t>(c, "g_boff", D + 1),
+           *dco = scratch_t<uint32_t>(c, "g_coff", D + 1), *dmo = scratch_t<uint32_t>(c, "g_moff", D + 1);
+  uint64_t *cid = scratch_t<uint64_t>(c, "g_cid", NCs), *cca = scratch_t<uint64_t>(c, "g_cca", NCs),
+           *cva = scratch_t<uint64_t>(c, "g_cva", NCs);
+  uint8_t *ckd = scratch_t<uint8_t>(c, "g_ckd", NCs);
+  uint64_t *mid = scratch_t<uint64_t>(c, "g_mid", NCs), *mca = scratch_t<uint64_t>(c, "g_mca", NCs);
+  uint8_t *mkd = scratch_t<uint8_t>(c, "g_mkd", NCs);
+  uint32_t *msrc = scratch_t<uint32_t>(c, "g_msrc", NCs), *mcnt = scratch_t<uint32_t>(c, "g_mcnt", D + 1),
+           *mst = scratch_t<uint32_t>(c, "g_mst", D + 1);
+  uint64_t *uskA = scratch_t<uint64_t>(c, "g_skA", NCs), *uskB = scratch_t<uint64_t>(c, "g_skB", NCs);
+  uint32_t *usvA = scratch_t<uint32_t>(c, "g_svA", NCs), *usvB = scratch_t<uint32_t>(c, "g_svB", NCs);
+  if (!aid || !aca || !ava || !bid || !bca || !bva || !akd || !bkd || !dao || !dbo || !dco || !dmo ||
+      !cid || !cca || !cva || !ckd || !mid || !mca || !mkd || !msrc || !mcnt || !mst || !uskA ||
+      !uskB || !usvA || !usvB)
+    return fail(c, "out of device memory (merge, N=%llu)", (unsigned long long)NC);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (Na) {
+    HIPCHK(c, hipMemcpy(aid, bt->a.id_key, Na * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(aca, bt->a.cause_key, Na * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(ava, bt->a_value, Na * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(akd, bt->a.kind, Na, hipMemcpyHostToDevice));
+  }
+  if (Nb) {
+    HIPCHK(c, hipMemcpy(bid, bt->b.id_key, Nb * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(bca, bt->b.cause_key, Nb * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(bva, bt->b_value, Nb * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(bkd, bt->b.kind, Nb, hipMemcpyHostToDevice));
+  }
+  HIPCHK(c, hipMemcpy(dao, h_ao.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(dbo, h_bo.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(dco, h_co.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  if (!grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
+  uint64_t *mo = res->merged_offsets;
+  mo[0] = 0;
+  if (NC == 0) {
+    for (uint64_t d = 0; d < D; d++) {
+      mo[d + 1] = 0;
+      W.status[d] = CW_STATUS_ROOT;
+      W.visible_count[d] = 0;
+      if (W.max_ts) W.max_ts[d] = 0;
+    }
+    return 0;
+  }
+  // 1. union: a then b per document, in capacity slots
+  hipLaunchKernelGGL(k_merge_concat, dim3((uint32_t)D), dim3(256), 0, c->stream, aid, aca, akd,
+                     ava, bid, bca, bkd, bva, dao, dbo, dco, cid, cca, ckd, cva);
+  if (check_launch(c, "merge_concat")) return -1;
+  // 2. id order per capacity slot (the general segmented radix sort)
+  if (ensure_tables(c, D, cap.data())) return -1;
+  uint32_t key_bits = bt->a.key_bits;
+  if (key_bits == 0 && find_key_bits(c, cid, (uint32_t)NC, &key_bits)) return -1;
+  uint64_t *skey;
+  uint32_t *sval;
+  if (radix_sort<uint64_t>(c, "m_idsort", cid, nullptr, uskA, usvA, uskB, usvB, key_bits, 0,
+                           (uint32_t)NC, &skey, &sval))
+    return -1;
+  // 3. dedup: count, offsets, write
+  hipLaunchKernelGGL((k_merge_dedup<1024>), dim3((uint32_t)D), dim3(1024), 0, c->stream, skey, sval,
+                     cca, ckd, cva, dco, 0, mcnt, dmo, mid, mca, mkd, msrc, mst);
+  if (check_launch(c, "merge_count")) return -1;
+  std::vector<uint32_t> h_cnt(D);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(h_cnt.data(), mcnt, D * 4, hipMemcpyDeviceToHost));
+  std::vector<uint32_t> h_mo(D + 1);
+  for (uint64_t d = 0; d < D; d++) {
+    mo[d + 1] = mo[d] + h_cnt[d];
+    h_mo[d] = (uint32_t)mo[d];
+  }
+  h_mo[D] = (uint32_t)mo[D];
+  HIPCHK(c, hipMemcpy(dmo, h_mo.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL((k_merge_dedup<1024>), dim3((uint32_t)D), dim3(1024), 0, c->stream, skey, sval,
+                     cca, ckd, cva, dco, 1, mcnt, dmo, mid, mca, mkd, msrc, mst);
+  if (check_launch(c, "merge_write")) return -1;
+  // 4. the merged documents through the list pipeline
+  const uint64_t NM = mo[D];
+  if (ensure_tables(c, D, mo)) return -1;
+  cw_list_batch lb = bt->a;
+  lb.doc_offsets = mo;
+  lb.key_bits = key_bits;
+  cw_list_result lr{};
+  lr.weave_perm = scratch_t<uint32_t>(c, "g_perm", NCs);
+  lr.visible_bits = W.visible_bits ? scratch_t<uint32_t>(c, "g_bits", (NCs + 31) / 32) : nullptr;
+  lr.visible_count = scratch_t<uint32_t>(c, "g_vc", D + 1);
+  lr.max_ts = W.max_ts ? scratch_t<uint64_t>(c, "g_mts", D + 1) : nullptr;
+  lr.status = scratch_t<uint32_t>(c, "g_st", D + 1);
+  lr.yarn_perm = W.yarn_perm ? scratch_t<uint32_t>(c, "g_yarn", NCs) : nullptr;
+  if (!lr.weave_perm || !lr.visible_count || !lr.status || (W.visible_bits && !lr.visible_bits) ||
+      (W.max_ts && !lr.max_ts) || (W.yarn_perm && !lr.yarn_perm))
+    return fail(c, "out of device memory (merge outputs)");
+  if (weave_lists_device(c, &lb, mid, mca, mkd, &lr)) return -1;
+  hipLaunchKernelGGL(k_or_status, dim3((uint32_t)((D + 255) / 256)), dim3(256), 0, c->stream, mst,
+                     lr.status, (uint32_t)D);
+  if (check_launch(c, "or_status")) return -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(res->merged_src, msrc, NM * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(W.weave_perm, lr.weave_perm, NM * 4, hipMemcpyDeviceToHost));
+  if (W.visible_bits)
+    HIPCHK(c, hipMemcpy(W.visible_bits, lr.visible_bits, (NM + 31) / 32 * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(W.visible_count, lr.visible_count, D * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(W.status, lr.status, D * 4, hipMemcpyDeviceToHost));
+  if (W.max_ts) HIPCHK(c, hipMemcpy(W.max_ts, lr.max_ts, D * 8, hipMemcpyDeviceToHost));
+  if (W.yarn_perm) HIPCHK(c, hipMemcpy(W.yarn_perm, lr.yarn_perm, NM * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipDeviceSynchronize());
+  for (uint64_t d = 0; d < D; d++)
+    if (mo[d + 1] == mo[d]) W.status[d] |= CW_STATUS_ROOT;
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -2432,6 +2660,12 @@ int cw_weave_maps(cw_ctx *c, const cw_map_batch *b, cw_map_result *r, int memspa
   if (!c) return -1;
   c->err.clear();
   return weave_maps_impl(c, b, r, memspace);
+}
+
+int cw_merge_lists(cw_ctx *c, const cw_merge_batch *b, cw_merge_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  return merge_lists_impl(c, b, r, memspace);
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

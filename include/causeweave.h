@@ -174,6 +174,41 @@ typedef struct {
 /* Host memory only (memspace must be CW_MEM_HOST in this version). */
 int cw_weave_maps(cw_ctx *ctx, const cw_map_batch *batch, cw_map_result *result, int memspace);
 
+/* ---------------------------------------------------------------- merge ---- */
+/* Union of two node bags per document followed by a full reweave: the result
+ * of s/merge-trees (shared.cljc:300-314) and of a bulk s/insert (:151-184),
+ * which equal the full reweave of the union.  Per document d the
+ * nodes of a (ct1) and b (ct2) are united by id:
+ *   - the same id with the same body (cause, kind, value token) is kept once
+ *     (insert's idempotency, shared.cljc:164-165);
+ *   - the same id with another body sets CW_STATUS_DUP ("edits-not-allowed",
+ *     :166-171);
+ *   - a cause missing from the union sets CW_STATUS_ORPHAN
+ *     ("cause-must-exist", :175-178).
+ * The reference inserts ct2's nodes one at a time in hash-map order, so it can
+ * also throw :cause-must-exist when a node of ct2 precedes its own cause in
+ * that order; the union is what it returns whenever it does not throw. */
+typedef struct {
+  cw_list_batch a;          /* ct1's nodes per document (doc_offsets: host memory)   */
+  const uint64_t *a_value;  /* [Na] value token: equal tokens <=> equal values       */
+  cw_list_batch b;          /* ct2's nodes, same n_docs; key layout fields unused    */
+  const uint64_t *b_value;  /* [Nb]                                                  */
+} cw_merge_batch;
+
+typedef struct {
+  uint64_t *merged_offsets; /* HOST memory [n_docs+1]: merged doc d is
+                               [merged_offsets[d], merged_offsets[d+1])              */
+  uint32_t *merged_src;     /* [Na+Nb]: merged nodes in id order, as source indices:
+                               s < na_d is a's doc-local s, else b's doc-local s-na_d */
+  cw_list_result weave;     /* every array sized for Na+Nb (n_docs for the per-
+                               document ones), laid out by merged_offsets; weave_perm
+                               holds doc-local merged indices (into merged_src)      */
+} cw_merge_result;
+
+/* Host memory only (memspace must be CW_MEM_HOST in this version). */
+int cw_merge_lists(cw_ctx *ctx, const cw_merge_batch *batch, cw_merge_result *result,
+                   int memspace);
+
 #ifdef __cplusplus
 }
 #endif
