@@ -630,6 +630,8 @@ __global__ __launch_bounds__(NT) void k_frank(
   if (tid == 0 && bst) atomicOr(&status[d], bst);
 }
 
+constexpr uint32_t KBM_WORDS = 2 * TILE / 32;  // per tile: special bits, then hide bits
+
 // Pass 2, one block per window (window w of document d covers ranks
 // [4096 w, 4096 (w+1)), the ranks of tile w): gather the window's records from
 // every tile of the document (one contiguous run each), place them by rank in
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(NT) void k_fplace(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ tile_first, const uint32_t *__restrict__ doc_off,
     const uint64_t *__restrict__ id_key, uint32_t *__restrict__ sval, uint32_t *__restrict__ par,
-    uint8_t *__restrict__ skind, uint64_t *__restrict__ skey) {
+    uint8_t *__restrict__ skind, uint64_t *__restrict__ skey, uint32_t *__restrict__ kbm) {
   __shared__ uint32_t s_val[TILE], s_par[TILE];
   __shared__ uint8_t s_kind[TILE];
   __shared__ uint32_t s_run[65], s_src[64];
@@ -694,6 +696,19 @@ __global__ __launch_bounds__(NT) void k_fplace(
     skind[base + r0 + j] = s_kind[j];
     if (skey) skey[base + r0 + j] = id_key[base + (v < n ? v : 0u)];
   }
+  // special and hide bits of the window's ranks (KBM_WORDS per tile) for k_tree
+  for (uint32_t j0 = (tid >> 6) << 6; j0 < TILE; j0 += NT) {
+    const uint32_t j = j0 + (tid & 63);
+    const uint8_t k = j < wlen ? s_kind[j] : 0;
+    const uint64_t sm = __ballot(is_special(k)), hm = __ballot(is_hide(k));
+    if ((tid & 63) == 0) {
+      uint32_t *o = kbm + (size_t)t * KBM_WORDS + (j0 >> 5);
+      o[0] = (uint32_t)sm;
+      o[1] = (uint32_t)(sm >> 32);
+      o[TILE / 32] = (uint32_t)hm;
+      o[TILE / 32 + 1] = (uint32_t)(hm >> 32);
+    }
+  }
 }
 
 // --- tree: effective parents, sibling order, links (one workgroup per document) --
@@ -713,7 +728,8 @@ __global__ __launch_bounds__(NT) void k_tree(
     const uint32_t *__restrict__ doc_log2k, uint32_t kbits, uint32_t bm_words,
     uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ fcN, uint32_t *__restrict__ thr, uint32_t *__restrict__ link,
-    uint32_t *__restrict__ status, unsigned long long *__restrict__ tprof) {
+    uint32_t *__restrict__ status, unsigned long long *__restrict__ tprof,
+    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first) {
   constexpr uint32_t IT = TILE_T / NT;
   // diagnostic phase stamps (tprof != nullptr only under CW_TREE_PROF)
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
@@ -734,7 +750,16 @@ __global__ __launch_bounds__(NT) void k_tree(
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   const bool in_lds = ((n + 31) >> 5) <= bm_words;
   uint32_t *spec_bm = bm, *hide_bm = bm + bm_words;
-  if (in_lds) {
+  if (in_lds && kbm) {
+    // the front end wrote both bitmaps per 4096-rank tile: coalesced word loads
+    const uint32_t *src = kbm + (size_t)tile_first[d] * KBM_WORDS;
+    for (uint32_t wi = tid; wi < ((n + 31) >> 5); wi += NT) {
+      const uint32_t *tw = src + (size_t)(wi >> 7) * KBM_WORDS + (wi & 127);
+      spec_bm[wi] = tw[0];
+      hide_bm[wi] = tw[TILE / 32];
+    }
+    __syncthreads();
+  } else if (in_lds) {
     // one ballot per wave per 64 ranks: bit r of the bitmap = special(rank r);
     // eight loads in flight per lane
     constexpr uint32_t BU = 8;
@@ -1960,6 +1985,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     const bool want_yarns = out->yarn_perm && bt->site_bits;
     // 1-2 (dense ids). id order and join through per-document rank directories
     bool front_done = false;
+    uint32_t *kbm = nullptr;  // special / hide bitmaps per tile (front end -> tree)
     if (c->front && N >= (uint64_t)c->front_min_avg * D && t.nmax <= 64 * TILE) {
       const uint32_t SG = c->front_slot_groups;
       uint4 *dir = scratch_t<uint4>(c, "fr_dir", (size_t)D * SG);
@@ -1984,7 +2010,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         sval = svA;
         uint32_t *rec_meta = svB, *rec_par = (uint32_t *)skB;  // free until the yarn sort
         uint32_t *woff = scratch_t<uint32_t>(c, "fr_woff", t.Wofftot);
-        if (!woff) return fail(c, "out of device memory (window table)");
+        kbm = scratch_t<uint32_t>(c, "fr_kbm", (size_t)t.T * KBM_WORDS);
+        if (!woff || !kbm) return fail(c, "out of device memory (window table)");
         {
           Launch L(c, "frank", (double)N * (8 + 8 + 1 + 4 + 4));
           hipLaunchKernelGGL((k_frank<512>), GT, dim3(512), (size_t)std::max(gmax, 1u) * 16,
@@ -1997,7 +2024,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
           Launch L(c, "fplace", (double)N * (4 + 4 + 4 + 4 + 1 + (skey ? 16 : 0)));
           hipLaunchKernelGGL((k_fplace<512>), GT, dim3(512), 0, c->stream, rec_meta, rec_par,
                              woff, dev_tab(c, "t_woff_base"), tile_start, tile_doc,
-                             dev_tab(c, "t_tile_first"), doc_off, id_key, sval, par, skind, skey);
+                             dev_tab(c, "t_tile_first"), doc_off, id_key, sval, par, skind, skey,
+                             kbm);
         }
         if (check_launch(c, "fplace")) return -1;
         front_done = true;
@@ -2046,15 +2074,18 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       if (c->tree_cfg == 2)
         hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                           dev_tab(c, "t_tile_first"));
       else if (c->tree_cfg == 1)
         hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                           dev_tab(c, "t_tile_first"));
       else
         hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
                            (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof);
+                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                           dev_tab(c, "t_tile_first"));
     }
     if (check_launch(c, "tree")) return -1;
     if (c->tree_prof) {
