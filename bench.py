@@ -38,10 +38,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the cpu_baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2],
+                    help="BASELINE.json configs[config-1]: 2 = the headline batch "
+                         "(default), 1 = one 100k-node list (latency; replicas on N GPUs)")
     return ap.parse_args()
 
 
-def cpu_baseline(spec, budget_s):
+def cpu_baseline(spec, budget_s, max_docs=64):
     """The reference algorithm (literal weave-node fold, oracle/weave_oracle.c,
     one core) on the first documents of this same workload, until ~budget_s."""
     import oracle
@@ -49,7 +52,7 @@ def cpu_baseline(spec, budget_s):
     done_nodes, t_total, ndocs = 0, 0.0, 0
     from cause_amd import gen
 
-    while t_total < budget_s and ndocs < 64:
+    while t_total < budget_s and ndocs < max_docs:
         off, idk, ck, kd = gen.generate(spec, ndocs, ndocs + 1, nthreads=1)
         t0 = time.perf_counter()
         _, st = oracle.list_weave(idk, ck, kd, oracle.METHOD_LITERAL)
@@ -78,10 +81,17 @@ def main():
     from cause_amd import abi, gen, shard
     import dataclasses
 
-    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
+    if a.config == 1:
+        # one list; every rank weaves its own replica (the path does not shard)
+        spec, D = gen.CONFIG1, 1
+        d0, d1 = 0, 1
+        workload = "config1: one CausalList of 100,000 inserts from 4 sites, full reweave"
+    else:
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
+        D = a.docs
+        d0, d1 = shard.doc_range(rank, world, docs_per_rank=D)  # weak scaling, no data exchange
+        workload = "config2: independent CausalLists, full reweave"
     layout = spec.layout()
-    D = a.docs
-    d0, d1 = shard.doc_range(rank, world, docs_per_rank=D)  # weak scaling, no data exchange
     t0 = time.time()
     off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16)
     N = len(idk)
@@ -140,24 +150,26 @@ def main():
     # passes (scripts/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
+    if os.path.exists(pmc) and a.config == 2 and a.docs == 10_000 and a.nodes == 50_000:
         entry = json.load(open(pmc)).get(name)
         traffic = entry["bytes"] if entry else None
 
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
-            cpu = cpu_baseline(spec, a.cpu_seconds)
+            cpu = cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64)
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
             "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt_max / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
-            "config": {"workload": "config2: independent CausalLists, full reweave",
+            "config": {"workload": workload,
                        "docs_per_gpu": D, "nodes_per_doc": spec.doc_size,
                        "nodes_per_gpu": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
                        "p_show": spec.p_show, "p_conj": spec.p_conj,
-                       "key_bits": layout.key_bits, "parallelism": f"docs sharded x{world}"},
+                       "key_bits": layout.key_bits,
+                       "parallelism": (f"replicas x{world}" if a.config == 1
+                                       else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic,

@@ -20,6 +20,7 @@ HEADER = os.path.join(os.path.dirname(_HERE), "include", "causeweave.h")
 CW_MEM_HOST, CW_MEM_DEVICE = 0, 1
 STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1, 2, 4, 8, 32
 STATUS_MAP_KEY = 16
+STATUS_WEFT = 64
 
 
 class CwListBatch(C.Structure):
@@ -54,6 +55,15 @@ class CwMergeBatch(C.Structure):
 
 class CwMergeResult(C.Structure):
     _fields_ = [("merged_offsets", C.POINTER(C.c_uint64)), ("merged_src", C.c_void_p),
+                ("weave", CwListResult)]
+
+
+class CwWeftBatch(C.Structure):
+    _fields_ = [("nodes", CwListBatch), ("cut", C.POINTER(C.c_uint64))]
+
+
+class CwWeftResult(C.Structure):
+    _fields_ = [("kept_offsets", C.POINTER(C.c_uint64)), ("kept_src", C.c_void_p),
                 ("weave", CwListResult)]
 
 
@@ -104,6 +114,9 @@ def lib():
         L.cw_merge_lists.argtypes = [C.c_void_p, C.POINTER(CwMergeBatch),
                                      C.POINTER(CwMergeResult), C.c_int]
         L.cw_merge_lists.restype = C.c_int
+        L.cw_weft_lists.argtypes = [C.c_void_p, C.POINTER(CwWeftBatch), C.POINTER(CwWeftResult),
+                                    C.c_int]
+        L.cw_weft_lists.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -289,6 +302,37 @@ class Weaver:
         w = ListResult(w.weave_perm[:M], w.visible_bits[:(M + 31) // 32], w.visible_count[:D],
                        w.max_ts[:D], w.status[:D], None if w.yarn_perm is None else w.yarn_perm[:M])
         return MergeResult(mo, src[:M], w)
+
+    def weft_lists(self, offsets, id_key, cause_key, kind, layout, cut, yarns=True) -> MergeResult:
+        """Host-memory call of cw_weft_lists.  cut: uint64[D << site_bits] packed
+        cut id per (document, site rank), 0 = site not named.  Returns the kept
+        nodes (src = doc-local input index, input order) and their weave."""
+        i = np.ascontiguousarray(id_key, np.uint64)
+        c = np.ascontiguousarray(cause_key, np.uint64)
+        k = np.ascontiguousarray(kind, np.uint8)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        cut = np.ascontiguousarray(cut, np.uint64)
+        D, N = len(off) - 1, len(i)
+        if int(off[-1]) != N or len(cut) != D << layout.site_bits:
+            raise ValueError("offsets / cut sizes")
+        b, off = self._batch(off, _ptr(i), _ptr(c), _ptr(k), layout)
+        wb = CwWeftBatch(b, cut.ctypes.data_as(C.POINTER(C.c_uint64)))
+        ko = np.zeros(D + 1, np.uint64)
+        src = np.zeros(max(N, 1), np.uint32)
+        w = ListResult(np.zeros(max(N, 1), np.uint32), np.zeros((N + 31) // 32 + 1, np.uint32),
+                       np.zeros(max(D, 1), np.uint32), np.zeros(max(D, 1), np.uint64),
+                       np.zeros(max(D, 1), np.uint32),
+                       np.zeros(max(N, 1), np.uint32) if (yarns and layout.site_bits) else None)
+        r = CwWeftResult(ko.ctypes.data_as(C.POINTER(C.c_uint64)), _ptr(src),
+                         CwListResult(_ptr(w.weave_perm), _ptr(w.visible_bits),
+                                      _ptr(w.visible_count), _ptr(w.max_ts), _ptr(w.status),
+                                      _ptr(w.yarn_perm)))
+        self._check(self._L.cw_weft_lists(self._h, C.byref(wb), C.byref(r), CW_MEM_HOST),
+                    "cw_weft_lists")
+        M = int(ko[-1])
+        w = ListResult(w.weave_perm[:M], w.visible_bits[:(M + 31) // 32], w.visible_count[:D],
+                       w.max_ts[:D], w.status[:D], None if w.yarn_perm is None else w.yarn_perm[:M])
+        return MergeResult(ko, src[:M], w)
 
     def weave_maps(self, offsets, id_key, cause, cause_is_id, kind, token_bits,
                    key_bits=0) -> MapResult:

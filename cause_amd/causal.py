@@ -9,6 +9,7 @@ order equals the full reweave).  There is no CPU weave in this module.
 
     shared.cljc:151-192   insert / append           -> insert, append, insert_bulk
     shared.cljc:300-314   merge-trees               -> merge_trees / merge_lists (cw_merge_lists)
+    shared.cljc:268-293   weft                      -> weft / weft_lists (cw_weft_lists)
     shared.cljc:259-266   refresh-caches            -> refresh_caches
     list.cljc:20-34       weave (all arities)       -> list_weave / weave_lists
     list.cljc:36-43       conj- / cons-             -> list_conj / list_cons
@@ -256,6 +257,46 @@ def insert_bulk(ct, nodes):
     ct2 = dict(ct)
     ct2["nodes"] = {n[0]: (n[1], n[2]) for n in nodes}
     return merge_trees(list_weave, ct, ct2)
+
+
+def weft_lists(items):
+    """s/weft (shared.cljc:268-293) for many (ct, ids-to-cut-yarns) list pairs in
+    ONE GPU call (cw_weft_lists): time travel to the cut, then the full reweave."""
+    docs = [[(i, b[0], b[1]) for i, b in ct["nodes"].items()] for ct, _ in items]
+    pk = pack.pack_lists(docs, min_site_bits=1)  # cw_weft_lists indexes cuts by site rank
+    lay = pk.layout
+    S = 1 << lay.site_bits
+    cut = np.zeros(len(items) << lay.site_bits, np.uint64)
+    for d, ((ct, ids), pd) in enumerate(zip(items, pk.docs)):
+        for i in ids:
+            if i == ROOT_ID or i[1] not in pd.site_rank:
+                continue  # a site with no node keeps nothing (its yarn is empty)
+            cut[d * S + pd.site_rank[i[1]]] = lay.pack(i[0], pd.site_rank[i[1]], i[2])
+    res = weaver().weft_lists(pk.offsets, pk.id_key, pk.cause_key, pk.kind, lay, cut)
+    vis = res.weave.visible()
+    out = []
+    for d, ((ct, ids), nodes) in enumerate(zip(items, docs)):
+        st = int(res.weave.status[d])
+        if st:
+            raise CauseError(f"weft outside the weave's domain (status {st})", {"weave-domain"})
+        lo, hi = int(res.offsets[d]), int(res.offsets[d + 1])
+        kept = [nodes[s] for s in res.src[lo:hi]]
+        new = new_list_ct(site_id=ct["site_id"], uuid=ct["uuid"])
+        new["nodes"] = {n[0]: (n[1], n[2]) for n in kept}
+        new["weave"] = [kept[p] for p in res.weave.weave_perm[lo:hi]]
+        new["_visible"] = [bool(v) for v in vis[lo:hi]]
+        yarns = {}
+        for p in res.weave.yarn_perm[lo:hi]:
+            yarns.setdefault(kept[p][0][1], []).append(kept[p])
+        new["yarns"] = yarns
+        new["lamport_ts"] = max(i[0] for i in ids if i != ROOT_ID)
+        out.append(new)
+    return out
+
+
+def weft(ct, ids):
+    """(c/weft causal-list ids) -- list.cljc:165-166 over shared.cljc:268-293."""
+    return weft_lists([(ct, ids)])[0]
 
 
 def append(weave_fn, ct, cause, value):

@@ -1560,6 +1560,59 @@ __global__ void k_or_status(const uint32_t *__restrict__ a, uint32_t *__restrict
   if (d < D) b[d] |= a[d];
 }
 
+// Weft (s/weft, shared.cljc:268-293): keep the root and, per site, the nodes
+// up to and including the site's cut id; count pass, then write pass at koff.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_weft_select(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
+    const uint64_t *__restrict__ cut, uint32_t site_shift, uint32_t site_bits, int pass,
+    uint32_t *__restrict__ kcount, const uint32_t *__restrict__ koff, uint64_t *__restrict__ kid,
+    uint64_t *__restrict__ kcause, uint8_t *__restrict__ kkind, uint32_t *__restrict__ ksrc,
+    uint32_t *__restrict__ kstatus) {
+  __shared__ uint32_t wtot[NT / 64];
+  __shared__ uint32_t found[1024 / 32];
+  const uint32_t d = blockIdx.x, base = doc_off[d], n = doc_off[d + 1] - base;
+  const uint32_t S = 1u << site_bits, smask = S - 1;
+  const uint64_t *dc = cut + ((size_t)d << site_bits);
+  for (uint32_t i = threadIdx.x; i < 32; i += NT) found[i] = 0;
+  __syncthreads();
+  uint32_t run = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += NT) {
+    const uint32_t i = i0 + threadIdx.x;
+    bool keep = false;
+    uint64_t k = 0;
+    if (i < n) {
+      k = id_key[base + i];
+      const uint32_t site = (uint32_t)(k >> site_shift) & smask;
+      const uint64_t c = dc[site];
+      keep = (kind[base + i] & KIND_ROOT) || (c != 0 && k <= c);
+      if (pass == 0 && c != 0 && k == c) atomicOr(&found[site >> 5], 1u << (site & 31));
+    }
+    uint32_t tot;
+    const uint32_t pos = run + block_exscan<NT>(keep ? 1u : 0u, wtot, &tot);
+    if (pass == 1 && keep) {
+      const uint32_t o = koff[d] + pos;
+      kid[o] = k;
+      kcause[o] = cause_key[base + i];
+      kkind[o] = kind[base + i];
+      ksrc[o] = i;
+    }
+    run += tot;
+  }
+  if (pass == 0) {
+    __syncthreads();
+    bool missing = false;
+    for (uint32_t s = threadIdx.x; s < S; s += NT)
+      missing |= dc[s] != 0 && !((found[s >> 5] >> (s & 31)) & 1u);
+    missing = __syncthreads_or(missing);
+    if (threadIdx.x == 0) {
+      kcount[d] = run;
+      kstatus[d] = missing ? (uint32_t)CW_STATUS_WEFT : 0u;
+    }
+  }
+}
+
 // ============================================================================
 // Host side
 // ============================================================================
@@ -2583,6 +2636,102 @@ int merge_lists_impl(cw_ctx *c, const cw_merge_batch *bt, cw_merge_result *res, 
   return 0;
 }
 
+int weft_lists_impl(cw_ctx *c, const cw_weft_batch *bt, cw_weft_result *res, int memspace) {
+  if (!bt || !res) return fail(c, "null batch/result");
+  if (memspace != CW_MEM_HOST) return fail(c, "cw_weft_lists: only CW_MEM_HOST is supported");
+  const cw_list_batch &L = bt->nodes;
+  const uint64_t D = L.n_docs;
+  const uint64_t *off = L.doc_offsets;
+  if (!off || off[0] != 0) return fail(c, "doc_offsets must start at 0");
+  if (L.site_bits == 0 || L.site_bits > 10) return fail(c, "weft needs site_bits in 1..10");
+  if (!bt->cut) return fail(c, "cut is required");
+  const uint64_t N = off[D];
+  if (N >= 0xFFFFFFFFull) return fail(c, "batch too large");
+  cw_list_result &W = res->weave;
+  if (!res->kept_offsets || !res->kept_src || !W.weave_perm || !W.visible_count || !W.status)
+    return fail(c, "kept_offsets, kept_src, weave_perm, visible_count and status are required");
+  std::vector<uint32_t> h_off(D + 1);
+  for (uint64_t d = 0; d <= D; d++) {
+    if (d < D && off[d + 1] < off[d]) return fail(c, "doc_offsets not monotone");
+    h_off[d] = (uint32_t)off[d];
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t Ns = std::max<uint64_t>(N, 1), NC = (size_t)D << L.site_bits;
+  uint64_t *id = scratch_t<uint64_t>(c, "w_id", Ns), *ca = scratch_t<uint64_t>(c, "w_ca", Ns);
+  uint8_t *kd = scratch_t<uint8_t>(c, "w_kd", Ns);
+  uint64_t *cut = scratch_t<uint64_t>(c, "w_cut", std::max<size_t>(NC, 1));
+  uint32_t *doff = scratch_t<uint32_t>(c, "w_off", D + 1), *koff = scratch_t<uint32_t>(c, "w_koff", D + 1);
+  uint32_t *kcnt = scratch_t<uint32_t>(c, "w_kcnt", D + 1), *kst = scratch_t<uint32_t>(c, "w_kst", D + 1);
+  uint64_t *kid = scratch_t<uint64_t>(c, "w_kid", Ns), *kca = scratch_t<uint64_t>(c, "w_kca", Ns);
+  uint8_t *kkd = scratch_t<uint8_t>(c, "w_kkd", Ns);
+  uint32_t *ksrc = scratch_t<uint32_t>(c, "w_ksrc", Ns);
+  if (!id || !ca || !kd || !cut || !doff || !koff || !kcnt || !kst || !kid || !kca || !kkd || !ksrc)
+    return fail(c, "out of device memory (weft)");
+  if (!grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (N) {
+    if (!L.id_key || !L.cause_key || !L.kind) return fail(c, "null input arrays");
+    HIPCHK(c, hipMemcpy(id, L.id_key, N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(ca, L.cause_key, N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(kd, L.kind, N, hipMemcpyHostToDevice));
+  }
+  if (NC) HIPCHK(c, hipMemcpy(cut, bt->cut, NC * 8, hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpy(doff, h_off.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  uint64_t *ko = res->kept_offsets;
+  ko[0] = 0;
+  if (D == 0) return 0;
+  hipLaunchKernelGGL((k_weft_select<1024>), dim3((uint32_t)D), dim3(1024), 0, c->stream, id, ca, kd,
+                     doff, cut, L.site_shift, L.site_bits, 0, kcnt, koff, kid, kca, kkd, ksrc, kst);
+  if (check_launch(c, "weft_count")) return -1;
+  std::vector<uint32_t> h_cnt(D), h_ko(D + 1);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(h_cnt.data(), kcnt, D * 4, hipMemcpyDeviceToHost));
+  for (uint64_t d = 0; d < D; d++) {
+    ko[d + 1] = ko[d] + h_cnt[d];
+    h_ko[d] = (uint32_t)ko[d];
+  }
+  h_ko[D] = (uint32_t)ko[D];
+  HIPCHK(c, hipMemcpy(koff, h_ko.data(), (D + 1) * 4, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL((k_weft_select<1024>), dim3((uint32_t)D), dim3(1024), 0, c->stream, id, ca, kd,
+                     doff, cut, L.site_shift, L.site_bits, 1, kcnt, koff, kid, kca, kkd, ksrc, kst);
+  if (check_launch(c, "weft_write")) return -1;
+  const uint64_t NK = ko[D];
+  if (ensure_tables(c, D, ko)) return -1;
+  cw_list_batch lb = L;
+  lb.doc_offsets = ko;
+  const size_t NKs = std::max<uint64_t>(NK, 1);
+  cw_list_result lr{};
+  lr.weave_perm = scratch_t<uint32_t>(c, "w_perm", NKs);
+  lr.visible_bits = W.visible_bits ? scratch_t<uint32_t>(c, "w_bits", (NKs + 31) / 32) : nullptr;
+  lr.visible_count = scratch_t<uint32_t>(c, "w_vc", D + 1);
+  lr.max_ts = W.max_ts ? scratch_t<uint64_t>(c, "w_mts", D + 1) : nullptr;
+  lr.status = scratch_t<uint32_t>(c, "w_st", D + 1);
+  lr.yarn_perm = W.yarn_perm ? scratch_t<uint32_t>(c, "w_yarn", NKs) : nullptr;
+  if (!lr.weave_perm || !lr.visible_count || !lr.status || (W.visible_bits && !lr.visible_bits) ||
+      (W.max_ts && !lr.max_ts) || (W.yarn_perm && !lr.yarn_perm))
+    return fail(c, "out of device memory (weft outputs)");
+  if (weave_lists_device(c, &lb, kid, kca, kkd, &lr)) return -1;
+  hipLaunchKernelGGL(k_or_status, dim3((uint32_t)((D + 255) / 256)), dim3(256), 0, c->stream, kst,
+                     lr.status, (uint32_t)D);
+  if (check_launch(c, "or_status")) return -1;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (NK) {
+    HIPCHK(c, hipMemcpy(res->kept_src, ksrc, NK * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(W.weave_perm, lr.weave_perm, NK * 4, hipMemcpyDeviceToHost));
+    if (W.visible_bits)
+      HIPCHK(c, hipMemcpy(W.visible_bits, lr.visible_bits, (NK + 31) / 32 * 4, hipMemcpyDeviceToHost));
+    if (W.yarn_perm) HIPCHK(c, hipMemcpy(W.yarn_perm, lr.yarn_perm, NK * 4, hipMemcpyDeviceToHost));
+  }
+  HIPCHK(c, hipMemcpy(W.visible_count, lr.visible_count, D * 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(W.status, lr.status, D * 4, hipMemcpyDeviceToHost));
+  if (W.max_ts) HIPCHK(c, hipMemcpy(W.max_ts, lr.max_ts, D * 8, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipDeviceSynchronize());
+  for (uint64_t d = 0; d < D; d++)
+    if (ko[d + 1] == ko[d]) W.status[d] |= CW_STATUS_ROOT;
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -2697,6 +2846,12 @@ int cw_merge_lists(cw_ctx *c, const cw_merge_batch *b, cw_merge_result *r, int m
   if (!c) return -1;
   c->err.clear();
   return merge_lists_impl(c, b, r, memspace);
+}
+
+int cw_weft_lists(cw_ctx *c, const cw_weft_batch *b, cw_weft_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  return weft_lists_impl(c, b, r, memspace);
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

@@ -158,10 +158,12 @@ class PackedBatch:
     docs: list             # PackedDoc per document
 
 
-def pack_lists(docs) -> PackedBatch:
+def pack_lists(docs, min_site_bits: int = 0) -> PackedBatch:
     """Pack a batch of list documents (each an iterable of nodes incl. root)."""
     docs = [list(d) for d in docs]
     lay = layout_for(docs)
+    if lay.site_bits < min_site_bits:
+        lay = KeyLayout(lay.ts_bits, min_site_bits, lay.tx_bits)
     packed = [pack_doc(d, lay) for d in docs]
     off = np.zeros(len(docs) + 1, np.uint64)
     off[1:] = np.cumsum([len(d) for d in docs], dtype=np.uint64)

@@ -64,7 +64,8 @@ enum {
   CW_STATUS_NON_LAMPORT = 1u << 3, /* a cause id is not older than its node                */
   CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits, or a node caused by
                                       the root id (its key weave mixes children and orphans) */
-  CW_STATUS_INTERNAL = 1u << 5     /* consistency check failed inside the pipeline         */
+  CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
+  CW_STATUS_WEFT = 1u << 6         /* weft: a cut id is not a node of the document         */
 };
 
 /* Where the arrays of a batch/result live. */
@@ -208,6 +209,31 @@ typedef struct {
 /* Host memory only (memspace must be CW_MEM_HOST in this version). */
 int cw_merge_lists(cw_ctx *ctx, const cw_merge_batch *batch, cw_merge_result *result,
                    int memspace);
+
+/* ----------------------------------------------------------------- weft ---- */
+/* s/weft (shared.cljc:268-293), time travel: per document, each named site's
+ * yarn up to and including its cut id, the root, nothing of the other sites,
+ * then the full reweave.  cut[(d << site_bits) | site_rank] is the packed cut
+ * id of that site, or 0 for a site that is not named (its nodes are dropped).
+ * A cut id that is not a node of the document sets CW_STATUS_WEFT (the
+ * reference then weaves a [id nil nil] node).  Cuts that do not preserve
+ * causality leave orphans: CW_STATUS_ORPHAN (the reference's "gibberish
+ * trees").  ::lamport-ts of the result is the largest cut ts (max_ts). */
+typedef struct {
+  cw_list_batch nodes;   /* site_bits must be 1..10                           */
+  const uint64_t *cut;   /* HOST memory [n_docs << site_bits]                */
+} cw_weft_batch;
+
+typedef struct {
+  uint64_t *kept_offsets; /* HOST memory [n_docs+1]                          */
+  uint32_t *kept_src;     /* [N]: doc-local input index of each kept node, in
+                             input order                                      */
+  cw_list_result weave;   /* laid out by kept_offsets; weave_perm holds indices
+                             into kept_src                                     */
+} cw_weft_result;
+
+/* Host memory only (memspace must be CW_MEM_HOST in this version). */
+int cw_weft_lists(cw_ctx *ctx, const cw_weft_batch *batch, cw_weft_result *result, int memspace);
 
 #ifdef __cplusplus
 }

@@ -226,6 +226,35 @@ def refresh_caches(weave_fn, ct):
     return weave_fn(refresh_ts(spin(base)))
 
 
+def yarns_to_nodes(ct):
+    """shared.cljc:251-257"""
+    out = dict(ct)
+    out["nodes"] = {n[0]: (n[1], n[2]) for y in ct["yarns"].values() for n in y}
+    return out
+
+
+def weft(weave_fn, new_ct_fn, ct, ids):
+    """shared.cljc:268-293: each named site's yarn up to and including its cut
+    id (``(new-node [id (get nodes id)])``: a missing id becomes [id nil nil]),
+    then yarns->nodes and the full reweave."""
+    filtered = [i for i in ids if i != ROOT_ID]
+    new = new_ct_fn()
+    yarns = dict(new["yarns"])
+    for i in filtered:
+        pre = []
+        for n in ct["yarns"].get(i[1], []):
+            if n[0] == i:
+                break
+            pre.append(n)
+        body = ct["nodes"].get(i)
+        pre.append((i, body[0], body[1]) if body is not None else (i, None, None))
+        yarns[i[1]] = pre
+    new["yarns"] = yarns
+    new["site_id"] = ct["site_id"]
+    new["lamport_ts"] = max(i[0] for i in filtered)
+    return weave_fn(yarns_to_nodes(new))
+
+
 class CauseError(Exception):
     def __init__(self, msg, causes):
         super().__init__(msg)

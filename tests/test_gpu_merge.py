@@ -196,3 +196,71 @@ def test_mirror_insert_bulk_matches_refresh():
     full = _ct(nodes, like=ct)
     assert bulk["weave"] == full["weave"]
     assert bulk["lamport_ts"] == max(n[0][0] for n in nodes)
+
+
+# -------------------------------------------------------------------- weft ----
+def _weft_ref(ct, ids):
+    nct = lambda: R.new_list_ct(site_id=ct["site_id"], uuid=ct["uuid"])
+    return R.weft(R.list_weave, nct, ct, ids)
+
+
+def _ref_ct(nodes, rng):
+    ct = R.new_list_ct(rng=rng)
+    ct["nodes"] = {n[0]: (n[1], n[2]) for n in [R.ROOT_NODE] + nodes}
+    return R.refresh_caches(R.list_weave, ct)
+
+
+def test_weft_matches_reference_restatement():
+    """shared.cljc:268-293: cut every site's yarn at a random node (or drop the
+    site), keep causally closed cuts, weave; compare with the restatement."""
+    rng = random.Random(21)
+    checked = 0
+    for steps in (5, 20, 60, 150):
+        for _ in range(25):
+            nodes, _ = G.random_history(rng, steps)
+            ref = _ref_ct(nodes, rng)
+            sites = sorted({n[0][1] for n in nodes})
+            ids = []
+            T = rng.randint(1, max(n[0][0] for n in nodes))
+            for s in sites:
+                if rng.random() < 0.25:
+                    ids.append(rng.choice(ref["yarns"][s])[0])  # arbitrary cut
+                elif rng.random() < 0.9:  # consistent cut: the site's state at time T
+                    older = [n for n in ref["yarns"][s] if n[0][0] <= T]
+                    if older:
+                        ids.append(older[-1][0])
+            if not ids:
+                continue
+            want = _weft_ref(ref, ids)
+            kept = set(want["nodes"])
+            if any(b[0] is not None and b[0] not in kept for b in want["nodes"].values()):
+                continue  # not causally closed: the reference weaves gibberish
+            ct = causal.new_list_ct(site_id=ref["site_id"], uuid=ref["uuid"])
+            ct["nodes"] = dict(ref["nodes"])
+            got = causal.weft(ct, ids)
+            assert got["weave"] == want["weave"]
+            assert causal.causal_list_to_edn(got) == R.causal_list_to_edn(want)
+            assert got["lamport_ts"] == want["lamport_ts"]
+            checked += 1
+    assert checked > 20
+
+
+def test_weft_status_bits(weaver):
+    """A cut id that is not a node: CW_STATUS_WEFT; a cut that drops a cause:
+    CW_STATUS_ORPHAN."""
+    s1, s2 = "aaaaaaaaaaaaa", "bbbbbbbbbbbbb"
+    a1 = ((1, s1, 0), R.ROOT_ID, "x")
+    b2 = ((2, s2, 0), (1, s1, 0), "y")
+    doc = [R.ROOT_NODE, a1, b2]
+    b = pack.pack_lists([doc, doc, doc], min_site_bits=1)
+    lay, S = b.layout, 1 << b.layout.site_bits
+    rk = b.docs[0].site_rank
+    cut = np.zeros(3 * S, np.uint64)
+    cut[0 * S + rk[s1]] = lay.pack(1, rk[s1], 0)          # s1 only: fine
+    cut[1 * S + rk[s1]] = lay.pack(5, rk[s1], 0)          # no node with that id
+    cut[2 * S + rk[s2]] = lay.pack(2, rk[s2], 0)          # b2 without its cause
+    res = weaver.weft_lists(b.offsets, b.id_key, b.cause_key, b.kind, lay, cut)
+    st = res.weave.status
+    assert st[0] == 0 and list(np.diff(res.offsets)) == [2, 2, 2]
+    assert st[1] & abi.STATUS_WEFT
+    assert st[2] & abi.STATUS_ORPHAN
