@@ -557,8 +557,10 @@ __global__ __launch_bounds__(NT) void k_frank(
     const uint32_t *__restrict__ dgroups, uint32_t *__restrict__ rec_meta,
     uint32_t *__restrict__ rec_par, uint32_t *__restrict__ woff, uint32_t *__restrict__ status) {
   constexpr uint32_t IT = TILE / NT;
+  // the directory, then (once every node is ranked) the tile's records: the
+  // dynamic LDS is max(directory, 2 * TILE words) so 4 blocks fit on a CU
   extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
-  __shared__ uint32_t st_meta[TILE], st_par[TILE];
+  uint32_t *st_meta = reinterpret_cast<uint32_t *>(sdir), *st_par = st_meta + TILE;
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
   __shared__ uint32_t run[64];
   __shared__ uint32_t bst;
@@ -568,9 +570,7 @@ __global__ __launch_bounds__(NT) void k_frank(
   const uint32_t G = dgroups[d];
   const uint64_t kmin = dkmin[d], xend = (uint64_t)G * FR_GROUP_BITS;
   const uint4 *src = dir + (size_t)d * slot_groups;
-  for (uint32_t g = tid; g < G; g += NT) sdir[g] = src[g];
-  if (tid == 0) bst = 0;
-  __syncthreads();
+  // the tile's nodes are loaded while the directory is staged
   const uint32_t s = tile_start[t], len = tile_start[t + 1] - s;
   uint64_t k[IT], c[IT];
   uint8_t kd[IT];
@@ -581,6 +581,9 @@ __global__ __launch_bounds__(NT) void k_frank(
     c[u] = j < len ? cause_key[s + j] : 0;
     kd[u] = j < len ? kind[s + j] : 0;
   }
+  for (uint32_t g = tid; g < G; g += NT) sdir[g] = src[g];
+  if (tid == 0) bst = 0;
+  __syncthreads();
   uint32_t st = 0, meta[IT], pr[IT], sd[IT], pos[IT];
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
@@ -607,11 +610,12 @@ __global__ __launch_bounds__(NT) void k_frank(
     sd[u] = min(r >> 12, nwin - 1);  // duplicates can push ranks past the end
   }
   if (wbits) {
-    rank_subdigit<NT, IT>(sd, len, wbits, pos, wcnt, run);
+    rank_subdigit<NT, IT>(sd, len, wbits, pos, wcnt, run);  // barriers: the directory is free
   } else {
 #pragma unroll
     for (uint32_t u = 0; u < IT; u++) pos[u] = wb_elem<IT>(u);
     if (tid == 0) run[0] = 0;
+    __syncthreads();
   }
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++)
@@ -2067,7 +2071,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         if (!woff || !kbm) return fail(c, "out of device memory (window table)");
         {
           Launch L(c, "frank", (double)N * (8 + 8 + 1 + 4 + 4));
-          hipLaunchKernelGGL((k_frank<512>), GT, dim3(512), (size_t)std::max(gmax, 1u) * 16,
+          hipLaunchKernelGGL((k_frank<512>), GT, dim3(512),
+                             std::max<size_t>((size_t)gmax * 16, 2 * TILE * 4),
                              c->stream, id_key, cause_key, kind, tile_start, tile_doc,
                              dev_tab(c, "t_tile_first"), doc_off, dev_tab(c, "t_woff_base"), dir,
                              SG, dkmin, dgroups, rec_meta, rec_par, woff, out->status);
