@@ -1617,6 +1617,114 @@ __global__ __launch_bounds__(NT) void k_weft_select(
   }
 }
 
+// --- tiny documents: one wave weaves one document of <= 64 nodes -----------------
+// The same exact weave (F5 preorder) as the list pipeline, for the
+// key weaves of maps (config 4: a few nodes per key) where the per-document
+// kernels of the pipeline would dominate: every step is a wave-wide loop over
+// the document's lanes.  Outputs the doc-local weave order and the status bits.
+constexpr uint32_t SMALL_MAX = 64;
+
+__global__ __launch_bounds__(256) void k_small_weave(
+    const uint64_t *__restrict__ doc_off, uint32_t D, const uint64_t *__restrict__ id_key,
+    const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
+    uint32_t *__restrict__ weave_perm, uint32_t *__restrict__ status) {
+  __shared__ uint32_t inv_s[4][SMALL_MAX];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t d = blockIdx.x * 4 + wv;
+  if (d >= D) return;  // uniform per wave
+  const uint64_t b = doc_off[d];
+  const uint32_t m = (uint32_t)(doc_off[d + 1] - b);
+  uint32_t *inv = inv_s[wv];
+  if (m == 0) {
+    if (lane == 0) status[d] = CW_STATUS_ROOT;
+    return;
+  }
+  const bool v = lane < m;
+  uint64_t id = v ? id_key[b + lane] : ~0ull, ca = v ? cause_key[b + lane] : 0;
+  uint32_t kd = v ? kind[b + lane] : 0u;
+  // 1. rank by id (count of smaller ids); a repeated id is a duplicate
+  uint32_t r = 0;
+  bool dup = false;
+  for (uint32_t j = 0; j < m; j++) {
+    const uint64_t o = __shfl(id, (int)j, 64);
+    r += o < id ? 1u : 0u;
+    dup |= (o == id) && j != lane;
+  }
+  const bool anydup = __ballot(dup) != 0;
+  if (v) inv[r] = lane;  // lane r takes the node of rank r
+  __builtin_amdgcn_wave_barrier();
+  // duplicate ids leave ranks unfilled: any permutation (the document is flagged)
+  const uint32_t src = v ? (anydup ? lane : inv[lane]) : 0u;
+  __builtin_amdgcn_wave_barrier();
+  id = __shfl(id, (int)src, 64);
+  ca = __shfl(ca, (int)src, 64);
+  kd = (uint32_t)__shfl((int)kd, (int)src, 64);
+  uint32_t st = dup ? (uint32_t)CW_STATUS_DUP : 0u;
+  // 2. domain checks and the cause rank (binary search over the sorted ids)
+  uint32_t par = 0;
+  if (v) {
+    if (lane == 0) {
+      if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
+    } else {
+      if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
+    }
+  }
+  uint32_t lo = 0, hi = m;  // lower bound of ca among ids[0..m)
+  for (uint32_t step = 0; step < 7; step++) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const uint64_t x = __shfl(id, (int)min(mid, 63u), 64);
+    if (lo < hi) {
+      if (x < ca) lo = mid + 1; else hi = mid;
+    }
+  }
+  const uint64_t at = __shfl(id, (int)min(lo, 63u), 64);
+  if (v && lane > 0) {
+    if (lo >= m || at != ca) st |= CW_STATUS_ORPHAN;
+    else if (lo >= lane) st |= CW_STATUS_NON_LAMPORT;
+    else par = lo;
+  }
+  // 3. effective parent: a non-special climbs through special causes
+  const bool sp = v && is_special((uint8_t)kd);
+  uint32_t e = par;
+  {
+    bool climb = v && lane > 0 && !sp;
+    for (uint32_t it = 0; it < m; it++) {
+      const uint32_t spe = (uint32_t)__shfl((int)(sp ? 1 : 0), (int)e, 64);
+      const uint32_t pe = (uint32_t)__shfl((int)par, (int)e, 64);
+      const bool go = climb && e != 0 && spe;
+      if (!__ballot(go)) break;
+      if (go) e = pe;
+    }
+  }
+  // 4. subtree sizes, children before parents (ranks descend)
+  uint32_t size = v ? 1u : 0u;
+  for (int c = (int)m - 1; c >= 1; c--) {
+    const uint32_t sc = (uint32_t)__shfl((int)size, c, 64), pc = (uint32_t)__shfl((int)e, c, 64);
+    if (lane == pc && (uint32_t)c != lane) size += sc;
+  }
+  // 5. siblings before me: specials first, each class by descending id
+  uint32_t before = 0;
+  for (uint32_t s = 1; s < m; s++) {
+    const uint32_t es = (uint32_t)__shfl((int)e, (int)s, 64), zs = (uint32_t)__shfl((int)size, (int)s, 64);
+    const bool ss = __shfl((int)(sp ? 1 : 0), (int)s, 64) != 0;
+    if (es == e && s != lane && lane > 0) {
+      if ((ss && !sp) || (ss == sp && s > lane)) before += zs;
+    }
+  }
+  // 6. preorder positions, parents first
+  uint32_t pos = 0;
+  for (uint32_t t = 1; t < m; t++) {
+    const uint32_t pp = (uint32_t)__shfl((int)pos, (int)e, 64);
+    if (lane == t) pos = pp + 1 + before;
+  }
+  if (v && pos < m) weave_perm[b + pos] = src;
+  // status: one word per document
+  uint32_t all = st;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) all |= (uint32_t)__shfl_xor((int)all, o, 64);
+  if (lane == 0) status[d] = all;
+}
+
 // ============================================================================
 // Host side
 // ============================================================================
@@ -1671,6 +1779,7 @@ struct cw_ctx {
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
+  uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
 };
 
 namespace {
@@ -2449,8 +2558,17 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   HIPCHK(c, hipMemcpy(seg_off, loff, (S + 1) * 8, hipMemcpyHostToDevice));
 
   // 4. every key weave is a list weave -- (s/weave-node key-weave ...), map.cljc:40-41
+  uint64_t max_len = 0;
+  for (uint64_t sg = 0; sg < S; sg++) max_len = std::max<uint64_t>(max_len, loff[sg + 1] - loff[sg]);
+  if (c->map_small && max_len <= SMALL_MAX) {
+    // key weaves are tiny (config 4: a few nodes per key): one wave each
+    Launch L(c, "m_small", (double)NL * (8 + 8 + 1 + 4) + (double)S * 12);
+    hipLaunchKernelGGL(k_small_weave, dim3((uint32_t)((S + 3) / 4)), dim3(256), 0, c->stream,
+                       seg_off, (uint32_t)S, lid, lcause, lkind, lperm, lst);
+  }
+  if (check_launch(c, "m_small")) return -1;
   std::vector<uint64_t> rel;
-  for (uint64_t s0 = 0; s0 < S;) {
+  for (uint64_t s0 = (c->map_small && max_len <= SMALL_MAX) ? S : 0; s0 < S;) {
     uint64_t s1 = s0 + 1;
     while (s1 < S && s1 - s0 < MAP_CHUNK_DOCS && loff[s1 + 1] - loff[s0] <= MAP_CHUNK_NODES) s1++;
     rel.resize(s1 - s0 + 1);
@@ -2775,6 +2893,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
+  c->map_small = knob("CW_MAP_SMALL", 1);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

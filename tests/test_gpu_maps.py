@@ -23,9 +23,21 @@ ID_KEY = 1 << 63
 NIL = (1 << 64) - 1
 
 
-@pytest.fixture(scope="module")
-def weaver():
-    w = abi.Weaver(0)
+@pytest.fixture(scope="module", params=["small", "pipeline"])
+def weaver(request):
+    """Both ways of weaving key weaves: one wave per tiny key weave
+    (k_small_weave) and the full list pipeline (CW_MAP_SMALL=0)."""
+    import os
+
+    old = os.environ.get("CW_MAP_SMALL")
+    os.environ["CW_MAP_SMALL"] = "1" if request.param == "small" else "0"
+    try:
+        w = abi.Weaver(0)
+    finally:
+        if old is None:
+            os.environ.pop("CW_MAP_SMALL", None)
+        else:
+            os.environ["CW_MAP_SMALL"] = old
     yield w
     w.close()
 
