@@ -38,9 +38,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the cpu_baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2],
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
                     help="BASELINE.json configs[config-1]: 2 = the headline batch "
-                         "(default), 1 = one 100k-node list (latency; replicas on N GPUs)")
+                         "(default), 1 = one 100k-node list (latency; replicas on N GPUs), "
+                         "4 = CausalMap collections (10^6 x 100 nodes per GPU)")
+    ap.add_argument("--colls", type=int, default=1_000_000, help="--config 4: collections per GPU")
     return ap.parse_args()
 
 
@@ -65,6 +67,108 @@ def cpu_baseline(spec, budget_s, max_docs=64):
                       f"in C, {t_total:.1f} s"}
 
 
+def cpu_baseline_maps(spec, budget_s):
+    """The literal c.map/weave fold (oracle/weave_oracle.c or_map_fold_literal,
+    map.cljc:21-59) on one core, collection by collection, until ~budget_s."""
+    import oracle
+    from cause_amd import gen
+
+    done, t_total, colls = 0, 0.0, 0
+    tok = np.uint64(1 << 63)
+    while t_total < budget_s and colls < 200_000:
+        off, idk, ck, ci, kd = gen.generate_maps(spec, colls, colls + 1000, nthreads=1)
+        c = np.where(ci == 1, ck, ck | tok)
+        t0 = time.perf_counter()
+        for d in range(1000):
+            a, b = int(off[d]), int(off[d + 1])
+            oracle.map_weave(idk[a:b], c[a:b], ci[a:b], kd[a:b], 0)
+        t_total += time.perf_counter() - t0
+        done += len(idk)
+        colls += 1000
+    return {"value": done / t_total, "unit": "nodes/s", "cores": 1, "kind": "port",
+            "sample": f"{colls} collections x {spec.nodes_per_coll} nodes of the same workload, "
+                      f"literal map weave + active-node (map.cljc:21-59) in C, {t_total:.1f} s"}
+
+
+def main_maps(a, world, rank, local, dist, torch, dev):
+    """--config 4: a batch of CausalMaps per GPU through cw_weave_maps (device memory)."""
+    from cause_amd import abi, gen, shard
+
+    spec = gen.CONFIG4
+    lay, tb = spec.layout()
+    d0, d1 = shard.doc_range(rank, world, docs_per_rank=a.colls)
+    t0 = time.time()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, d0, d1, nthreads=16)
+    t_gen = time.time() - t0
+    N, D = len(idk), d1 - d0
+    g = [torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+         for x in (idk, ck, ci, kd)]
+    cap = N
+    o = {"seg_offsets": torch.empty(cap + 1, dtype=torch.int64, device=dev),
+         "seg_coll": torch.empty(cap, dtype=torch.int32, device=dev),
+         "seg_key": torch.empty(cap, dtype=torch.int64, device=dev),
+         "seg_active": torch.empty(cap, dtype=torch.int64, device=dev),
+         "seg_perm": torch.empty(N + cap, dtype=torch.int32, device=dev),
+         "status": torch.empty(D, dtype=torch.int32, device=dev)}
+    ptrs = [x.data_ptr() for x in g]
+    outs = {k: v.data_ptr() for k, v in o.items()}
+    torch.cuda.synchronize()
+    w = abi.Weaver(local)
+    w.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        return w.weave_maps_device(off, ptrs, tb, lay.key_bits, outs, cap)
+
+    for _ in range(a.warmup):
+        S = step()
+    torch.cuda.synchronize()
+    if int(o["status"].max().item()) != 0:
+        raise SystemExit(f"rank {rank}: collections out of domain")
+    w.reset_kernel_stats()
+    w.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    w.set_profiling(False)
+    stats = w.kernel_stats()
+    dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
+    value = N * world * a.steps / dt_max
+    name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
+    achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    if rank == 0:
+        cpu = cpu_baseline_maps(spec, a.cpu_seconds) if (world == 1 and not a.no_cpu) else None
+        line = {
+            "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
+            "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt_max / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": "config4: CausalMap collections, key weaves + active-node",
+                       "colls_per_gpu": D, "nodes_per_coll": spec.nodes_per_coll,
+                       "nodes_per_gpu": N, "key_weaves_per_gpu": S, "keys": spec.n_keys,
+                       "zipf_s": spec.zipf_s, "parallelism": f"collections sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "launches_per_step": launches / a.steps,
+                         "kernel_ms_per_step": ms / a.steps},
+            "cpu_baseline": cpu,
+            "kernels_ms_per_step": {k: round(v[1] / a.steps, 4) for k, v in
+                                    sorted(stats.items(), key=lambda kv: -kv[1][1])},
+            "kernel_sum_ms_per_step": sum(v[1] for v in stats.values()) / a.steps,
+            "gen_s": t_gen,
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        print(json.dumps(line), flush=True)
+    w.close()
+
+
 def main():
     a = parse()
     import torch
@@ -77,6 +181,12 @@ def main():
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+
+    if a.config == 4:
+        main_maps(a, world, rank, local, dist, torch, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from cause_amd import abi, gen, shard
     import dataclasses

@@ -334,6 +334,24 @@ class Weaver:
                        w.max_ts[:D], w.status[:D], None if w.yarn_perm is None else w.yarn_perm[:M])
         return MergeResult(ko, src[:M], w)
 
+    def weave_maps_device(self, offsets, ptrs, token_bits, key_bits, out_ptrs, cap_segs) -> int:
+        """Device-memory call of cw_weave_maps: ptrs = (id_key, cause, cause_is_id,
+        kind) device pointers; out_ptrs: seg_offsets, seg_coll, seg_key,
+        seg_active, seg_perm, status device pointers.  Returns n_segs."""
+        off = np.ascontiguousarray(offsets, np.uint64)
+        b = CwMapBatch()
+        b.n_colls = len(off) - 1
+        b.coll_offsets = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        b.id_key, b.cause, b.cause_is_id, b.kind = (C.c_void_p(p) for p in ptrs)
+        b.key_bits = key_bits
+        b.token_bits = token_bits
+        g = lambda n: C.c_void_p(out_ptrs[n])
+        r = CwMapResult(cap_segs, 0, g("seg_offsets"), g("seg_coll"), g("seg_key"),
+                        g("seg_active"), g("seg_perm"), g("status"))
+        self._check(self._L.cw_weave_maps(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
+                    "cw_weave_maps")
+        return int(r.n_segs)
+
     def weave_maps(self, offsets, id_key, cause, cause_is_id, kind, token_bits,
                    key_bits=0) -> MapResult:
         """Host-memory call of cw_weave_maps."""

@@ -1725,6 +1725,56 @@ __global__ __launch_bounds__(256) void k_small_weave(
   if (lane == 0) status[d] = all;
 }
 
+// --- device exclusive scan of u32 counts (map key-weave numbering) ---------------
+// chunk sums (1024 per block) -> one block scans the sums -> chunks add their base
+__global__ __launch_bounds__(1024) void k_scan_chunks(const uint32_t *__restrict__ in, uint32_t n,
+                                                      uint32_t *__restrict__ out,
+                                                      uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wtot[16];
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t v = i < n ? in[i] : 0u;
+  uint32_t tot;
+  const uint32_t ex = block_exscan<1024>(v, wtot, &tot);
+  if (i < n) out[i] = ex;
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_sums(uint32_t *__restrict__ sums, uint32_t nb,
+                                                    uint32_t *__restrict__ total) {
+  __shared__ uint32_t wtot[16];
+  uint32_t run = 0;
+  for (uint32_t b0 = 0; b0 < nb; b0 += 1024) {
+    const uint32_t i = b0 + threadIdx.x;
+    const uint32_t v = i < nb ? sums[i] : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_exscan<1024>(v, wtot, &tot);
+    if (i < nb) sums[i] = run + ex;
+    run += tot;
+  }
+  if (threadIdx.x == 0) *total = run;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_add(uint32_t *__restrict__ out, uint32_t n,
+                                                   const uint32_t *__restrict__ sums) {
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  if (i < n) out[i] += sums[blockIdx.x];
+}
+
+// Key weave s is list document [seg_start[s] + s, seg_start[s+1] + s + 1): its
+// offset, and the longest key weave (atomicMax into *maxlen).
+__global__ __launch_bounds__(256) void k_seg_off(const uint32_t *__restrict__ seg_start, uint32_t S,
+                                                 uint32_t N, uint64_t *__restrict__ seg_off,
+                                                 uint32_t *__restrict__ maxlen) {
+  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sg > S) return;
+  const uint64_t o = sg < S ? (uint64_t)seg_start[sg] + sg : (uint64_t)N + S;
+  seg_off[sg] = o;
+  if (sg < S) {
+    const uint32_t e = sg + 1 < S ? seg_start[sg + 1] + sg + 1 : N + S;
+    atomicMax(maxlen, (uint32_t)(e - o));
+  }
+}
+
 // ============================================================================
 // Host side
 // ============================================================================
@@ -2413,7 +2463,8 @@ constexpr uint64_t MAP_CHUNK_DOCS = 1ull << 20, MAP_CHUNK_NODES = 1ull << 30;
 
 int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int memspace) {
   if (!bt || !res) return fail(c, "null batch/result");
-  if (memspace != CW_MEM_HOST) return fail(c, "cw_weave_maps: only CW_MEM_HOST is supported");
+  if (memspace != CW_MEM_HOST && memspace != CW_MEM_DEVICE) return fail(c, "bad memspace");
+  const bool dev = memspace == CW_MEM_DEVICE;
   const uint64_t D = bt->n_colls;
   if (!bt->coll_offsets) return fail(c, "coll_offsets is required (host memory)");
   if (bt->coll_offsets[0] != 0) return fail(c, "coll_offsets[0] must be 0");
@@ -2433,9 +2484,15 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   const uint32_t N = (uint32_t)N64;
   HIPCHK(c, hipSetDevice(c->device));
   res->n_segs = 0;
-  res->seg_offsets[0] = 0;
   if (N == 0) {
-    memset(res->status, 0, D * 4);
+    if (dev) {
+      HIPCHK(c, hipMemsetAsync(res->status, 0, D * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(res->seg_offsets, 0, 8, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    } else {
+      memset(res->status, 0, D * 4);
+      res->seg_offsets[0] = 0;
+    }
     return 0;
   }
   if (!bt->id_key || !bt->cause || !bt->cause_is_id || !bt->kind)
@@ -2445,8 +2502,10 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   if (ensure_tables(c, D, bt->coll_offsets)) return -1;
   auto &t = c->tab;
   const uint32_t T = t.T;
-  uint64_t *id = scratch_t<uint64_t>(c, "m_id", N), *cause = scratch_t<uint64_t>(c, "m_cause", N);
-  uint8_t *cis = scratch_t<uint8_t>(c, "m_cis", N), *kind = scratch_t<uint8_t>(c, "m_kind", N);
+  const uint64_t *id = dev ? bt->id_key : scratch_t<uint64_t>(c, "m_id", N);
+  const uint64_t *cause = dev ? bt->cause : scratch_t<uint64_t>(c, "m_cause", N);
+  const uint8_t *cis = dev ? bt->cause_is_id : scratch_t<uint8_t>(c, "m_cis", N);
+  const uint8_t *kind = dev ? bt->kind : scratch_t<uint8_t>(c, "m_kind", N);
   uint32_t *status = scratch_t<uint32_t>(c, "m_status", D);
   uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
   uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
@@ -2462,11 +2521,13 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
     return fail(c, "out of device memory (maps, N=%u)", N);
   if (!grid_ok(T, SORT_THREADS) || !grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
 
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(id, bt->id_key, (size_t)N * 8, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(cause, bt->cause, (size_t)N * 8, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(cis, bt->cause_is_id, N, hipMemcpyHostToDevice));
-  HIPCHK(c, hipMemcpy(kind, bt->kind, N, hipMemcpyHostToDevice));
+  if (!dev) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy((void *)id, bt->id_key, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)cause, bt->cause, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)cis, bt->cause_is_id, N, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)kind, bt->kind, N, hipMemcpyHostToDevice));
+  }
   HIPCHK(c, hipMemsetAsync(status, 0, D * 4, c->stream));
   uint32_t key_bits = bt->key_bits;
   if (key_bits == 0 && find_key_bits(c, id, N, &key_bits)) return -1;
@@ -2504,18 +2565,24 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
                        dev_tab(c, "t_doc_off"), tcnt);
   }
   if (check_launch(c, "m_segcount")) return -1;
-  std::vector<uint32_t> h_tsb(T);
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(h_tsb.data(), tcnt, (size_t)T * 4, hipMemcpyDeviceToHost));
-  uint64_t S = 0;
-  for (uint32_t i = 0; i < T; i++) {
-    const uint32_t v = h_tsb[i];
-    h_tsb[i] = (uint32_t)S;
-    S += v;
+  // key weaves before each tile (device scan) and their number S (one readback)
+  uint32_t *chunk = scratch_t<uint32_t>(c, "m_chunk", (T + 1023) / 1024 + 1);
+  uint32_t *small = scratch_t<uint32_t>(c, "m_small", 4);
+  if (!chunk || !small) return fail(c, "out of device memory (maps scan)");
+  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+  HIPCHK(c, hipMemsetAsync(small, 0, 16, c->stream));
+  {
+    const uint32_t nb = (T + 1023) / 1024;
+    hipLaunchKernelGGL(k_scan_chunks, dim3(nb), dim3(1024), 0, c->stream, tcnt, T, tsb, chunk);
+    hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, c->stream, chunk, nb, small);
+    hipLaunchKernelGGL(k_scan_add, dim3(nb), dim3(1024), 0, c->stream, tsb, T, chunk);
   }
+  if (check_launch(c, "m_scan")) return -1;
+  HIPCHK(c, hipMemcpyAsync(c->pin_small, small, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const uint64_t S = c->pin_small[0];
   if (S > res->cap_segs)
     return fail(c, "cap_segs too small: %llu key weaves", (unsigned long long)S);
-  HIPCHK(c, hipMemcpy(tsb, h_tsb.data(), (size_t)T * 4, hipMemcpyHostToDevice));
   uint32_t *seg_start = scratch_t<uint32_t>(c, "m_segstart", S + 1);
   uint32_t *seg_coll = scratch_t<uint32_t>(c, "m_segcoll", S);
   uint64_t *seg_key = scratch_t<uint64_t>(c, "m_segkey", S);
@@ -2549,17 +2616,19 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   if (check_launch(c, "m_segroots")) return -1;
 
   // key weave s = list document [seg_start[s] + s, seg_start[s+1] + s + 1)
-  std::vector<uint32_t> h_start(S);
+  hipLaunchKernelGGL(k_seg_off, dim3((uint32_t)((S + 256) / 256)), dim3(256), 0, c->stream,
+                     seg_start, (uint32_t)S, N, seg_off, small + 1);
+  if (check_launch(c, "m_segoff")) return -1;
+  HIPCHK(c, hipMemcpyAsync(c->pin_small, small + 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(h_start.data(), seg_start, S * 4, hipMemcpyDeviceToHost));
-  uint64_t *loff = res->seg_offsets;
-  for (uint64_t sg = 0; sg < S; sg++) loff[sg] = h_start[sg] + sg;
-  loff[S] = NL;
-  HIPCHK(c, hipMemcpy(seg_off, loff, (S + 1) * 8, hipMemcpyHostToDevice));
+  const uint64_t max_len = c->pin_small[0];
+  std::vector<uint64_t> loff;  // host copy, only for the list pipeline's chunks
+  if (!(c->map_small && max_len <= SMALL_MAX)) {
+    loff.resize(S + 1);
+    HIPCHK(c, hipMemcpy(loff.data(), seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+  }
 
   // 4. every key weave is a list weave -- (s/weave-node key-weave ...), map.cljc:40-41
-  uint64_t max_len = 0;
-  for (uint64_t sg = 0; sg < S; sg++) max_len = std::max<uint64_t>(max_len, loff[sg + 1] - loff[sg]);
   if (c->map_small && max_len <= SMALL_MAX) {
     // key weaves are tiny (config 4: a few nodes per key): one wave each
     Launch L(c, "m_small", (double)NL * (8 + 8 + 1 + 4) + (double)S * 12);
@@ -2602,13 +2671,14 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   }
   if (check_launch(c, "m_active")) return -1;
 
+  const hipMemcpyKind out_kind = dev ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+  HIPCHK(c, hipMemcpyAsync(res->seg_perm, seg_perm, NL * 4, out_kind, c->stream));
+  HIPCHK(c, hipMemcpyAsync(res->seg_offsets, seg_off, (S + 1) * 8, out_kind, c->stream));
+  HIPCHK(c, hipMemcpyAsync(res->seg_coll, seg_coll, S * 4, out_kind, c->stream));
+  HIPCHK(c, hipMemcpyAsync(res->seg_key, seg_key, S * 8, out_kind, c->stream));
+  HIPCHK(c, hipMemcpyAsync(res->seg_active, seg_act, S * 8, out_kind, c->stream));
+  HIPCHK(c, hipMemcpyAsync(res->status, status, D * 4, out_kind, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(res->seg_perm, seg_perm, NL * 4, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(res->seg_coll, seg_coll, S * 4, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(res->seg_key, seg_key, S * 8, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(res->seg_active, seg_act, S * 8, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipMemcpy(res->status, status, D * 4, hipMemcpyDeviceToHost));
-  HIPCHK(c, hipDeviceSynchronize());
   res->n_segs = S;
   if (c->prof) return collect_prof(c);
   return 0;

@@ -172,7 +172,8 @@ typedef struct {
   uint32_t *status;       /* [n_colls] CW_STATUS_* bits                                     */
 } cw_map_result;
 
-/* Host memory only (memspace must be CW_MEM_HOST in this version). */
+/* memspace: where id_key / cause / cause_is_id / kind and every result array
+ * live (coll_offsets is always host memory; n_segs is returned in the struct). */
 int cw_weave_maps(cw_ctx *ctx, const cw_map_batch *batch, cw_map_result *result, int memspace);
 
 /* ---------------------------------------------------------------- merge ---- */

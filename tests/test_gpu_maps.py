@@ -233,3 +233,34 @@ def test_repeat_calls_identical(weaver):
     b = weaver.weave_maps(off, idk, ck, ci, kd, tb)
     for f in ("seg_offsets", "seg_coll", "seg_key", "seg_active", "seg_perm", "status"):
         np.testing.assert_array_equal(getattr(a, f), getattr(b, f))
+
+
+def test_device_memory_call_matches_host(weaver):
+    """cw_weave_maps with CW_MEM_DEVICE (what bench.py --config 4 times) gives
+    the host-memory call's key weaves and active nodes."""
+    import torch
+
+    spec = gen.CONFIG4
+    lay, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 500, nthreads=8)
+    host = weaver.weave_maps(off, idk, ck, ci, kd, tb, lay.key_bits)
+    dev = torch.device("cuda", 0)
+    g = [torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+         for x in (idk, ck, ci, kd)]
+    N, D = len(idk), len(off) - 1
+    o = {"seg_offsets": torch.zeros(N + 1, dtype=torch.int64, device=dev),
+         "seg_coll": torch.zeros(N, dtype=torch.int32, device=dev),
+         "seg_key": torch.zeros(N, dtype=torch.int64, device=dev),
+         "seg_active": torch.zeros(N, dtype=torch.int64, device=dev),
+         "seg_perm": torch.zeros(2 * N, dtype=torch.int32, device=dev),
+         "status": torch.zeros(D, dtype=torch.int32, device=dev)}
+    S = weaver.weave_maps_device(off, [x.data_ptr() for x in g], tb, lay.key_bits,
+                                 {k: v.data_ptr() for k, v in o.items()}, N)
+    assert S == len(host.seg_key)
+    np.testing.assert_array_equal(o["seg_offsets"][:S + 1].cpu().numpy().view(np.uint64),
+                                  host.seg_offsets)
+    np.testing.assert_array_equal(o["seg_key"][:S].cpu().numpy().view(np.uint64), host.seg_key)
+    np.testing.assert_array_equal(o["seg_active"][:S].cpu().numpy(), host.seg_active)
+    np.testing.assert_array_equal(o["seg_perm"][:N + S].cpu().numpy().view(np.uint32),
+                                  host.seg_perm)
+    np.testing.assert_array_equal(o["status"].cpu().numpy().view(np.uint32), host.status)
