@@ -276,6 +276,78 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
   }
 }
 
+// Small documents (every one <= TILE): packs of whole consecutive documents
+// (<= TILE elements) are sorted entirely in LDS by (document in pack, digit
+// bits of the key) -- stable LSD sub-passes -- and written back in place, one
+// kernel instead of the global hist/scan/scatter passes (maps: 10^6
+// collections of ~100 nodes, and their key weaves).
+template <typename K>
+__global__ __launch_bounds__(SORT_THREADS) void k_pack_sort(
+    const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
+    uint32_t *__restrict__ vals_out, const uint32_t *__restrict__ pack_doc0,
+    const uint32_t *__restrict__ doc_off, uint32_t shift, uint32_t kbits, uint32_t dbits) {
+  constexpr uint32_t IT = SORT_ITEMS;
+  __shared__ K skey[TILE];
+  __shared__ uint32_t sval[TILE];
+  __shared__ uint32_t dstart[TILE + 1];
+  __shared__ uint32_t wcnt[SORT_WAVES][SUB_BINS];
+  __shared__ uint32_t run[64];
+  const uint32_t pk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t d0 = pack_doc0[pk], d1 = pack_doc0[pk + 1], nd = d1 - d0;
+  const uint32_t s = doc_off[d0], len = doc_off[d1] - s;
+  for (uint32_t i = tid; i <= nd; i += SORT_THREADS) dstart[i] = doc_off[d0 + i] - s;
+  __syncthreads();
+  const K kmask = kbits >= 8 * sizeof(K) ? ~(K)0 : (((K)1 << kbits) - 1);
+  K ck[IT];  // composite key: document in pack above the key bits
+  K key[IT];
+  uint32_t val[IT], sd[IT], pos[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t j = wb_elem<IT>(u);
+    key[u] = 0;
+    val[u] = 0;
+    ck[u] = 0;
+    if (j < len) {
+      uint32_t lo = 0, hi = nd;  // document of element j
+      while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (dstart[m] <= j) lo = m; else hi = m;
+      }
+      key[u] = keys_in[s + j];
+      val[u] = vals_in ? vals_in[s + j] : j - dstart[lo];
+      ck[u] = ((K)lo << kbits) | ((key[u] >> shift) & kmask);
+    }
+  }
+  const uint32_t bits = kbits + dbits;
+  for (uint32_t sh = 0; sh < bits; sh += SUB_BITS) {
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) sd[u] = (uint32_t)(ck[u] >> sh) & (SUB_BINS - 1);
+    rank_subdigit<SORT_THREADS, IT>(sd, len, min(SUB_BITS, bits - sh), pos, wcnt, run);
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++)
+      if (wb_elem<IT>(u) < len) {
+        skey[pos[u]] = key[u];
+        sval[pos[u]] = val[u];
+        dstart[pos[u]] = (uint32_t)(ck[u] >> kbits);  // the document, to rebuild ck
+      }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t j = wb_elem<IT>(u);
+      if (j < len) {
+        key[u] = skey[j];
+        val[u] = sval[j];
+        ck[u] = ((K)dstart[j] << kbits) | ((key[u] >> shift) & kmask);
+      }
+    }
+    __syncthreads();
+  }
+  for (uint32_t j = tid; j < len; j += SORT_THREADS) {
+    keys_out[s + j] = skey[j];
+    vals_out[s + j] = sval[j];
+  }
+}
+
 // --- join: cause -> parent rank ---------------------------------------------
 __device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *__restrict__ a, uint32_t n,
                                                     uint64_t x) {
@@ -1617,112 +1689,136 @@ __global__ __launch_bounds__(NT) void k_weft_select(
   }
 }
 
-// --- tiny documents: one wave weaves one document of <= 64 nodes -----------------
+// --- tiny documents: one block weaves every document that starts in its chunk ----
 // The same exact weave (F5 preorder) as the list pipeline, for the
-// key weaves of maps (config 4: a few nodes per key) where the per-document
-// kernels of the pipeline would dominate: every step is a wave-wide loop over
-// the document's lanes.  Outputs the doc-local weave order and the status bits.
-constexpr uint32_t SMALL_MAX = 64;
+// key weaves of maps (config 4: ~3 nodes per key) where the per-document
+// kernels of the pipeline would dominate.  A block takes the documents (of <=
+// SMALL_MAX nodes) that start in its 192-node chunk -- at most 255 nodes, one
+// per thread -- and works in LDS: ranks by counting inside the document, cause
+// ranks by binary search, effective parents, subtree sizes and preorder
+// positions by walking each node's ancestor chain (no per-step barriers).
+constexpr uint32_t SMALL_MAX = 64, SMALL_CHUNK = 192, SMALL_SLOTS = 256;
 
-__global__ __launch_bounds__(256) void k_small_weave(
+__global__ __launch_bounds__(SMALL_SLOTS) void k_small_weave(
     const uint64_t *__restrict__ doc_off, uint32_t D, const uint64_t *__restrict__ id_key,
     const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
     uint32_t *__restrict__ weave_perm, uint32_t *__restrict__ status) {
-  __shared__ uint32_t inv_s[4][SMALL_MAX];
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t d = blockIdx.x * 4 + wv;
-  if (d >= D) return;  // uniform per wave
-  const uint64_t b = doc_off[d];
-  const uint32_t m = (uint32_t)(doc_off[d + 1] - b);
-  uint32_t *inv = inv_s[wv];
-  if (m == 0) {
-    if (lane == 0) status[d] = CW_STATUS_ROOT;
-    return;
+  __shared__ uint64_t sid[SMALL_SLOTS];
+  __shared__ uint32_t ds[SMALL_CHUNK + 2], at[SMALL_SLOTS], par[SMALL_SLOTS], eff[SMALL_SLOTS];
+  __shared__ uint32_t size[SMALL_SLOTS], before[SMALL_SLOTS], dst[SMALL_CHUNK + 1];
+  __shared__ uint8_t spk[SMALL_SLOTS];
+  __shared__ uint32_t s_df, s_nd;
+  __shared__ uint64_t s_base;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t NL = doc_off[D], c0 = (uint64_t)blockIdx.x * SMALL_CHUNK;
+  const uint64_t c1 = min(c0 + SMALL_CHUNK, NL);
+  if (tid < 2) {  // documents [df, dl) start in [c0, c1)
+    const uint64_t x = tid == 0 ? c0 : c1;
+    uint32_t lo = 0, hi = D + 1;
+    while (lo < hi) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (doc_off[m] < x) lo = m + 1; else hi = m;
+    }
+    if (tid == 0) s_df = lo; else s_nd = lo;
   }
-  const bool v = lane < m;
-  uint64_t id = v ? id_key[b + lane] : ~0ull, ca = v ? cause_key[b + lane] : 0;
-  uint32_t kd = v ? kind[b + lane] : 0u;
-  // 1. rank by id (count of smaller ids); a repeated id is a duplicate
-  uint32_t r = 0;
-  bool dup = false;
-  for (uint32_t j = 0; j < m; j++) {
-    const uint64_t o = __shfl(id, (int)j, 64);
-    r += o < id ? 1u : 0u;
-    dup |= (o == id) && j != lane;
-  }
-  const bool anydup = __ballot(dup) != 0;
-  if (v) inv[r] = lane;  // lane r takes the node of rank r
-  __builtin_amdgcn_wave_barrier();
-  // duplicate ids leave ranks unfilled: any permutation (the document is flagged)
-  const uint32_t src = v ? (anydup ? lane : inv[lane]) : 0u;
-  __builtin_amdgcn_wave_barrier();
-  id = __shfl(id, (int)src, 64);
-  ca = __shfl(ca, (int)src, 64);
-  kd = (uint32_t)__shfl((int)kd, (int)src, 64);
-  uint32_t st = dup ? (uint32_t)CW_STATUS_DUP : 0u;
-  // 2. domain checks and the cause rank (binary search over the sorted ids)
-  uint32_t par = 0;
+  __syncthreads();
+  const uint32_t df = s_df, nd = (c1 > c0 ? s_nd : s_df) - df;
+  if (nd == 0) return;  // uniform
+  if (tid <= nd) ds[tid] = (uint32_t)(doc_off[df + tid] - doc_off[df]);
+  if (tid < nd) dst[tid] = 0;
+  if (tid == 0) s_base = doc_off[df];
+  __syncthreads();
+  const uint64_t base = s_base;
+  const uint32_t span = ds[nd];
+  const bool v = tid < span;
+  uint32_t di = 0;  // my document (in the chunk)
   if (v) {
-    if (lane == 0) {
+    uint32_t lo = 0, hi = nd;
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (ds[m] <= tid) lo = m; else hi = m;
+    }
+    di = lo;
+  }
+  const uint32_t g0 = v ? ds[di] : 0u, m = v ? ds[di + 1] - g0 : 0u, li = tid - g0;
+  const uint64_t id = v ? id_key[base + tid] : 0, ca = v ? cause_key[base + tid] : 0;
+  const uint32_t kd = v ? kind[base + tid] : 0u;
+  if (v) sid[tid] = id;
+  __syncthreads();
+  // 1. rank in the document (count of smaller ids); duplicates flag the document
+  uint32_t r = 0, st = 0;
+  for (uint32_t j = 0; j < m; j++) {
+    const uint64_t o = sid[g0 + j];
+    r += o < id ? 1u : 0u;
+    if (o == id && j != li) st |= CW_STATUS_DUP;
+  }
+  if (v && m > SMALL_MAX) st |= CW_STATUS_INTERNAL;
+  if (st) atomicOr(&dst[di], st);
+  __syncthreads();
+  const bool dirty = v && (dst[di] & CW_STATUS_DUP);
+  if (dirty) r = li;  // any permutation (the document is flagged)
+  if (v) at[g0 + r] = tid;
+  __syncthreads();
+  // 2. domain checks; cause rank by binary search over the ranked ids
+  uint32_t p = 0;
+  if (v) {
+    if (r == 0) {
       if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
     } else {
       if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
+      uint32_t lo = 0, hi = m;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sid[at[g0 + mid]] < ca) lo = mid + 1; else hi = mid;
+      }
+      if (lo >= m || sid[at[g0 + lo]] != ca) st |= CW_STATUS_ORPHAN;
+      else if (lo >= r) st |= CW_STATUS_NON_LAMPORT;
+      else p = lo;
     }
+    par[g0 + r] = p;
+    spk[g0 + r] = (uint8_t)(is_special((uint8_t)kd) ? 1 : 0);
+    size[g0 + r] = 1;
   }
-  uint32_t lo = 0, hi = m;  // lower bound of ca among ids[0..m)
-  for (uint32_t step = 0; step < 7; step++) {
-    const uint32_t mid = (lo + hi) >> 1;
-    const uint64_t x = __shfl(id, (int)min(mid, 63u), 64);
-    if (lo < hi) {
-      if (x < ca) lo = mid + 1; else hi = mid;
-    }
-  }
-  const uint64_t at = __shfl(id, (int)min(lo, 63u), 64);
-  if (v && lane > 0) {
-    if (lo >= m || at != ca) st |= CW_STATUS_ORPHAN;
-    else if (lo >= lane) st |= CW_STATUS_NON_LAMPORT;
-    else par = lo;
-  }
+  if (st) atomicOr(&dst[di], st);
+  __syncthreads();
   // 3. effective parent: a non-special climbs through special causes
   const bool sp = v && is_special((uint8_t)kd);
-  uint32_t e = par;
-  {
-    bool climb = v && lane > 0 && !sp;
+  uint32_t e = p;
+  if (v && r > 0 && !sp)
+    for (uint32_t it = 0; e != 0 && spk[g0 + e] && it < m; it++) e = par[g0 + e];
+  if (v) eff[g0 + r] = e;
+  __syncthreads();
+  // 4. subtree sizes: every node counts itself into each ancestor
+  if (v && r > 0) {
+    uint32_t a = e;
     for (uint32_t it = 0; it < m; it++) {
-      const uint32_t spe = (uint32_t)__shfl((int)(sp ? 1 : 0), (int)e, 64);
-      const uint32_t pe = (uint32_t)__shfl((int)par, (int)e, 64);
-      const bool go = climb && e != 0 && spe;
-      if (!__ballot(go)) break;
-      if (go) e = pe;
+      atomicAdd(&size[g0 + a], 1u);
+      if (a == 0) break;
+      a = eff[g0 + a];
     }
   }
-  // 4. subtree sizes, children before parents (ranks descend)
-  uint32_t size = v ? 1u : 0u;
-  for (int c = (int)m - 1; c >= 1; c--) {
-    const uint32_t sc = (uint32_t)__shfl((int)size, c, 64), pc = (uint32_t)__shfl((int)e, c, 64);
-    if (lane == pc && (uint32_t)c != lane) size += sc;
-  }
+  __syncthreads();
   // 5. siblings before me: specials first, each class by descending id
-  uint32_t before = 0;
-  for (uint32_t s = 1; s < m; s++) {
-    const uint32_t es = (uint32_t)__shfl((int)e, (int)s, 64), zs = (uint32_t)__shfl((int)size, (int)s, 64);
-    const bool ss = __shfl((int)(sp ? 1 : 0), (int)s, 64) != 0;
-    if (es == e && s != lane && lane > 0) {
-      if ((ss && !sp) || (ss == sp && s > lane)) before += zs;
+  if (v && r > 0) {
+    uint32_t bf = 0;
+    for (uint32_t q = 1; q < m; q++) {
+      if (q == r || eff[g0 + q] != e) continue;
+      const bool sq = spk[g0 + q];
+      if ((sq && !sp) || (sq == sp && q > r)) bf += size[g0 + q];
     }
+    before[g0 + r] = bf;
   }
-  // 6. preorder positions, parents first
-  uint32_t pos = 0;
-  for (uint32_t t = 1; t < m; t++) {
-    const uint32_t pp = (uint32_t)__shfl((int)pos, (int)e, 64);
-    if (lane == t) pos = pp + 1 + before;
+  __syncthreads();
+  // 6. preorder position = sum over the ancestor chain of (1 + siblings before)
+  if (v) {
+    uint32_t pos = 0, x = r;
+    for (uint32_t it = 0; x != 0 && it < m; it++) {
+      pos += 1 + before[g0 + x];
+      x = eff[g0 + x];
+    }
+    if (pos < m) weave_perm[base + g0 + pos] = li;
   }
-  if (v && pos < m) weave_perm[b + pos] = src;
-  // status: one word per document
-  uint32_t all = st;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) all |= (uint32_t)__shfl_xor((int)all, o, 64);
-  if (lane == 0) status[d] = all;
+  if (tid < nd) status[df + tid] = dst[tid];
 }
 
 // --- device exclusive scan of u32 counts (map key-weave numbering) ---------------
@@ -1816,9 +1912,11 @@ struct cw_ctx {
   std::vector<uint64_t> last_off;
   struct Tables {
     std::vector<uint32_t> doc_off, tile_start, tile_doc, tile_first, doc_log2k, doc_W, walk_first,
-        wblk_doc, wblk_w0, bkt_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0, woff_base;
+        wblk_doc, wblk_w0, bkt_off, doc_log2cap, doc_Wcap, eblk_doc, eblk_x0, woff_base,
+        pack_doc0;
     std::vector<uint64_t> slot_first;
     uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Btot = 0, Wmax = 0, Wofftot = 0;
+    uint32_t pack_dmax = 0;  // most documents in one sort pack (k_pack_sort)
     uint64_t slots = 0;
   } tab;
   bool tab_on_device = false;
@@ -1830,6 +1928,7 @@ struct cw_ctx {
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
+  uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
 };
 
 namespace {
@@ -2014,6 +2113,21 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   t.slots = slots;
   t.Be = (uint32_t)t.eblk_doc.size();
   t.Wofftot = wofft;
+  // sort packs: runs of whole consecutive documents of <= TILE nodes in all
+  // (only used when every document fits one tile)
+  t.pack_doc0.clear();
+  t.pack_dmax = 0;
+  if (t.nmax <= TILE) {
+    uint64_t d = 0;
+    while (d < D) {
+      const uint64_t d0 = d;
+      while (d < D && off[d + 1] - off[d0] <= TILE) d++;
+      if (d == d0) d++;  // (cannot happen: every document <= TILE)
+      t.pack_doc0.push_back((uint32_t)d0);
+      t.pack_dmax = std::max(t.pack_dmax, (uint32_t)(d - d0));
+    }
+    t.pack_doc0.push_back((uint32_t)D);
+  }
   t.bkt_off[D] = stot;
   t.Btot = stot;
   t.T = (uint32_t)t.tile_doc.size();
@@ -2030,7 +2144,7 @@ int upload_tables(cw_ctx *c) {
       {"t_walk_first", &t.walk_first}, {"t_wblk_doc", &t.wblk_doc},  {"t_wblk_w0", &t.wblk_w0},
       {"t_bkt_off", &t.bkt_off}, {"t_doc_log2cap", &t.doc_log2cap},
       {"t_doc_Wcap", &t.doc_Wcap}, {"t_eblk_doc", &t.eblk_doc}, {"t_eblk_x0", &t.eblk_x0},
-      {"t_woff_base", &t.woff_base}};
+      {"t_woff_base", &t.woff_base}, {"t_pack_doc0", &t.pack_doc0}};
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the pinned staging may still be read
   size_t total = (t.slot_first.size() + 64) * 8;
   for (auto &it : items) total += (it.second->size() + 64) * 4;
@@ -2073,6 +2187,23 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
                K **kout, uint32_t **vout, uint32_t *inv = nullptr) {
   auto &t = c->tab;
   if (bits == 0) bits = 1;
+  const uint32_t dbits_pack = ceil_log2(std::max(t.pack_dmax, 1u));
+  if (c->pack_sort && !inv && !t.pack_doc0.empty() && bits + dbits_pack <= 8 * sizeof(K)) {
+    // every document fits one tile: one in-LDS sort per pack of documents
+    const uint32_t P = (uint32_t)t.pack_doc0.size() - 1;
+    char nm[48];
+    snprintf(nm, sizeof nm, "%s_pack", tag);
+    {
+      Launch L(c, nm, (double)N * (2 * sizeof(K) + (vin ? 8 : 4)));
+      hipLaunchKernelGGL(k_pack_sort<K>, dim3(P), dim3(SORT_THREADS), 0, c->stream, kin, vin, kA,
+                         vA, dev_tab(c, "t_pack_doc0"), dev_tab(c, "t_doc_off"), shift0, bits,
+                         dbits_pack);
+    }
+    if (check_launch(c, nm)) return -1;
+    *kout = kA;
+    *vout = vA;
+    return 0;
+  }
   const uint32_t maxd = std::min<uint32_t>(c->max_digit, MAX_DIGIT);
   const int passes = (int)((bits + maxd - 1) / maxd);
   uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * (1u << ((bits + passes - 1) / passes)));
@@ -2632,8 +2763,9 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   if (c->map_small && max_len <= SMALL_MAX) {
     // key weaves are tiny (config 4: a few nodes per key): one wave each
     Launch L(c, "m_small", (double)NL * (8 + 8 + 1 + 4) + (double)S * 12);
-    hipLaunchKernelGGL(k_small_weave, dim3((uint32_t)((S + 3) / 4)), dim3(256), 0, c->stream,
-                       seg_off, (uint32_t)S, lid, lcause, lkind, lperm, lst);
+    hipLaunchKernelGGL(k_small_weave, dim3((uint32_t)((NL + SMALL_CHUNK - 1) / SMALL_CHUNK)),
+                       dim3(SMALL_SLOTS), 0, c->stream, seg_off, (uint32_t)S, lid, lcause, lkind,
+                       lperm, lst);
   }
   if (check_launch(c, "m_small")) return -1;
   std::vector<uint64_t> rel;
@@ -2964,6 +3096,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
+  c->pack_sort = knob("CW_PACK_SORT", 1);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

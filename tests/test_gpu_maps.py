@@ -26,18 +26,23 @@ NIL = (1 << 64) - 1
 @pytest.fixture(scope="module", params=["small", "pipeline"])
 def weaver(request):
     """Both ways of weaving key weaves: one wave per tiny key weave
-    (k_small_weave) and the full list pipeline (CW_MAP_SMALL=0)."""
+    (k_small_weave, LDS pack sorts) and the full list pipeline (CW_MAP_SMALL=0,
+    global radix passes)."""
     import os
 
-    old = os.environ.get("CW_MAP_SMALL")
-    os.environ["CW_MAP_SMALL"] = "1" if request.param == "small" else "0"
+    # "pipeline" also sorts with the global radix passes instead of the LDS packs
+    knobs = ({"CW_MAP_SMALL": "1", "CW_PACK_SORT": "1"} if request.param == "small"
+             else {"CW_MAP_SMALL": "0", "CW_PACK_SORT": "0"})
+    old = {k: os.environ.get(k) for k in knobs}
+    os.environ.update(knobs)
     try:
         w = abi.Weaver(0)
     finally:
-        if old is None:
-            os.environ.pop("CW_MAP_SMALL", None)
-        else:
-            os.environ["CW_MAP_SMALL"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     yield w
     w.close()
 

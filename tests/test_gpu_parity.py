@@ -21,7 +21,8 @@ pytestmark = pytest.mark.gpu
 
 # Front ends: "front" = rank directories for every document (CW_FRONT_MIN_AVG=0
 # also sends tiny documents through it), "radix" = segmented radix sort + join.
-FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"}, "radix": {"CW_FRONT": "0"}}
+FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"}, "radix": {"CW_FRONT": "0"},
+          "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"}}  # no LDS pack sorts
 
 
 @pytest.fixture(scope="module", params=sorted(FRONTS))
