@@ -996,7 +996,21 @@ __global__ __launch_bounds__(NT) void k_tree(
       qns[k] = ok ? nsc[base + r] : 0u;
     }
   };
+  // loads that depend on a node's nsc, issued one tile ahead: the newest
+  // non-special of a last special's parent, and the thread of a parent two or
+  // more tiles back (both final by then)
+  uint32_t dfn[IT], dth[IT];
+  auto load_dep = [&](uint32_t r0) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t r = r0 + k * NT + tid, ns = qns[k], e = ns & ~NSC_UP;
+      const bool up = r < n && r > 0 && (ns & NSC_UP);
+      dfn[k] = up && special_at(r) ? fcN[base + e] : 0u;
+      dth[k] = up && e + TILE_T < r0 ? thr[base + e] : 0u;
+    }
+  };
   load_tile(0);
+  load_dep(0);
   for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
     const uint32_t len = min((uint32_t)TILE_T, n - r0);
     uint32_t fs4[IT], ns4[IT], fcr[IT], flg[IT];
@@ -1020,12 +1034,12 @@ __global__ __launch_bounds__(NT) void k_tree(
         uint32_t ns = ns4[k], e = 0;
         if (ns & NSC_UP) {
           e = ns & ~NSC_UP;
-          ns = sp ? fcN[base + e] : 0u;  // last special -> newest non-special
+          ns = sp ? dfn[k] : 0u;  // last special -> newest non-special
         }
         if (ns) tv = RES | ns;
         else if (e >= r0) tv = e - r0;
         else if (e + TILE_T >= r0) tv = P[e + TILE_T - r0];
-        else tv = RES | thr[base + e];
+        else tv = RES | dth[k];
       }
       T[j] = tv;
       // after a non-special comes its first child, which is its
@@ -1067,6 +1081,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     uint32_t *x = T;  // this tile's resolved threads become the previous tile's
     T = P;
     P = x;
+    if (r0 + TILE_T < n) load_dep(r0 + TILE_T);
   }
   if (tprof && tid == 0)
     for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
