@@ -870,9 +870,22 @@ __global__ __launch_bounds__(NT) void k_tree(
   auto hide_at = [&](uint32_t r) -> bool {
     return in_lds ? ((hide_bm[r >> 5] >> (r & 31)) & 1u) : is_hide(skind[base + r]);
   };
+  // parents of the next tile are loaded while this tile is sorted
+  uint32_t qpar[IT];
+  auto load_par = [&](uint32_t r0) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t r = r0 + wb_elem<IT>(k);
+      qpar[k] = r < n ? par[base + r] : 0u;
+    }
+  };
+  load_par(0);
   for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
     const uint32_t len = min((uint32_t)TILE_T, n - r0);
-    uint32_t key[IT], rk[IT], sd[IT], pos[IT];
+    uint32_t key[IT], rk[IT], sd[IT], pos[IT], cpar[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) cpar[k] = qpar[k];
+    if (r0 + TILE_T < n) load_par(r0 + TILE_T);
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = wb_elem<IT>(k), r = r0 + j;
@@ -888,7 +901,7 @@ __global__ __launch_bounds__(NT) void k_tree(
         const bool sp = special_at(r);
         // causes are older (c < r); the clamps only keep out-of-domain
         // documents (duplicate ids leave ranks unwritten) in bounds
-        uint32_t c = par[base + r];
+        uint32_t c = cpar[k];
         c = c < r ? c : 0u;
         if (!sp)
           while (c != 0 && special_at(c)) {
