@@ -3113,8 +3113,9 @@ int cw_ctx_create(int device, cw_ctx **out) {
     return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
   };
   c->tb = knob("CW_TB", 1024);
-  c->walk_threads = knob("CW_WALK_THREADS", 1024);
-  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 2048));
+  c->walk_threads = knob("CW_WALK_THREADS", 512);
+  // one walker per thread (span == threads): a dynamic walker queue per block was slower
+  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 512));
   c->walk_lds = knob("CW_WALK_LDS", 0);
   c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
   c->min_log2cap = std::max(2u, knob("CW_LOG2CAP", 4));

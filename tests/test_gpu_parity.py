@@ -240,6 +240,7 @@ def test_duplicate_ids_beside_clean_documents(weaver):
 
 KNOBS = [{}, {"CW_LOG2CAP": "5"}, {"CW_LOG2K": "4", "CW_LOG2CAP": "5"},
          {"CW_MAX_DIGIT": "8"}, {"CW_WALK_THREADS": "256", "CW_WALK_SPAN": "512"},
+         {"CW_WALK_THREADS": "1024", "CW_WALK_SPAN": "2048"},
          {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"}, {"CW_TREE": "0"}, {"CW_TREE": "1"}]
 
 
