@@ -4,24 +4,29 @@
 // Pipeline for a batch of independent CausalLists (DESIGN.md has the byte
 // accounting and the reference lines each stage replaces):
 //
-//   1. id sort      segmented LSD radix sort of (id_key, input index) per doc
-//                   -- (sort (::s/nodes ct)), list.cljc:28
-//   2. join         cause -> parent rank by binary search in the sorted ids,
-//                   domain checks (root, dup, orphan, lamport) -- shared.cljc:163-178
-//   3. eff parent   non-specials climb through special causes
-//   4. child sort   segmented radix sort by (eff parent, class): siblings
-//                   specials-first, then by id -- weave-later?, shared.cljc:202-223
-//   5. links        first child / next sibling / parent per node, visibility
-//                   (hide?, list.cljc:48-55 via SURVEY F6), splitter flags
-//   6. Euler walk   each splitter arc walks its sublist of the Euler tour
-//   7. rank         per-document list ranking of the sublists in LDS
-//   8. emit         weave position -> weave_perm, visibility, counts
-//   9. pack         visibility bytes -> bitmap
-//  (10. yarns       stable radix partition of the id order by site, spin 1-arity)
+//   1-2. front end  (dense ids) k_fdir / k_frank / k_fplace: per-document rank
+//                   directory (id bitmap + popcounts) -> id order, cause ranks
+//                   and the domain checks of shared.cljc:163-178, written in
+//                   rank order through window records; (sparse ids) segmented
+//                   LSD radix sort + bucket index + join -- (sort (::s/nodes ct)),
+//                   list.cljc:28, and the cause scan of weave-node
+//   3-5. tree       k_tree, one workgroup per document: effective parents
+//                   (SURVEY F5), sibling order (weave-later?, shared.cljc:202-223),
+//                   first children, threads -> each node's preorder successor,
+//                   visibility (hide?, list.cljc:48-55 via SURVEY F6), splitters
+//   6.   walk       each splitter's walker follows successors to the next splitter
+//   7.   rank       per-document list ranking of the sublists in LDS
+//   8.   emit       weave position -> weave_perm, visibility, counts
+//   9.   pack       visibility bytes -> bitmap
+//  (10.  yarns      stable radix partition of the id order by site, spin 1-arity)
 //
-// Everything is integer work bounded by HBM/L2 traffic; MFMA is not used.
-// Launch grids map documents contiguously so the blocks that touch one
-// document run close together in time and share its lines in L2.
+// Maps (cw_weave_maps), merge (cw_merge_lists) and weft (cw_weft_lists) reuse
+// the pipeline after their own selection / grouping kernels; tiny documents
+// (map key weaves) have their own in-LDS sort and weave kernels.
+//
+// Everything is integer work bounded by HBM/L2 traffic and latency; MFMA is
+// not used.  Tile grids map documents contiguously onto one XCD so the blocks
+// that touch one document run close together in time and share its L2.
 
 #include <hip/hip_runtime.h>
 
@@ -793,7 +798,7 @@ __global__ __launch_bounds__(NT) void k_fplace(
 // non-specials by descending id (weave-later?, shared.cljc:202-223): with the
 // group key (eff parent, class) the next sibling of r is the previous node of
 // the same group in rank order, and the first child is the group's last node.
-// Ranks are swept in tiles of TREE_TILE: each tile is sorted by group key in
+// Ranks are swept in tiles of TILE_T ranks: each tile is sorted by group key in
 // LDS (stable), neighbours inside the tile link directly, and a per-group
 // "last node so far" table (fcS/fcN, which ends as the first-child table)
 // links across tiles.  A second sweep assembles the link word the walk uses.
@@ -1180,10 +1185,10 @@ __global__ __launch_bounds__(1024) void k_walk(
 }
 
 // --- sublist ranking: one workgroup per document, all in LDS -------------------
-// The W sublists of a document form one linked list (the Euler tour).  Every
+// The W sublists of a document form one linked list (the preorder).  Every
 // CHAIN-th sublist id heads an LDS chain; one lane per head walks its chain
 // (prefix sums in place), lane 0 ranks the <= W/CHAIN chains, then every
-// sublist gets chain base + local prefix = number of down arcs before it, and
+// sublist gets chain base + local prefix = number of nodes before it, and
 // its index in tour order (order[] lists sublists in tour order for the emit).
 __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
                                               const uint32_t *__restrict__ wnext,
@@ -1217,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
     uint32_t j = h * CHAIN, acc = 0, len = 0;
     for (;;) {
       const uint32_t x = nx[j], cval = val[j];
-      val[j] = acc;            // down arcs before j inside the chain
+      val[j] = acc;            // nodes before j inside the chain
       nx[j] = (h << 24) | len;  // chain of j, index of j inside the chain
       acc += cval;
       len++;
@@ -2476,7 +2481,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
               acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
     }
 
-    // 6. Euler walk
+    // 6. walk: sublists of the preorder successor list
     HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
     {
       Launch L(c, "walk", (double)N * (4 + 4));

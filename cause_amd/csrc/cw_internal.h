@@ -15,24 +15,18 @@ constexpr uint32_t MAX_BINS = 1u << MAX_DIGIT;
 constexpr uint32_t SUB_BITS = 6;                  // in-tile sub-pass digit
 constexpr uint32_t SUB_BINS = 1u << SUB_BITS;
 
-// Tree sweep: one workgroup per document, ranks in LDS-sorted tiles.
-constexpr uint32_t TREE_THREADS = 1024;
-constexpr uint32_t TREE_TILE = 4096;
 
-// Join: per-document sample of the sorted ids (every 2^ls-th key, <= MAX_SAMPLES)
-// staged in LDS so the cause search touches global memory only at the end.
+// Join (general front end): nodes per lane, their loads and bucket searches interleaved.
 constexpr int JOIN_ITEMS = 4;
 
-// Euler walk: one walker per splitter arc; <= MAX_SUBLISTS sublists per document
+// Walk: one walker per splitter node; <= MAX_SUBLISTS sublists per document
 // so the sublist ranking of a document fits one workgroup's LDS.
-constexpr uint32_t WALK_THREADS = 256;
-constexpr uint32_t WALK_SPAN = 2048;              // walkers pulled by one workgroup
 constexpr uint32_t MAX_SUBLISTS = 16384;          // rank: 128 KiB of LDS
 constexpr uint32_t CHAIN = 64;                     // rank: sublists per LDS chain head
 constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter block
 
-// link word: low 32 = first child (bit 31: node renders, bit 30: node is a
-// splitter), high 32 = next arc after the node's up arc.
+// link word (u32): low 30 bits = the node's preorder successor (SUCC_END for the
+// last node), bit 31 = the node renders, bit 30 = the node is a splitter.
 constexpr uint32_t LINK_VIS = 0x80000000u;
 constexpr uint32_t LINK_SPLIT = 0x40000000u;
 constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
