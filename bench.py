@@ -38,12 +38,29 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the cpu_baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4],
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4, 5],
                     help="BASELINE.json configs[config-1]: 2 = the headline batch "
                          "(default), 1 = one 100k-node list (latency; replicas on N GPUs), "
-                         "4 = CausalMap collections (10^6 x 100 nodes per GPU)")
+                         "4 = CausalMap collections (10^6 x 100 nodes per GPU), "
+                         "5 = one giant list (--giant nodes; replicas on N GPUs)")
+    ap.add_argument("--giant", type=int, default=1 << 26, help="--config 5: nodes in the list")
     ap.add_argument("--colls", type=int, default=1_000_000, help="--config 4: collections per GPU")
     return ap.parse_args()
+
+
+def cpu_baseline_prefix(idk, ck, kd, prefix):
+    """Config 5: the literal fold is quadratic, so it runs on the id-order prefix
+    of `prefix` nodes of the same list (causally closed: causes are older)."""
+    import oracle
+
+    o = np.argsort(idk, kind="stable")[:prefix]
+    t0 = time.perf_counter()
+    _, st = oracle.list_weave(idk[o], ck[o], kd[o], oracle.METHOD_LITERAL)
+    t = time.perf_counter() - t0
+    return {"value": prefix / t, "unit": "nodes/s", "cores": 1, "kind": "port",
+            "sample": f"literal weave-node fold (shared.cljc:194-241) in C on the first {prefix:,} "
+                      f"nodes (id order) of the same list, {t:.1f} s; the fold is quadratic, so "
+                      f"the whole list would run far slower than this rate"}
 
 
 def cpu_baseline(spec, budget_s, max_docs=64):
@@ -196,6 +213,13 @@ def main():
         spec, D = gen.CONFIG1, 1
         d0, d1 = 0, 1
         workload = "config1: one CausalList of 100,000 inserts from 4 sites, full reweave"
+    elif a.config == 5:
+        # one giant list (config 5 scaled to one GPU: the 2e9-node list needs the
+        # RCCL sample sort of DESIGN.md 8); every rank weaves its own replica
+        spec, D = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.giant), 1
+        d0, d1 = 0, 1
+        workload = (f"config5 (scaled): one CausalList of {a.giant + 1:,} nodes, 8 sites, "
+                    f"10% hides, full reweave on the giant-document path")
     else:
         spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
         D = a.docs
@@ -267,7 +291,8 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
-            cpu = cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64)
+            cpu = (cpu_baseline_prefix(idk, ck, kd, 100_000) if a.config == 5 else
+                   cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64))
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
             "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
@@ -278,7 +303,7 @@ def main():
                        "nodes_per_gpu": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
                        "p_show": spec.p_show, "p_conj": spec.p_conj,
                        "key_bits": layout.key_bits,
-                       "parallelism": (f"replicas x{world}" if a.config == 1
+                       "parallelism": (f"replicas x{world}" if a.config in (1, 5)
                                        else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

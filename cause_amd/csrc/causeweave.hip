@@ -123,6 +123,66 @@ __global__ __launch_bounds__(1024) void k_radix_scan(uint32_t *__restrict__ hist
       }
 }
 
+// One document of many tiles (the giant-document path): the per-document scan
+// above would walk every tile in one workgroup.  Chunked scan instead, in
+// digit-major then tile order: per-chunk column sums, a scan over chunks per
+// digit, a scan over digits, and each chunk applies its bases.
+constexpr uint32_t GSCAN_CHUNK = 128;  // tiles per chunk
+
+__global__ __launch_bounds__(1024) void k_gscan_colsum(const uint32_t *__restrict__ hist, uint32_t T,
+                                                       uint32_t nb, uint32_t *__restrict__ cs) {
+  const uint32_t c = blockIdx.x, t0 = c * GSCAN_CHUNK, t1 = min(T, t0 + GSCAN_CHUNK);
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    uint32_t sum = 0;
+    for (uint32_t t = t0; t < t1; t++) sum += hist[(size_t)t * nb + b];
+    cs[(size_t)c * nb + b] = sum;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_gscan_chunks(uint32_t *__restrict__ cs, uint32_t nc,
+                                                       uint32_t nb, uint32_t *__restrict__ tot) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  uint32_t run = 0;
+  for (uint32_t c = 0; c < nc; c++) {
+    const uint32_t v = cs[(size_t)c * nb + b];
+    cs[(size_t)c * nb + b] = run;
+    run += v;
+  }
+  tot[b] = run;
+}
+
+__global__ __launch_bounds__(1024) void k_gscan_bins(uint32_t *__restrict__ tot, uint32_t nb,
+                                                     uint32_t base) {
+  __shared__ uint32_t wtot[16];
+  const uint32_t per = (nb + 1023) / 1024, b0 = threadIdx.x * per;
+  uint32_t v[2] = {0, 0}, sum = 0;
+  for (uint32_t k = 0; k < per && k < 2; k++) {
+    v[k] = b0 + k < nb ? tot[b0 + k] : 0u;
+    sum += v[k];
+  }
+  uint32_t run = base + block_exscan<1024>(sum, wtot, nullptr);
+  for (uint32_t k = 0; k < per && k < 2; k++)
+    if (b0 + k < nb) {
+      tot[b0 + k] = run;
+      run += v[k];
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_gscan_apply(uint32_t *__restrict__ hist, uint32_t T,
+                                                      uint32_t nb, const uint32_t *__restrict__ cs,
+                                                      const uint32_t *__restrict__ tot) {
+  const uint32_t c = blockIdx.x, t0 = c * GSCAN_CHUNK, t1 = min(T, t0 + GSCAN_CHUNK);
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    uint32_t run = tot[b] + cs[(size_t)c * nb + b];
+    for (uint32_t t = t0; t < t1; t++) {
+      const uint32_t v = hist[(size_t)t * nb + b];
+      hist[(size_t)t * nb + b] = run;
+      run += v;
+    }
+  }
+}
+
 // Element index of item k of the calling lane when ITEMS items per lane are
 // wave-blocked: wave w owns elements [w*ITEMS*64, (w+1)*ITEMS*64), item k of
 // lane l is element (w*ITEMS + k)*64 + l.
@@ -414,6 +474,26 @@ __global__ __launch_bounds__(256) void k_index(const uint64_t *__restrict__ skey
   }
   if (threadIdx.x == 0) B[nb] = n;
   if (__syncthreads_or(dup) && threadIdx.x == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
+}
+
+// k_index for a batch that is one (large) document: one thread per sorted id.
+__global__ __launch_bounds__(256) void k_index_flat(const uint64_t *__restrict__ skey, uint32_t n,
+                                                    uint32_t *__restrict__ bkt,
+                                                    uint32_t *__restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t kmin = skey[0], kmax = skey[n - 1];
+  const uint32_t sh = bucket_shift(kmax - kmin, n);
+  const uint64_t x = skey[i];
+  const uint32_t h = (uint32_t)((x - kmin) >> sh);
+  uint32_t h0 = 0;
+  if (i > 0) {
+    const uint64_t prev = skey[i - 1];
+    if (prev == x) atomicOr(&status[0], (uint32_t)CW_STATUS_DUP);
+    h0 = (uint32_t)((prev - kmin) >> sh) + 1;
+  }
+  for (uint32_t hh = h0; hh <= h; hh++) bkt[hh] = i;
+  if (i == n - 1) bkt[(uint32_t)((kmax - kmin) >> sh) + 1] = n;
 }
 
 // Join in sorted order: gather each node's cause id and kind, find the cause
@@ -1105,13 +1185,128 @@ __global__ __launch_bounds__(NT) void k_tree(
     for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
 }
 
+// --- tree for one giant document (all tiles in parallel) -------------------------
+// k_tree sweeps a document in order in one workgroup, which is hopeless for a
+// single list of 10^8+ nodes (BASELINE config 5).  Same tree, three passes
+// over all ranks at once:
+//   k_geff   effective parent and class per rank -> group key (e << 1 | class);
+//   (the keys are radix sorted, stable in rank: siblings become adjacent)
+//   k_gsib   next sibling of every node from its sorted neighbour, last child of
+//            every group (-> first children), the oldest special's next sibling
+//            = its parent's newest non-special (binary search in the keys);
+//   k_gthr   per tile: threads by pointer jumping inside the tile; a chain that
+//            leaves the tile is left to the walk (LINK_PEND: thr[x] is chased).
+__global__ __launch_bounds__(256) void k_geff(const uint32_t *__restrict__ par,
+                                              const uint8_t *__restrict__ skind, uint32_t n,
+                                              uint32_t root_key, uint32_t *__restrict__ gk) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (r == 0) {
+    gk[0] = root_key;  // the root has no group: it sorts last
+    return;
+  }
+  const bool sp = is_special(skind[r]);
+  uint32_t c = par[r];
+  c = c < r ? c : 0u;  // clamps keep out-of-domain documents in bounds
+  if (!sp)
+    while (c != 0 && is_special(skind[c])) {
+      const uint32_t pc = par[c];
+      c = pc < c ? pc : 0u;
+    }
+  gk[r] = (c << 1) | (sp ? 0u : 1u);
+}
+
+__global__ __launch_bounds__(256) void k_gsib(const uint32_t *__restrict__ key,
+                                              const uint32_t *__restrict__ val, uint32_t n,
+                                              uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+                                              uint32_t *__restrict__ fcN) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t g = key[i];
+  if (g >= 2 * n) return;  // the root
+  const uint32_t r = val[i], e = g >> 1;
+  const bool first = i == 0 || key[i - 1] != g, last = i + 1 == n || key[i + 1] != g;
+  if (last) ((g & 1) ? fcN : fcS)[e] = r;
+  uint32_t ns = first ? 0u : val[i - 1];
+  if (first && !(g & 1)) {  // oldest special: the newest non-special of e follows its group
+    const uint32_t want = g | 1u;
+    uint32_t lo = i, hi = n;  // first position with key > want
+    while (lo < hi) {
+      const uint32_t m = lo + ((hi - lo) >> 1);
+      if (key[m] <= want) lo = m + 1; else hi = m;
+    }
+    if (lo > 0 && key[lo - 1] == want) ns = val[lo - 1];
+  }
+  nsc[r] = ns ? ns : (NSC_UP | e);
+}
+
+template <int NT, int TT>
+__global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
+                                             const uint32_t *__restrict__ fcS,
+                                             const uint32_t *__restrict__ fcN,
+                                             const uint8_t *__restrict__ skind, uint32_t n,
+                                             uint32_t log2k, uint32_t *__restrict__ thr,
+                                             uint32_t *__restrict__ link) {
+  constexpr uint32_t IT = TT / NT, RES = 0x80000000u, OUT = 0x40000000u;
+  __shared__ uint32_t T[TT];
+  const uint32_t r0 = blockIdx.x * TT, tid = threadIdx.x, len = min((uint32_t)TT, n - r0);
+  uint32_t fcr[IT], flg[IT];
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = k * NT + tid, r = r0 + j;
+    fcr[k] = flg[k] = 0;
+    if (j >= len) continue;
+    const uint32_t fs = fcS[r], fn = fcN[r], ns = nsc[r];
+    const bool sp = is_special(skind[r]);
+    fcr[k] = fs ? fs : fn;
+    uint32_t tv;
+    if (r == 0) tv = RES | SUCC_END;
+    else if (!(ns & NSC_UP)) tv = RES | ns;
+    else {
+      const uint32_t e = ns & ~NSC_UP;
+      tv = e >= r0 ? (e < r ? e - r0 : (RES | SUCC_END)) : (OUT | e);
+    }
+    T[j] = tv;
+    const bool vis = !sp && r != 0 && !(fs && is_hide(skind[fs]));
+    const bool split = r == split_node(0, r >> log2k, log2k, n);
+    flg[k] = (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
+  }
+  __syncthreads();
+  for (;;) {  // pointer jumping inside the tile (pointers go to lower ranks)
+    bool open = false;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid;
+      if (j < len) {
+        const uint32_t a = T[j];
+        if (!(a & (RES | OUT))) {
+          const uint32_t b = T[a];
+          T[j] = b;
+          open |= !(b & (RES | OUT));
+        }
+      }
+    }
+    if (!__syncthreads_or(open)) break;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = k * NT + tid, r = r0 + j;
+    if (j >= len) continue;
+    const uint32_t a = T[j];
+    const uint32_t th = (a & RES) ? (a & ~RES) : (LINK_PEND | (a & ~OUT));
+    thr[r] = th;
+    link[r] = (fcr[k] ? fcr[k] : th) | flg[k];
+  }
+}
+
 // Walker w of document d starts at the splitter node of rank block w and
 // follows preorder successors up to the next splitter (or the end).  The nodes
 // it passes (rank | renders << 31) are appended to its sublist's slot of `cap`
 // entries; a full slot continues as a new sublist (id >= W, from a per-document
 // counter), so slots are written sequentially by one lane, no per-node scatter.
 __global__ __launch_bounds__(1024) void k_walk(
-    const uint32_t *__restrict__ link, const uint32_t *__restrict__ wblk_doc,
+    const uint32_t *__restrict__ link, const uint32_t *__restrict__ thr,
+    const uint32_t *__restrict__ wblk_doc,
     const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_log2cap,
     const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ doc_Wcap,
@@ -1136,7 +1331,13 @@ __global__ __launch_bounds__(1024) void k_walk(
     // (slots are 16-byte aligned: cap >= 4 and every slot start is a multiple)
     uint4 q = make_uint4(v | (L & LINK_VIS), 0u, 0u, 0u);
     for (uint32_t steps = 0;; steps++) {
-      const uint32_t u = L & LINK_IDX;
+      uint32_t u = L & LINK_IDX;
+      if (L & LINK_PEND)  // the successor is the thread of an ancestor: chase it
+        for (uint32_t hop = 0; hop <= n; hop++) {
+          const uint32_t tv = thr[base + (u < n ? u : 0u)];
+          u = tv & LINK_IDX;
+          if (!(tv & LINK_PEND) || u >= n) break;
+        }
       if (u >= n) {  // SUCC_END: the tour is over
         if (u != SUCC_END) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
@@ -1962,6 +2163,7 @@ struct cw_ctx {
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
+  uint32_t giant_min = 1u << 20;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
 };
 
 namespace {
@@ -2260,7 +2462,19 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scan", tag);
-    {
+    if (D == 1 && t.T > 2 * GSCAN_CHUNK) {
+      // one document of many tiles: chunked scan over all workgroups
+      const uint32_t nc = (t.T + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
+      uint32_t *cs = scratch_t<uint32_t>(c, "gscan_cs", (size_t)nc * nb);
+      uint32_t *tot = scratch_t<uint32_t>(c, "gscan_tot", nb);
+      if (!cs || !tot) return fail(c, "out of device memory (scan)");
+      Launch L(c, nm, (double)t.T * nb * 12);
+      hipLaunchKernelGGL(k_gscan_colsum, dim3(nc), dim3(1024), 0, c->stream, hist, t.T, nb, cs);
+      hipLaunchKernelGGL(k_gscan_chunks, dim3((nb + 1023) / 1024), dim3(1024), 0, c->stream, cs, nc,
+                         nb, tot);
+      hipLaunchKernelGGL(k_gscan_bins, dim3(1), dim3(1024), 0, c->stream, tot, nb, 0u);
+      hipLaunchKernelGGL(k_gscan_apply, dim3(nc), dim3(1024), 0, c->stream, hist, t.T, nb, cs, tot);
+    } else {
       Launch L(c, nm, (double)t.T * nb * 8);
       hipLaunchKernelGGL(k_radix_scan, dim3(D), dim3(1024), 0, c->stream, hist,
                          dev_tab(c, "t_tile_first"), dev_tab(c, "t_doc_off"), dbits);
@@ -2426,8 +2640,12 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (!bkt) return fail(c, "out of device memory (bucket index)");
     {
       Launch L(c, "index", (double)N * 8 + (double)t.Btot * 4);
-      hipLaunchKernelGGL(k_index, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
-                         dev_tab(c, "t_bkt_off"), bkt, out->status);
+      if (D == 1 && N > (1u << 20))  // one large document: a thread per id
+        hipLaunchKernelGGL(k_index_flat, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, bkt,
+                           out->status);
+      else
+        hipLaunchKernelGGL(k_index, dim3((uint32_t)D), B256, 0, c->stream, skey, doc_off,
+                           dev_tab(c, "t_bkt_off"), bkt, out->status);
     }
     if (check_launch(c, "index")) return -1;
     {
@@ -2440,7 +2658,37 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }  // general front end
 
     // 3-5. effective parents, sibling order, links
-    {
+    const bool giant = D == 1 && N >= c->giant_min;
+    if (giant) {
+      const uint32_t gbits = ceil_log2(2ull * N + 2), root_key = (1u << gbits) - 1;
+      uint32_t *gkA = scratch_t<uint32_t>(c, "g_keyA", N), *gkB = scratch_t<uint32_t>(c, "g_keyB", N);
+      uint32_t *gvA = scratch_t<uint32_t>(c, "g_valA", N), *gvB = scratch_t<uint32_t>(c, "g_valB", N);
+      uint32_t *gk = scratch_t<uint32_t>(c, "g_key", N);
+      if (!gkA || !gkB || !gvA || !gvB || !gk) return fail(c, "out of device memory (giant tree)");
+      const dim3 GN((N + 255) / 256);
+      {
+        Launch L(c, "geff", (double)N * (4 + 1 + 4));
+        hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk);
+      }
+      if (check_launch(c, "geff")) return -1;
+      uint32_t *gks, *gvs;
+      if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
+        return -1;
+      HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
+      {
+        Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
+        hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
+      }
+      if (check_launch(c, "gsib")) return -1;
+      {
+        Launch L(c, "gthr", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
+        hipLaunchKernelGGL((k_gthr<256, 1024>), dim3((N + 1023) / 1024), B256, 0, c->stream, nsc,
+                           fcS, fcN, skind, N, t.doc_log2k[0], thr, (uint32_t *)link);
+      }
+      if (check_launch(c, "gthr")) return -1;
+    }
+    if (!giant) {
       const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
       // special/hide bitmaps in LDS for documents up to 2^18 nodes
       const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
@@ -2469,7 +2717,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            dev_tab(c, "t_tile_first"));
     }
     if (check_launch(c, "tree")) return -1;
-    if (c->tree_prof) {
+    if (c->tree_prof && !giant) {
       std::vector<unsigned long long> h((size_t)D * 8);
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 64, hipMemcpyDeviceToHost));
@@ -2486,7 +2734,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     {
       Launch L(c, "walk", (double)N * (4 + 4));
       hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream,
-                         (const uint32_t *)link,
+                         (const uint32_t *)link, thr,
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
                          dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
                          (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
@@ -2552,7 +2800,7 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   for (uint64_t d = 0; d < D; d++) {
     if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
     if (bt->doc_offsets[d + 1] - bt->doc_offsets[d] >= LINK_IDX)
-      return fail(c, "document %llu too large (limit 2^30-1 nodes)", (unsigned long long)d);
+      return fail(c, "document %llu too large (limit 2^29-1 nodes)", (unsigned long long)d);
   }
   if (!res->weave_perm || !res->visible_count || !res->status)
     return fail(c, "weave_perm, visible_count and status are required");
@@ -3131,6 +3379,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->pack_sort = knob("CW_PACK_SORT", 1);
+  c->giant_min = knob("CW_GIANT_MIN", 1u << 20);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

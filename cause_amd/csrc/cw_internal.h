@@ -25,11 +25,14 @@ constexpr uint32_t MAX_SUBLISTS = 16384;          // rank: 128 KiB of LDS
 constexpr uint32_t CHAIN = 64;                     // rank: sublists per LDS chain head
 constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter block
 
-// link word (u32): low 30 bits = the node's preorder successor (SUCC_END for the
-// last node), bit 31 = the node renders, bit 30 = the node is a splitter.
+// link word (u32): low 29 bits = the node's preorder successor (SUCC_END for the
+// last node), bit 31 = the node renders, bit 30 = the node is a splitter, bit
+// 29 = the successor is thr[low bits] (a thread the giant-document tree left
+// to the walk: thr entries are a successor or again LINK_PEND | node).
 constexpr uint32_t LINK_VIS = 0x80000000u;
 constexpr uint32_t LINK_SPLIT = 0x40000000u;
-constexpr uint32_t LINK_IDX = 0x3FFFFFFFu;        // documents < 2^30 nodes
+constexpr uint32_t LINK_PEND = 0x20000000u;
+constexpr uint32_t LINK_IDX = 0x1FFFFFFFu;        // documents < 2^29 nodes
 constexpr uint32_t EMIT_STAGE = 4096;          // weave positions staged per emit block
 constexpr uint32_t NSC_UP = 0x80000000u;         // nsc: no next sibling, low bits = eff parent
 constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder

@@ -127,7 +127,7 @@ typedef struct {
 } cw_list_result;
 
 /* Full reweave of a batch of independent CausalLists (N = doc_offsets[n_docs]
- * < 2^32, each document < 2^31 nodes).  `memspace` says where id_key /
+ * < 2^32, each document < 2^29 nodes).  `memspace` says where id_key /
  * cause_key / kind and every result array live (doc_offsets is always host). */
 int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
                    int memspace);

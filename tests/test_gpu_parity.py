@@ -285,3 +285,65 @@ def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
             f"{np.array_equal(g, lk)}, oracle==linked {np.array_equal(o, lk)}, gpu is a perm "
             f"{len(np.unique(g)) == e - b}")
     assert np.array_equal(res.visible(), vis)
+
+
+# ------------------------------------------------- one giant document (config 5)
+@pytest.fixture(scope="module")
+def giant_weaver():
+    """A context that sends every one-document batch through the giant-document
+    tree (k_geff / radix sort / k_gsib / k_gthr + the walk's thread chase)."""
+    import os
+
+    old = os.environ.get("CW_GIANT_MIN")
+    os.environ["CW_GIANT_MIN"] = "0"
+    try:
+        w = abi.Weaver(0)
+    finally:
+        if old is None:
+            os.environ.pop("CW_GIANT_MIN", None)
+        else:
+            os.environ["CW_GIANT_MIN"] = old
+    with w:
+        yield w
+
+
+def test_giant_path_small_documents(giant_weaver):
+    """The reference's edge cases, random and stress histories, one per call."""
+    rng = random.Random(31)
+    docs = [[R.ROOT_NODE] + case for case in G.EDGE_CASES]
+    for steps in (1, 9, 60, 300):
+        for _ in range(3):
+            nodes, _ = G.random_history(rng, steps)
+            docs.append([R.ROOT_NODE] + nodes)
+    for steps, tx in ((200, 0.0), (2000, 0.0), (1500, 0.3)):
+        docs.append(G.stress_history(rng, steps, tx_chain=tx))
+    docs.append([R.ROOT_NODE])
+    for d in docs:
+        rng.shuffle(d)
+        b = pack.pack_lists([d])
+        check_batch(giant_weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+def test_giant_path_shapes(giant_weaver):
+    """Config 1, a deep typing chain (threads chased across every tile) and a
+    root with 30k children."""
+    off, idk, ck, kd = gen.generate(gen.CONFIG1, 0, 1)
+    check_batch(giant_weaver, off, idk, ck, kd, gen.CONFIG1.layout(), method=oracle.METHOD_LINKED)
+    spec = dataclasses.replace(gen.CONFIG1, nodes_per_doc=200_000, n_sites=1, p_chain=1.0)
+    off, idk, ck, kd = gen.generate(spec, 0, 1)
+    check_batch(giant_weaver, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_LINKED)
+    s = "aaaaaaaaaaaaa"
+    doc = [R.ROOT_NODE] + [((t, s, 0), R.ROOT_ID, "c") for t in range(1, 30_001)]
+    random.Random(3).shuffle(doc)
+    b = pack.pack_lists([doc])
+    check_batch(giant_weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout,
+                method=oracle.METHOD_LINKED)
+
+
+def test_giant_document_default_threshold(weaver):
+    """A 3M-node config-2-shaped list: over the default threshold, so the giant
+    tree, the chunked radix scan and the flat bucket index all run."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3_000_000)
+    off, idk, ck, kd = gen.generate(spec, 0, 1)
+    lay = spec.layout()
+    check_batch(weaver, off, idk, ck, kd, lay, method=oracle.METHOD_EFF, yarns=False)
