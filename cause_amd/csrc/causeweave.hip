@@ -1458,6 +1458,101 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
   }
 }
 
+// --- multi-level sublist ranking (one giant document) ----------------------------
+// The sublists form one linked list.  A level: every K-th element below
+// Wsplit starts a walker that follows the links to the next such element,
+// recording for each element it passes its walker, and the prefix sums (a:
+// nodes, b: sublists) before it inside the walk; per walker the sums and the
+// next walker.  Levels repeat until <= 8192 walkers remain, which one
+// workgroup ranks in LDS (k_sup_rank); k_lvl_apply hands the bases back down.
+__global__ __launch_bounds__(256) void k_lvl_walk(const uint32_t *__restrict__ ca,
+                                                  const uint32_t *__restrict__ cb,
+                                                  const uint32_t *__restrict__ nxt, uint32_t Wsplit,
+                                                  uint32_t Wall, uint32_t K, uint32_t S,
+                                                  uint32_t *__restrict__ sup, uint32_t *__restrict__ pa,
+                                                  uint32_t *__restrict__ pb, uint32_t *__restrict__ sa,
+                                                  uint32_t *__restrict__ sb,
+                                                  uint32_t *__restrict__ snext,
+                                                  uint32_t *__restrict__ status) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= S) return;
+  uint32_t x = q * K, acc = 0, cnt = 0, nq = NX_END;
+  for (uint32_t steps = 0; steps <= Wall; steps++) {
+    sup[x] = q;
+    pa[x] = acc;
+    pb[x] = cnt;
+    acc += ca[x];
+    cnt += cb ? cb[x] : 1u;
+    const uint32_t nx = nxt[x];
+    if (nx == NX_END) break;
+    if (nx >= Wall) {
+      atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
+      break;
+    }
+    if (nx < Wsplit && nx % K == 0) {
+      nq = nx / K;
+      break;
+    }
+    x = nx;
+  }
+  sa[q] = acc;
+  sb[q] = cnt;
+  snext[q] = nq;
+}
+
+// Bases of a level's elements from their walker's bases.  order != nullptr
+// (the sublist level): sbase = node base, order[sublist base] = element.
+__global__ __launch_bounds__(256) void k_lvl_apply(const uint32_t *__restrict__ sup,
+                                                   const uint32_t *__restrict__ pa,
+                                                   const uint32_t *__restrict__ pb,
+                                                   const uint32_t *__restrict__ ba,
+                                                   const uint32_t *__restrict__ bb, uint32_t Wall,
+                                                   uint32_t *__restrict__ oa, uint32_t *__restrict__ ob,
+                                                   uint32_t *__restrict__ order) {
+  const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x >= Wall) return;
+  const uint32_t q = sup[x], va = ba[q] + pa[x], vb = bb[q] + pb[x];
+  oa[x] = va;
+  if (order) {
+    if (vb < Wall) order[vb] = x;
+  } else {
+    ob[x] = vb;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ scnt,
+                                                   const uint32_t *__restrict__ ssub,
+                                                   const uint32_t *__restrict__ snext, uint32_t S2,
+                                                   uint32_t n, uint32_t Weff, uint32_t *__restrict__ nb,
+                                                   uint32_t *__restrict__ tb,
+                                                   uint32_t *__restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // next, count, sublists
+  uint32_t *nx = sm, *cn = sm + S2, *sb = sm + 2 * S2;
+  for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
+    nx[i] = snext[i];
+    cn[i] = scnt[i];
+    sb[i] = ssub[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the super list in order: <= 8192 steps in LDS
+    uint32_t q = 0, run = 0, trun = 0, steps = 0;
+    while (q != NX_END && q < S2 && steps++ <= S2) {
+      const uint32_t a = run, b = trun;
+      run += cn[q];
+      trun += sb[q];
+      cn[q] = a;
+      sb[q] = b;
+      q = nx[q];
+    }
+    if (run != n || trun != Weff || q != NX_END) atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
+    nb[i] = cn[i];
+    tb[i] = sb[i];
+  }
+}
+
 // --- emit: sublist slots -> weave order ------------------------------------------
 // Entry k of sublist x is the node at weave position sbase[x] + k.  One lane
 // per sublist (its slot is contiguous); a block covers 256 consecutive
@@ -1564,6 +1659,11 @@ __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ v
     for (uint32_t g = g0; g < N; g++) m |= (uint32_t)(vis8[g] & 1u) << (g - g0);
   }
   bits[w] = m;
+}
+
+__global__ void k_max_ts1(const uint64_t *__restrict__ skey, uint32_t n, uint32_t ts_shift,
+                          uint64_t *__restrict__ max_ts) {
+  if (threadIdx.x == 0) max_ts[0] = n ? skey[n - 1] >> ts_shift : 0ull;
 }
 
 __global__ void k_or_reduce(const uint64_t *__restrict__ keys, uint32_t N,
@@ -2154,6 +2254,7 @@ struct cw_ctx {
     uint64_t slots = 0;
   } tab;
   bool tab_on_device = false;
+  bool last_giant = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
   uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
@@ -2272,7 +2373,7 @@ uint32_t ceil_log2(uint64_t x) {
 }
 
 // Host tables: tiles (sort/pass grids), splitter blocks and walker blocks.
-void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
+void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
   auto &t = c->tab;
   t.doc_off.resize(D + 1);
   t.tile_start.clear();
@@ -2314,7 +2415,8 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
       return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
     };
-    while (subl() > MAX_SUBLISTS) {
+    // (a giant document ranks its sublists in two levels: no LDS limit here)
+    while (!giant && subl() > MAX_SUBLISTS) {
       if (log2k < log2cap) log2k++;
       else log2cap++;
     }
@@ -2517,14 +2619,21 @@ int find_key_bits(cw_ctx *c, const uint64_t *keys, uint32_t N, uint32_t *bits) {
 }
 
 // Host tables for a document layout, rebuilt only when the layout changes.
+// A one-document batch this large takes the giant-document path.
+bool is_giant(const cw_ctx *c, uint64_t D, const uint64_t *off) {
+  return D == 1 && off[1] >= c->giant_min;
+}
+
 int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
-  const bool same = c->tab_on_device && c->last_off.size() == D + 1 &&
+  const bool giant = is_giant(c, D, off);
+  const bool same = c->tab_on_device && c->last_off.size() == D + 1 && c->last_giant == giant &&
                     memcmp(c->last_off.data(), off, (D + 1) * 8) == 0;
   if (same) return 0;
   c->tab_on_device = false;
-  build_tables(c, D, off);
+  build_tables(c, D, off, giant);
   if (upload_tables(c)) return -1;
   c->last_off.assign(off, off + D + 1);
+  c->last_giant = giant;
   c->tab_on_device = true;
   return 0;
 }
@@ -2658,7 +2767,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }  // general front end
 
     // 3-5. effective parents, sibling order, links
-    const bool giant = D == 1 && N >= c->giant_min;
+    const bool giant = is_giant(c, D, bt->doc_offsets);
     if (giant) {
       const uint32_t gbits = ceil_log2(2ull * N + 2), root_key = (1u << gbits) - 1;
       uint32_t *gkA = scratch_t<uint32_t>(c, "g_keyA", N), *gkB = scratch_t<uint32_t>(c, "g_keyB", N);
@@ -2743,7 +2852,50 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (check_launch(c, "walk")) return -1;
 
     // 7. rank sublists (+ max lamport-ts per document)
-    {
+    if (giant) {
+      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
+      // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
+      const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
+      uint32_t K3 = 1;
+      while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
+      const uint32_t S3 = (S2 + K3 - 1) / K3;
+      const bool three = K3 > 1;
+      uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
+      uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
+      uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
+      if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
+      uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
+      uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
+               *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
+      {
+        Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
+        hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
+                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
+        if (three) {
+          hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
+                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
+          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
+                             sn3, S3, N, Weff, nb3, tb3, out->status);
+          hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
+                             nb3, tb3, S2, ba2, bb2, nullptr);
+        } else {
+          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
+                             sn2, S2, N, Weff, ba2, bb2, out->status);
+        }
+        hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
+                           ba2, bb2, Weff, sbase, nullptr, order);
+      }
+      if (check_launch(c, "rank")) return -1;
+      if (out->max_ts && !front_done) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
+        if (!skey) return fail(c, "giant path without sorted ids");
+        hipLaunchKernelGGL(k_max_ts1, dim3(1), dim3(64), 0, c->stream, skey, N, bt->ts_shift,
+                           out->max_ts);
+        if (check_launch(c, "max_ts")) return -1;
+      }
+    } else {
       Launch L(c, "rank", (double)t.Wtot * 12);
       hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
                          wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, bt->ts_shift, sbase,
