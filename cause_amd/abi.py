@@ -67,6 +67,10 @@ class CwWeftResult(C.Structure):
                 ("weave", CwListResult)]
 
 
+class CwRankedList(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("par", C.c_void_p), ("kind", C.c_void_p), ("val", C.c_void_p)]
+
+
 class CwKernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double),
                 ("bytes_alg", C.c_double)]
@@ -117,6 +121,16 @@ def lib():
         L.cw_weft_lists.argtypes = [C.c_void_p, C.POINTER(CwWeftBatch), C.POINTER(CwWeftResult),
                                     C.c_int]
         L.cw_weft_lists.restype = C.c_int
+        P, U64, U32 = C.c_void_p, C.c_uint64, C.c_uint32
+        L.cw_sort_keys.argtypes = [P, P, U64, U32, P, P]
+        L.cw_lookup_keys.argtypes = [P, P, U64, P, U64, U32, P]
+        L.cw_partition_keys.argtypes = [P, P, U64, P, U32, P, P]
+        L.cw_gather.argtypes = [P, P, P, U64, U32, P]
+        L.cw_scatter32.argtypes = [P, P, P, U64, P]
+        L.cw_weave_ranked.argtypes = [P, C.POINTER(CwRankedList), C.POINTER(CwListResult)]
+        for f in ("cw_sort_keys", "cw_lookup_keys", "cw_partition_keys", "cw_gather", "cw_scatter32",
+                  "cw_weave_ranked"):
+            getattr(L, f).restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -266,6 +280,35 @@ class Weaver:
                          g("status"), g("yarn_perm"))
         self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
                     "cw_weave_lists")
+
+    # --- building blocks of the distributed giant list (device pointers) ---------
+    def sort_keys_device(self, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr):
+        self._check(self._L.cw_sort_keys(self._h, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr),
+                    "cw_sort_keys")
+
+    def lookup_keys_device(self, sorted_ptr, n, q_ptr, m, base, out_ptr):
+        self._check(self._L.cw_lookup_keys(self._h, sorted_ptr, n, q_ptr, m, base, out_ptr),
+                    "cw_lookup_keys")
+
+    def partition_keys_device(self, keys_ptr, m, split_ptr, n_split, perm_ptr) -> np.ndarray:
+        counts = np.zeros(n_split + 1, np.uint64)
+        self._check(self._L.cw_partition_keys(self._h, keys_ptr, m, split_ptr, n_split, perm_ptr,
+                                              counts.ctypes.data), "cw_partition_keys")
+        return counts
+
+    def gather_device(self, src_ptr, idx_ptr, m, elem_size, dst_ptr):
+        self._check(self._L.cw_gather(self._h, src_ptr, idx_ptr, m, elem_size, dst_ptr), "cw_gather")
+
+    def scatter32_device(self, src_ptr, idx_ptr, m, dst_ptr):
+        self._check(self._L.cw_scatter32(self._h, src_ptr, idx_ptr, m, dst_ptr), "cw_scatter32")
+
+    def weave_ranked_device(self, n, par_ptr, kind_ptr, val_ptr, out_ptrs):
+        """out_ptrs: weave_perm, visible_bits (or None), visible_count, status."""
+        lst = CwRankedList(n, par_ptr, kind_ptr, val_ptr)
+        g = lambda k: C.c_void_p(out_ptrs[k]) if out_ptrs.get(k) else None
+        r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), None, g("status"),
+                         None)
+        self._check(self._L.cw_weave_ranked(self._h, C.byref(lst), C.byref(r)), "cw_weave_ranked")
 
     def merge_lists(self, a, b, layout, yarns=True) -> MergeResult:
         """Host-memory call of cw_merge_lists.  a, b: (offsets, id_key, cause_key,

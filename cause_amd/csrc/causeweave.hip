@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(256) void k_gsib(const uint32_t *__restrict__ key,
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t g = key[i];
-  if (g >= 2 * n) return;  // the root
+  if ((uint64_t)g >= 2ull * n) return;  // the root
   const uint32_t r = val[i], e = g >> 1;
   const bool first = i == 0 || key[i - 1] != g, last = i + 1 == n || key[i + 1] != g;
   if (last) ((g & 1) ? fcN : fcS)[e] = r;
@@ -1246,9 +1246,12 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
                                              const uint32_t *__restrict__ fcN,
                                              const uint8_t *__restrict__ skind, uint32_t n,
                                              uint32_t log2k, uint32_t *__restrict__ thr,
-                                             uint32_t *__restrict__ link) {
-  constexpr uint32_t IT = TT / NT, RES = 0x80000000u, OUT = 0x40000000u;
-  __shared__ uint32_t T[TT];
+                                             uint64_t *__restrict__ link) {
+  // T: a pointer to a lower rank of the tile, RES | resolved thread, or OUT | an
+  // ancestor outside the tile (its thread is left to the walk)
+  constexpr uint32_t IT = TT / NT;
+  constexpr uint64_t RES = 1ull << 63, OUT = 1ull << 62;
+  __shared__ uint64_t T[TT];
   const uint32_t r0 = blockIdx.x * TT, tid = threadIdx.x, len = min((uint32_t)TT, n - r0);
   uint32_t fcr[IT], flg[IT];
 #pragma unroll
@@ -1259,12 +1262,12 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
     const uint32_t fs = fcS[r], fn = fcN[r], ns = nsc[r];
     const bool sp = is_special(skind[r]);
     fcr[k] = fs ? fs : fn;
-    uint32_t tv;
-    if (r == 0) tv = RES | SUCC_END;
+    uint64_t tv;
+    if (r == 0) tv = RES | SUCCW_END;
     else if (!(ns & NSC_UP)) tv = RES | ns;
     else {
       const uint32_t e = ns & ~NSC_UP;
-      tv = e >= r0 ? (e < r ? e - r0 : (RES | SUCC_END)) : (OUT | e);
+      tv = e >= r0 ? (e < r ? (uint64_t)(e - r0) : (RES | SUCCW_END)) : (OUT | e);
     }
     T[j] = tv;
     const bool vis = !sp && r != 0 && !(fs && is_hide(skind[fs]));
@@ -1278,9 +1281,9 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = k * NT + tid;
       if (j < len) {
-        const uint32_t a = T[j];
+        const uint64_t a = T[j];
         if (!(a & (RES | OUT))) {
-          const uint32_t b = T[a];
+          const uint64_t b = T[(uint32_t)a];
           T[j] = b;
           open |= !(b & (RES | OUT));
         }
@@ -1292,10 +1295,13 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
   for (uint32_t k = 0; k < IT; k++) {
     const uint32_t j = k * NT + tid, r = r0 + j;
     if (j >= len) continue;
-    const uint32_t a = T[j];
-    const uint32_t th = (a & RES) ? (a & ~RES) : (LINK_PEND | (a & ~OUT));
-    thr[r] = th;
-    link[r] = (fcr[k] ? fcr[k] : th) | flg[k];
+    const uint64_t a = T[j];
+    const bool res = (a & RES) != 0;
+    const uint32_t v = (uint32_t)a;  // resolved thread, or the ancestor to chase
+    thr[r] = res ? v : (THRW_PEND | v);
+    const uint32_t succ = fcr[k] ? fcr[k] : v;
+    const uint32_t f = flg[k] | (!fcr[k] && !res ? LINK_PEND : 0u);
+    link[r] = (uint64_t)succ | ((uint64_t)f << 32);
   }
 }
 
@@ -1304,8 +1310,9 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
 // it passes (rank | renders << 31) are appended to its sublist's slot of `cap`
 // entries; a full slot continues as a new sublist (id >= W, from a per-document
 // counter), so slots are written sequentially by one lane, no per-node scatter.
+template <bool WIDE>
 __global__ __launch_bounds__(1024) void k_walk(
-    const uint32_t *__restrict__ link, const uint32_t *__restrict__ thr,
+    const void *__restrict__ linkp, const uint32_t *__restrict__ thr,
     const uint32_t *__restrict__ wblk_doc,
     const uint32_t *__restrict__ wblk_w0, const uint32_t *__restrict__ doc_off,
     const uint32_t *__restrict__ doc_log2k, const uint32_t *__restrict__ doc_log2cap,
@@ -1321,28 +1328,50 @@ __global__ __launch_bounds__(1024) void k_walk(
   const uint32_t log2cap = doc_log2cap[d], cap = 1u << log2cap;
   const uint32_t f = walk_first[d];
   uint32_t *const sl = slots + slot_first[d];
+  // link word of node x: successor index and LINK_* flags (narrow: one u32;
+  // wide: u64 = successor | flags << 32)
+  constexpr uint32_t END = WIDE ? SUCCW_END : SUCC_END;
+  auto load = [&](uint32_t x, uint32_t &succ) -> uint32_t {
+    if (WIDE) {
+      const uint64_t L = static_cast<const uint64_t *>(linkp)[base + x];
+      succ = (uint32_t)L;
+      return (uint32_t)(L >> 32);
+    }
+    const uint32_t L = static_cast<const uint32_t *>(linkp)[base + x];
+    succ = L & LINK_IDX;
+    return L & ~LINK_IDX;
+  };
   if (threadIdx.x == 0) next_walker = w0 + blockDim.x;
   __syncthreads();
   for (uint32_t lw = w0 + threadIdx.x; lw < w1; lw = atomicAdd(&next_walker, 1u)) {
     const uint32_t v = split_node(d, lw, log2k, n);
-    uint32_t L = link[base + v];
+    uint32_t sv;
+    uint32_t L = load(v, sv);
     uint32_t x = lw, cnt = 1, nextsub = NX_END;
     // entries are buffered four at a time and written as one 16-byte store
     // (slots are 16-byte aligned: cap >= 4 and every slot start is a multiple)
     uint4 q = make_uint4(v | (L & LINK_VIS), 0u, 0u, 0u);
     for (uint32_t steps = 0;; steps++) {
-      uint32_t u = L & LINK_IDX;
+      uint32_t u = sv;
       if (L & LINK_PEND)  // the successor is the thread of an ancestor: chase it
         for (uint32_t hop = 0; hop <= n; hop++) {
           const uint32_t tv = thr[base + (u < n ? u : 0u)];
-          u = tv & LINK_IDX;
-          if (!(tv & LINK_PEND) || u >= n) break;
+          bool pend;
+          if (WIDE) {
+            u = tv & ~THRW_PEND;
+            pend = (tv & THRW_PEND) != 0;
+          } else {
+            u = tv & LINK_IDX;
+            pend = (tv & LINK_PEND) != 0;
+          }
+          if (!pend || u >= n) break;
         }
-      if (u >= n) {  // SUCC_END: the tour is over
-        if (u != SUCC_END) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+      if (u >= n) {  // the end marker: the tour is over
+        if (u != END) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
       }
-      const uint32_t Lu = link[base + u];
+      uint32_t su;
+      const uint32_t Lu = load(u, su);
       if (Lu & LINK_SPLIT) {
         nextsub = u >> log2k;
         break;
@@ -1369,6 +1398,7 @@ __global__ __launch_bounds__(1024) void k_walk(
       if ((cnt & 3) == 0)
         *reinterpret_cast<uint4 *>(sl + ((size_t)x << log2cap) + cnt - 4) = q;
       L = Lu;
+      sv = su;
       if (steps > n) {
         atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
@@ -1611,13 +1641,13 @@ __global__ __launch_bounds__(256) void k_emit(
     for (uint32_t u = 0; u < 4; u++) {
       const uint32_t k = k0 + u;
       if (k >= cnt) break;
-      const uint32_t r = e4[u] & LINK_IDX;
+      const uint32_t r = e4[u] & SLOT_IDX;
       if (r >= n) {
         bad = true;
         continue;
       }
       const uint32_t v = e4[u] >> 31;
-      const uint32_t pv = sval[base + r];
+      const uint32_t pv = sval ? sval[base + r] : r;
       if (staged) {
         stage_p[off + k] = pv;
         stage_v[off + k] = (uint8_t)v;
@@ -2262,6 +2292,7 @@ struct cw_ctx {
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
+  uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 20;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
@@ -2405,8 +2436,10 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     for (uint32_t s = 0; s < n; s += TILE) {
       t.tile_start.push_back(b + s);
       t.tile_doc.push_back((uint32_t)d);
-      t.woff_base.push_back(wofft);  // rank-window table of this tile: ntile + 1 entries
-      wofft += ntile + 1;
+      // rank-window table of this tile: ntile + 1 entries (front end only,
+      // which takes documents of <= 64 tiles)
+      t.woff_base.push_back(wofft);
+      if (ntile <= 64) wofft += ntile + 1;
     }
     // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
@@ -2621,11 +2654,11 @@ int find_key_bits(cw_ctx *c, const uint64_t *keys, uint32_t N, uint32_t *bits) {
 // Host tables for a document layout, rebuilt only when the layout changes.
 // A one-document batch this large takes the giant-document path.
 bool is_giant(const cw_ctx *c, uint64_t D, const uint64_t *off) {
-  return D == 1 && off[1] >= c->giant_min;
+  return D == 1 && (off[1] >= c->giant_min || off[1] >= LINK_IDX);
 }
 
-int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
-  const bool giant = is_giant(c, D, off);
+int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool force_giant = false) {
+  const bool giant = force_giant || is_giant(c, D, off);
   const bool same = c->tab_on_device && c->last_off.size() == D + 1 && c->last_giant == giant &&
                     memcmp(c->last_off.data(), off, (D + 1) * 8) == 0;
   if (same) return 0;
@@ -2635,6 +2668,195 @@ int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off) {
   c->last_off.assign(off, off + D + 1);
   c->last_giant = giant;
   c->tab_on_device = true;
+  return 0;
+}
+
+// Steps 3-9 of the list weave from the rank-ordered arrays: par (cause rank),
+// skind, sval (the value emitted for each rank; nullptr = the rank itself).
+// skey != nullptr: ::lamport-ts from the largest sorted id (otherwise the
+// front end wrote it).  kbm: the front end's special/hide bitmaps or nullptr.
+int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *par,
+               const uint8_t *skind, const uint32_t *sval, const uint32_t *kbm,
+               const uint64_t *skey, uint32_t ts_shift, cw_list_result *out) {
+  auto &t = c->tab;
+  const dim3 B256(256);
+  uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
+  uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
+  uint64_t *link = scratch_t<uint64_t>(c, "link", N);  // u32 or u64 links; room for the yarn sort
+  uint32_t *thr = scratch_t<uint32_t>(c, "thr", N);
+  uint32_t *slots = scratch_t<uint32_t>(c, "slots", t.slots);
+  uint32_t *dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
+  uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
+  uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
+  uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
+  uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
+  uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
+  if (!nsc || !fcS || !fcN || !link || !thr || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext ||
+      !sbase || !order)
+    return fail(c, "out of device memory (N=%u)", N);
+  uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
+  uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
+  // 3-5. effective parents, sibling order, links
+  if (giant) {
+    const uint32_t gbits = ceil_log2(2ull * N + 2);
+    const uint32_t root_key = gbits >= 32 ? 0xFFFFFFFFu : (1u << gbits) - 1;
+    uint32_t *gkA = scratch_t<uint32_t>(c, "g_keyA", N), *gkB = scratch_t<uint32_t>(c, "g_keyB", N);
+    uint32_t *gvA = scratch_t<uint32_t>(c, "g_valA", N), *gvB = scratch_t<uint32_t>(c, "g_valB", N);
+    uint32_t *gk = scratch_t<uint32_t>(c, "g_key", N);
+    if (!gkA || !gkB || !gvA || !gvB || !gk) return fail(c, "out of device memory (giant tree)");
+    const dim3 GN((N + 255) / 256);
+    {
+      Launch L(c, "geff", (double)N * (4 + 1 + 4));
+      hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk);
+    }
+    if (check_launch(c, "geff")) return -1;
+    uint32_t *gks, *gvs;
+    if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
+      return -1;
+    HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
+    {
+      Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
+      hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
+    }
+    if (check_launch(c, "gsib")) return -1;
+    {
+      Launch L(c, "gthr", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
+      hipLaunchKernelGGL((k_gthr<256, 1024>), dim3((N + 1023) / 1024), B256, 0, c->stream, nsc,
+                         fcS, fcN, skind, N, t.doc_log2k[0], thr, link);
+    }
+    if (check_launch(c, "gthr")) return -1;
+  }
+  if (!giant) {
+    const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
+    // special/hide bitmaps in LDS for documents up to 2^18 nodes
+    const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
+    // par, skind in; nsc, last-node tables, thr, link out; sweep 2 reads nsc
+    // and the tables back
+    unsigned long long *tprof = nullptr;
+    if (c->tree_prof) {
+      tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 8);
+      HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
+    }
+    Launch L(c, "tree", (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
+    if (c->tree_cfg == 2)
+      hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
+                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
+    else if (c->tree_cfg == 3)
+      hipLaunchKernelGGL((k_tree<256, 512>), dim3((uint32_t)D), dim3(256),
+                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
+    else if (c->tree_cfg == 1)
+      hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
+                         (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
+    else
+      hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
+                         (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
+  }
+  if (check_launch(c, "tree")) return -1;
+  if (c->tree_prof && !giant) {
+    std::vector<unsigned long long> h((size_t)D * 8);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 64, hipMemcpyDeviceToHost));
+    double acc[8] = {0};
+    for (uint64_t d = 0; d < D; d++)
+      for (int ph = 0; ph < 8; ph++) acc[ph] += (double)h[d * 8 + ph];
+    fprintf(stderr, "tree phases (memtime ticks per doc): bitmap %.0f climb %.0f sort %.0f prv %.0f "
+            "s2load %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
+            acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
+  }
+
+  // 6. walk: sublists of the preorder successor list
+  HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
+  {
+    Launch L(c, "walk", (double)N * (4 + 4));
+    hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
+                       c->walk_lds, c->stream, (const void *)link, thr,
+                       dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
+                       dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
+                       (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
+                       out->status, c->walk_span);
+  }
+  if (check_launch(c, "walk")) return -1;
+
+  // 7. rank sublists (+ max lamport-ts per document)
+  if (giant) {
+    if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
+    // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
+    const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
+    uint32_t K3 = 1;
+    while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
+    const uint32_t S3 = (S2 + K3 - 1) / K3;
+    const bool three = K3 > 1;
+    uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
+    uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
+    uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
+    if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
+    uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
+    uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
+             *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
+    {
+      Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
+      hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
+                         wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
+      if (three) {
+        hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
+                           S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
+        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
+                           sn3, S3, N, Weff, nb3, tb3, out->status);
+        hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
+                           nb3, tb3, S2, ba2, bb2, nullptr);
+      } else {
+        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
+                           sn2, S2, N, Weff, ba2, bb2, out->status);
+      }
+      hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
+                         ba2, bb2, Weff, sbase, nullptr, order);
+    }
+    if (check_launch(c, "rank")) return -1;
+    if (out->max_ts && skey) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
+      hipLaunchKernelGGL(k_max_ts1, dim3(1), dim3(64), 0, c->stream, skey, N, ts_shift,
+                         out->max_ts);
+      if (check_launch(c, "max_ts")) return -1;
+    }
+  } else {
+    Launch L(c, "rank", (double)t.Wtot * 12);
+    hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
+                       wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, ts_shift, sbase,
+                       order, skey ? out->max_ts : nullptr, out->status);
+  }
+  if (check_launch(c, "rank")) return -1;
+
+  // 8. emit
+  {
+    Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
+    hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
+                       (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
+                       dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
+                       dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
+                       out->visible_count, out->status);
+  }
+  if (check_launch(c, "emit")) return -1;
+
+  // 9. visibility bitmap
+  if (out->visible_bits) {
+    const uint32_t words = (N + 31) / 32;
+    Launch L(c, "packbits", (double)N + (double)words * 4);
+    hipLaunchKernelGGL(k_pack_bits, dim3((words + 255) / 256), B256, 0, c->stream, vis8, N,
+                       out->visible_bits);
+  }
+  if (check_launch(c, "packbits")) return -1;
+
   return 0;
 }
 
@@ -2658,24 +2880,14 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
   uint32_t *par = scratch_t<uint32_t>(c, "par", N);
   uint8_t *skind = scratch_t<uint8_t>(c, "skind", N);
+  // (the tail's node arrays; the yarn sort below reuses two of them)
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
-  uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
-  uint64_t *link = scratch_t<uint64_t>(c, "link", N);  // u32 links; u64 room for the yarn sort
-  uint32_t *thr = scratch_t<uint32_t>(c, "thr", N);
-  uint32_t *slots = scratch_t<uint32_t>(c, "slots", t.slots);
-  uint32_t *dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
-  uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
-  uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
-  uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
-  uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
-  uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
-  if (!skA || !skB || !svA || !svB || !par || !skind ||
-      !nsc || !fcS || !fcN || !link || !thr || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext || !sbase || !order)
+  uint64_t *link = scratch_t<uint64_t>(c, "link", N);
+  if (!skA || !skB || !svA || !svB || !par || !skind || !nsc || !link)
     return fail(c, "out of device memory (N=%u)", N);
 
   uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc");
-  uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
-  uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
+  uint32_t *doc_off = dev_tab(c, "t_doc_off");
   const dim3 GT(t.T);
   const dim3 TB(c->tb);
   if (!grid_ok(t.T, std::max(c->tb, SORT_THREADS)) || !grid_ok(t.Bw, c->walk_threads) ||
@@ -2766,162 +2978,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (check_launch(c, "join")) return -1;
     }  // general front end
 
-    // 3-5. effective parents, sibling order, links
-    const bool giant = is_giant(c, D, bt->doc_offsets);
-    if (giant) {
-      const uint32_t gbits = ceil_log2(2ull * N + 2), root_key = (1u << gbits) - 1;
-      uint32_t *gkA = scratch_t<uint32_t>(c, "g_keyA", N), *gkB = scratch_t<uint32_t>(c, "g_keyB", N);
-      uint32_t *gvA = scratch_t<uint32_t>(c, "g_valA", N), *gvB = scratch_t<uint32_t>(c, "g_valB", N);
-      uint32_t *gk = scratch_t<uint32_t>(c, "g_key", N);
-      if (!gkA || !gkB || !gvA || !gvB || !gk) return fail(c, "out of device memory (giant tree)");
-      const dim3 GN((N + 255) / 256);
-      {
-        Launch L(c, "geff", (double)N * (4 + 1 + 4));
-        hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk);
-      }
-      if (check_launch(c, "geff")) return -1;
-      uint32_t *gks, *gvs;
-      if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
-        return -1;
-      HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
-      HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
-      {
-        Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
-        hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
-      }
-      if (check_launch(c, "gsib")) return -1;
-      {
-        Launch L(c, "gthr", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
-        hipLaunchKernelGGL((k_gthr<256, 1024>), dim3((N + 1023) / 1024), B256, 0, c->stream, nsc,
-                           fcS, fcN, skind, N, t.doc_log2k[0], thr, (uint32_t *)link);
-      }
-      if (check_launch(c, "gthr")) return -1;
-    }
-    if (!giant) {
-      const uint32_t kbits = ceil_log2((uint64_t)t.nmax + 1) + 1;
-      // special/hide bitmaps in LDS for documents up to 2^18 nodes
-      const uint32_t bm_words = std::min<uint32_t>((t.nmax + 31) / 32, (1u << 18) / 32);
-      // par, skind in; nsc, last-node tables, thr, link out; sweep 2 reads nsc
-      // and the tables back
-      unsigned long long *tprof = nullptr;
-      if (c->tree_prof) {
-        tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 8);
-        HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
-      }
-      Launch L(c, "tree", (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
-      if (c->tree_cfg == 2)
-        hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
-                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                           dev_tab(c, "t_tile_first"));
-      else if (c->tree_cfg == 1)
-        hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
-                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                           dev_tab(c, "t_tile_first"));
-      else
-        hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
-                           (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                           kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                           dev_tab(c, "t_tile_first"));
-    }
-    if (check_launch(c, "tree")) return -1;
-    if (c->tree_prof && !giant) {
-      std::vector<unsigned long long> h((size_t)D * 8);
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 64, hipMemcpyDeviceToHost));
-      double acc[8] = {0};
-      for (uint64_t d = 0; d < D; d++)
-        for (int ph = 0; ph < 8; ph++) acc[ph] += (double)h[d * 8 + ph];
-      fprintf(stderr, "tree phases (memtime ticks per doc): bitmap %.0f climb %.0f sort %.0f prv %.0f "
-              "s2load %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
-              acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
-    }
-
-    // 6. walk: sublists of the preorder successor list
-    HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
-    {
-      Launch L(c, "walk", (double)N * (4 + 4));
-      hipLaunchKernelGGL(k_walk, dim3(t.Bw), dim3(c->walk_threads), c->walk_lds, c->stream,
-                         (const uint32_t *)link, thr,
-                         dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
-                         dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
-                         (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
-                         out->status, c->walk_span);
-    }
-    if (check_launch(c, "walk")) return -1;
-
-    // 7. rank sublists (+ max lamport-ts per document)
-    if (giant) {
-      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-      HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
-      // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
-      const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
-      uint32_t K3 = 1;
-      while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
-      const uint32_t S3 = (S2 + K3 - 1) / K3;
-      const bool three = K3 > 1;
-      uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
-      uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
-      uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
-      if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
-      uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
-      uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
-               *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
-      {
-        Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
-        hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
-                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
-        if (three) {
-          hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
-                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
-          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
-                             sn3, S3, N, Weff, nb3, tb3, out->status);
-          hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
-                             nb3, tb3, S2, ba2, bb2, nullptr);
-        } else {
-          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
-                             sn2, S2, N, Weff, ba2, bb2, out->status);
-        }
-        hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
-                           ba2, bb2, Weff, sbase, nullptr, order);
-      }
-      if (check_launch(c, "rank")) return -1;
-      if (out->max_ts && !front_done) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
-        if (!skey) return fail(c, "giant path without sorted ids");
-        hipLaunchKernelGGL(k_max_ts1, dim3(1), dim3(64), 0, c->stream, skey, N, bt->ts_shift,
-                           out->max_ts);
-        if (check_launch(c, "max_ts")) return -1;
-      }
-    } else {
-      Launch L(c, "rank", (double)t.Wtot * 12);
-      hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
-                         wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, bt->ts_shift, sbase,
-                         order, front_done ? nullptr : out->max_ts, out->status);
-    }
-    if (check_launch(c, "rank")) return -1;
-
-    // 8. emit
-    {
-      Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
-      hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
-                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
-                         dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
-                         dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
-                         out->visible_count, out->status);
-    }
-    if (check_launch(c, "emit")) return -1;
-
-    // 9. visibility bitmap
-    if (out->visible_bits) {
-      const uint32_t words = (N + 31) / 32;
-      Launch L(c, "packbits", (double)N + (double)words * 4);
-      hipLaunchKernelGGL(k_pack_bits, dim3((words + 255) / 256), B256, 0, c->stream, vis8, N,
-                         out->visible_bits);
-    }
-    if (check_launch(c, "packbits")) return -1;
+    // 3-9. tree, walk, rank, emit, visibility
+    if (weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
+                   front_done ? nullptr : skey, bt->ts_shift, out))
+      return -1;
 
     // 10. yarns: stable partition of the id order by site rank
     if (want_yarns) {
@@ -2949,10 +3009,14 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   if (bt->doc_offsets[0] != 0) return fail(c, "doc_offsets[0] must be 0");
   if (N64 >= 0xFFFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^32-1)",
                                         (unsigned long long)N64);
+  // a one-document batch takes the giant path (wide links) up to 2^31 - 2
+  // nodes; in a batch of several documents each stays below 2^29 - 1
   for (uint64_t d = 0; d < D; d++) {
     if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
-    if (bt->doc_offsets[d + 1] - bt->doc_offsets[d] >= LINK_IDX)
-      return fail(c, "document %llu too large (limit 2^29-1 nodes)", (unsigned long long)d);
+    const uint64_t nd = bt->doc_offsets[d + 1] - bt->doc_offsets[d];
+    if (D == 1 ? nd >= SUCCW_END : nd >= LINK_IDX)
+      return fail(c, "document %llu too large (limit %s nodes)", (unsigned long long)d,
+                  D == 1 ? "2^31-2" : "2^29-2 in a batch of several documents");
   }
   if (!res->weave_perm || !res->visible_count || !res->status)
     return fail(c, "weave_perm, visible_count and status are required");
@@ -3017,6 +3081,231 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
                                     c->stream));
     if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
   }
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
+// --- building blocks of the distributed giant list (cause_amd/giant.py) ---------
+// Gather dst[i] = src[idx[i]].
+template <typename E>
+__global__ __launch_bounds__(256) void k_gather(const E *__restrict__ src,
+                                                const uint32_t *__restrict__ idx, uint64_t m,
+                                                E *__restrict__ dst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) dst[i] = src[idx[i]];
+}
+
+// Bucket of each key among ns ascending splitters (number of splitters <= key)
+// as a sort key, and the bucket sizes.
+__global__ __launch_bounds__(256) void k_bucket(const uint64_t *__restrict__ keys, uint64_t m,
+                                                const uint64_t *__restrict__ split, uint32_t ns,
+                                                uint64_t *__restrict__ bucket,
+                                                unsigned long long *__restrict__ counts) {
+  __shared__ unsigned long long cnt[1024];
+  for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x) cnt[j] = 0;
+  __syncthreads();
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) {
+    const uint64_t x = keys[i];
+    uint32_t lo = 0, hi = ns;  // first splitter > x
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (split[mid] <= x) lo = mid + 1; else hi = mid;
+    }
+    bucket[i] = lo;
+    atomicAdd(&cnt[lo], 1ull);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x)
+    if (cnt[j]) atomicAdd(&counts[j], cnt[j]);
+}
+
+// Scatter dst[idx[i]] = src[i] (idx a permutation).
+__global__ __launch_bounds__(256) void k_scatter32(const uint32_t *__restrict__ src,
+                                                   const uint32_t *__restrict__ idx, uint64_t m,
+                                                   uint32_t *__restrict__ dst) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) dst[idx[i]] = src[i];
+}
+
+// Index of each query among n sorted unique keys (bucket index from
+// k_index_flat), or CW_NOT_FOUND.
+__global__ __launch_bounds__(256) void k_lookup(const uint64_t *__restrict__ skey, uint32_t n,
+                                                const uint32_t *__restrict__ bkt,
+                                                const uint64_t *__restrict__ q, uint64_t m,
+                                                uint32_t base, uint32_t *__restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t kmin = skey[0], kmax = skey[n - 1], x = q[i];
+  uint32_t r = CW_NOT_FOUND;
+  if (x >= kmin && x <= kmax) {
+    const uint32_t sh = bucket_shift(kmax - kmin, n), h = (uint32_t)((x - kmin) >> sh);
+    uint32_t lo = bkt[h], hi = bkt[h + 1];
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (skey[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    if (lo < n && skey[lo] == x) r = base + lo;
+  }
+  out[i] = r;
+}
+
+// Root at rank 0 only, causes older than their node (s/insert's checks,
+// shared.cljc:163-178) for a list handed over in rank order.
+__global__ __launch_bounds__(256) void k_ranked_check(const uint32_t *__restrict__ par,
+                                                      const uint8_t *__restrict__ kind, uint32_t n,
+                                                      uint32_t *__restrict__ status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t st = 0;
+  if (r < n) {
+    const bool root = (kind[r] & KIND_ROOT) != 0;
+    if ((r == 0) != root) st |= CW_STATUS_ROOT;
+    if (r > 0 && par[r] >= r) st |= par[r] == CW_NOT_FOUND ? CW_STATUS_ORPHAN : CW_STATUS_NON_LAMPORT;
+  }
+  if (__syncthreads_or(st != 0)) {
+    if (st) atomicOr(status, st);
+  }
+}
+
+int sort_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t n64, uint32_t key_bits,
+                   uint64_t *keys_out, uint32_t *idx_out) {
+  if (n64 == 0) return 0;
+  if (!keys || !keys_out || !idx_out) return fail(c, "null array");
+  if (n64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)n64);
+  const uint32_t n = (uint32_t)n64;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t off[2] = {0, n64};
+  if (ensure_tables(c, 1, off)) return -1;
+  if (key_bits == 0 && find_key_bits(c, keys, n, &key_bits)) return -1;
+  if (key_bits > 64) key_bits = 64;
+  uint64_t *kB = scratch_t<uint64_t>(c, "skB", n);
+  uint32_t *vB = scratch_t<uint32_t>(c, "svB", n);
+  if (!kB || !vB) return fail(c, "out of device memory (sort)");
+  uint64_t *ko;
+  uint32_t *vo;
+  if (radix_sort<uint64_t>(c, "ksort", keys, nullptr, keys_out, idx_out, kB, vB, key_bits, 0, n,
+                           &ko, &vo))
+    return -1;
+  if (ko != keys_out) {
+    HIPCHK(c, hipMemcpyAsync(keys_out, ko, (size_t)n * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(idx_out, vo, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  return 0;
+}
+
+int lookup_keys_impl(cw_ctx *c, const uint64_t *sorted, uint64_t n64, const uint64_t *q,
+                     uint64_t m, uint32_t base, uint32_t *out) {
+  if (m == 0) return 0;
+  if (!q || !out || (n64 && !sorted)) return fail(c, "null array");
+  if (n64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)n64);
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n64 == 0) {
+    HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)out, CW_NOT_FOUND, m, c->stream));
+    return 0;
+  }
+  const uint32_t n = (uint32_t)n64;
+  uint32_t *bkt = scratch_t<uint32_t>(c, "lk_bkt", (size_t)std::max(n >> 2, 1u) + 2);
+  uint32_t *st = scratch_t<uint32_t>(c, "lk_status", 1);
+  if (!bkt || !st) return fail(c, "out of device memory (lookup)");
+  {
+    Launch L(c, "lk_index", (double)n * 8);
+    hipLaunchKernelGGL(k_index_flat, dim3((n + 255) / 256), dim3(256), 0, c->stream, sorted, n, bkt, st);
+  }
+  if (check_launch(c, "lk_index")) return -1;
+  {
+    Launch L(c, "lookup", (double)m * (8 + 4 + 8 + 8));
+    hipLaunchKernelGGL(k_lookup, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, c->stream, sorted,
+                       n, bkt, q, m, base, out);
+  }
+  return check_launch(c, "lookup");
+}
+
+int gather_impl(cw_ctx *c, const void *src, const uint32_t *idx, uint64_t m, uint32_t es,
+                void *dst) {
+  if (m == 0) return 0;
+  if (!src || !idx || !dst) return fail(c, "null array");
+  HIPCHK(c, hipSetDevice(c->device));
+  const dim3 G((uint32_t)((m + 255) / 256)), B(256);
+  Launch L(c, "gather", (double)m * (4 + 2 * es));
+  if (es == 8)
+    hipLaunchKernelGGL(k_gather<uint64_t>, G, B, 0, c->stream, (const uint64_t *)src, idx, m, (uint64_t *)dst);
+  else if (es == 4)
+    hipLaunchKernelGGL(k_gather<uint32_t>, G, B, 0, c->stream, (const uint32_t *)src, idx, m, (uint32_t *)dst);
+  else if (es == 1)
+    hipLaunchKernelGGL(k_gather<uint8_t>, G, B, 0, c->stream, (const uint8_t *)src, idx, m, (uint8_t *)dst);
+  else
+    return fail(c, "gather: element size %u (1, 4 or 8)", es);
+  return check_launch(c, "gather");
+}
+
+int partition_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t m64, const uint64_t *split,
+                        uint32_t ns, uint32_t *perm, uint64_t *counts) {
+  if (ns > 1023) return fail(c, "partition: at most 1023 splitters");
+  if (!counts) return fail(c, "null counts");
+  if (m64 == 0) {
+    memset(counts, 0, (size_t)(ns + 1) * 8);
+    return 0;
+  }
+  if (!keys || !perm || (ns && !split)) return fail(c, "null array");
+  if (m64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)m64);
+  const uint32_t m = (uint32_t)m64;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t off[2] = {0, m64};
+  if (ensure_tables(c, 1, off)) return -1;
+  uint64_t *bk = scratch_t<uint64_t>(c, "pt_bucket", m), *kA = scratch_t<uint64_t>(c, "skA", m);
+  uint64_t *kB = scratch_t<uint64_t>(c, "skB", m);
+  uint32_t *vB = scratch_t<uint32_t>(c, "svB", m);
+  unsigned long long *dc = scratch_t<unsigned long long>(c, "pt_counts", ns + 1);
+  if (!bk || !kA || !kB || !vB || !dc) return fail(c, "out of device memory (partition)");
+  HIPCHK(c, hipMemsetAsync(dc, 0, (size_t)(ns + 1) * 8, c->stream));
+  {
+    Launch L(c, "bucket", (double)m * 16);
+    hipLaunchKernelGGL(k_bucket, dim3((m + 255) / 256), dim3(256), 0, c->stream, keys, m, split, ns, bk,
+                       dc);
+  }
+  if (check_launch(c, "bucket")) return -1;
+  uint64_t *ko;
+  uint32_t *vo;
+  if (radix_sort<uint64_t>(c, "psort", bk, nullptr, kA, perm, kB, vB, std::max(1u, ceil_log2(ns + 1)),
+                           0, m, &ko, &vo))
+    return -1;
+  if (vo != perm) HIPCHK(c, hipMemcpyAsync(perm, vo, (size_t)m * 4, hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(counts, dc, (size_t)(ns + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+int scatter_impl(cw_ctx *c, const uint32_t *src, const uint32_t *idx, uint64_t m, uint32_t *dst) {
+  if (m == 0) return 0;
+  if (!src || !idx || !dst) return fail(c, "null array");
+  HIPCHK(c, hipSetDevice(c->device));
+  Launch L(c, "scatter", (double)m * 12);
+  hipLaunchKernelGGL(k_scatter32, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, c->stream, src, idx,
+                     m, dst);
+  return check_launch(c, "scatter");
+}
+
+int weave_ranked_impl(cw_ctx *c, const cw_ranked_list *in, cw_list_result *out) {
+  if (!in || !out) return fail(c, "null list/result");
+  if (!out->weave_perm || !out->visible_count || !out->status)
+    return fail(c, "weave_perm, visible_count and status are required");
+  if (out->yarn_perm || out->max_ts) return fail(c, "yarn_perm / max_ts: not produced from ranks");
+  const uint64_t n64 = in->n;
+  if (n64 == 0 || n64 >= SUCCW_END) return fail(c, "list size %llu (1 .. 2^31-2)", (unsigned long long)n64);
+  if (!in->par || !in->kind) return fail(c, "null input arrays");
+  const uint32_t n = (uint32_t)n64;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t off[2] = {0, n64};
+  if (ensure_tables(c, 1, off, true)) return -1;
+  HIPCHK(c, hipMemsetAsync(out->status, 0, 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(out->visible_count, 0, 4, c->stream));
+  if (out->visible_bits)
+    HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)n + 31) / 32 * 4, c->stream));
+  hipLaunchKernelGGL(k_ranked_check, dim3((n + 255) / 256), dim3(256), 0, c->stream, in->par,
+                     in->kind, n, out->status);
+  if (check_launch(c, "ranked_check")) return -1;
+  if (weave_tail(c, 1, n, true, in->par, in->kind, in->val, nullptr, nullptr, 0, out)) return -1;
+  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->prof) return collect_prof(c);
   return 0;
 }
@@ -3529,6 +3818,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
+  c->tree_pad = knob("CW_TREE_PAD", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 20);
@@ -3614,6 +3904,55 @@ int cw_weft_lists(cw_ctx *c, const cw_weft_batch *b, cw_weft_result *r, int mems
   if (!c) return -1;
   c->err.clear();
   return weft_lists_impl(c, b, r, memspace);
+}
+
+int cw_sort_keys(cw_ctx *c, const uint64_t *keys, uint64_t n, uint32_t key_bits, uint64_t *keys_out,
+                 uint32_t *idx_out) {
+  if (!c) return -1;
+  c->err.clear();
+  if (sort_keys_impl(c, keys, n, key_bits, keys_out, idx_out)) return -1;
+  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_lookup_keys(cw_ctx *c, const uint64_t *sorted, uint64_t n, const uint64_t *queries,
+                   uint64_t m, uint32_t base, uint32_t *out) {
+  if (!c) return -1;
+  c->err.clear();
+  if (lookup_keys_impl(c, sorted, n, queries, m, base, out)) return -1;
+  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_gather(cw_ctx *c, const void *src, const uint32_t *idx, uint64_t m, uint32_t elem_size,
+              void *dst) {
+  if (!c) return -1;
+  c->err.clear();
+  if (gather_impl(c, src, idx, m, elem_size, dst)) return -1;
+  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_partition_keys(cw_ctx *c, const uint64_t *keys, uint64_t m, const uint64_t *splitters,
+                      uint32_t n_split, uint32_t *perm, uint64_t *counts) {
+  if (!c) return -1;
+  c->err.clear();
+  if (partition_keys_impl(c, keys, m, splitters, n_split, perm, counts)) return -1;
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_scatter32(cw_ctx *c, const uint32_t *src, const uint32_t *idx, uint64_t m, uint32_t *dst) {
+  if (!c) return -1;
+  c->err.clear();
+  if (scatter_impl(c, src, idx, m, dst)) return -1;
+  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_weave_ranked(cw_ctx *c, const cw_ranked_list *l, cw_list_result *r) {
+  if (!c) return -1;
+  c->err.clear();
+  return weave_ranked_impl(c, l, r);
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

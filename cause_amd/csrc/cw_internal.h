@@ -37,6 +37,12 @@ constexpr uint32_t EMIT_STAGE = 4096;          // weave positions staged per emi
 constexpr uint32_t NSC_UP = 0x80000000u;         // nsc: no next sibling, low bits = eff parent
 constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder
 constexpr uint32_t NX_END = 0xFFFFFFFFu;          // last sublist of a document
+// Wide links (the giant-document path, documents < 2^31 - 1 nodes): a u64 link
+// word = successor (low 32 bits; SUCCW_END for the last node) | the LINK_*
+// flags above << 32; thr entries = node | THRW_PEND when still pending.
+constexpr uint32_t SUCCW_END = 0x7FFFFFFFu;
+constexpr uint32_t THRW_PEND = 0x80000000u;
+constexpr uint32_t SLOT_IDX = 0x7FFFFFFFu;        // walk slot entry: rank | renders << 31
 
 constexpr uint8_t KIND_CLASS = 3, KIND_ROOT = 4, KIND_HIDE = 1, KIND_HHIDE = 2;
 

@@ -1,0 +1,274 @@
+"""One CausalList spread over several GPUs (BASELINE config 5: a single list of
+2*10^9 nodes on 8 MI355X).
+
+The reference weaves a list by `(sort ::nodes)` and a fold (list.cljc:26-28);
+its nodes live in one hash map.  Here each rank (one process per GPU) holds an
+arbitrary share of the node bag and the weave runs as
+
+  1. local sort of the ids (cw_sort_keys);
+  2. sample sort: weighted regular samples -> all_gather -> W-1 splitters;
+     ids, causes, kinds and origins go to their owner rank (all_to_all, the
+     only data exchange of the weave: RCCL over xGMI with the nccl backend);
+  3. the owner sorts what it received: rank r owns a contiguous run of the
+     global id order, so a node's global rank = owner base + local index;
+  4. cause join (shared.cljc:175-178): cause ids travel to the rank owning
+     them (cw_partition_keys + all_to_all), are looked up there
+     (cw_lookup_keys) and the global ranks travel back (all_to_all);
+  5. the rank-ordered (parent rank, kind, origin) arrays -- 9 bytes a node --
+     gather on one rank, which runs the tree and the Euler tour for the whole
+     list (cw_weave_ranked: the giant-document path of causeweave.hip).
+
+Every step that touches node data is a HIP kernel of libcauseweave behind the
+C ABI; torch provides device memory, the collectives and tiny host-side
+arithmetic on W-sized arrays (sample weights, splitters).  `ops` is the
+kernel interface: HipOps in production; tests may pass a CPU double to check
+the exchange logic with gloo on CPU.
+"""
+from __future__ import annotations
+
+import contextlib
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+NOT_FOUND = 0xFFFFFFFF
+
+
+def _on_stream(f):
+    """Run a HipOps method on the ops' stream (ordered after the caller's)."""
+    def g(self, *a, **k):
+        with self.stream_context():
+            return f(self, *a, **k)
+    g.__name__ = f.__name__
+    return g
+
+
+class HipOps:
+    """The kernels of the distributed weave on one GPU (libcauseweave).
+
+    The library and torch share one stream (a torch stream handed to the
+    context; torch's default stream has no handle to hand over), so kernels,
+    torch's allocations and the collectives are ordered without host syncs."""
+
+    def __init__(self, weaver, device):
+        self.w = weaver
+        self.dev = torch.device(device)
+        self.stream = torch.cuda.Stream(self.dev)
+        weaver.set_stream(self.stream.cuda_stream)
+        weaver.set_async(True)
+
+    @contextlib.contextmanager
+    def stream_context(self):
+        cur = torch.cuda.current_stream(self.dev)
+        if cur == self.stream:
+            yield
+            return
+        self.stream.wait_stream(cur)
+        with torch.cuda.stream(self.stream):
+            yield
+        cur.wait_stream(self.stream)
+
+    def _e(self, n, dtype):
+        return torch.empty(n, dtype=dtype, device=self.dev)
+
+    @_on_stream
+    def sort_keys(self, keys, key_bits):
+        n = keys.numel()
+        ko, io = self._e(n, torch.int64), self._e(n, torch.int32)
+        if n:
+            self.w.sort_keys_device(keys.data_ptr(), n, key_bits, ko.data_ptr(), io.data_ptr())
+        return ko, io
+
+    @_on_stream
+    def partition(self, keys, splitters):
+        m = keys.numel()
+        perm = self._e(m, torch.int32)
+        sp = splitters.to(self.dev)
+        counts = self.w.partition_keys_device(keys.data_ptr() if m else 0, m,
+                                              sp.data_ptr() if sp.numel() else 0, sp.numel(),
+                                              perm.data_ptr() if m else 0)
+        return perm, [int(x) for x in counts]
+
+    @_on_stream
+    def lookup(self, sorted_keys, queries, base):
+        m = queries.numel()
+        out = self._e(m, torch.int32)
+        if m:
+            self.w.lookup_keys_device(sorted_keys.data_ptr() if sorted_keys.numel() else 0,
+                                      sorted_keys.numel(), queries.data_ptr(), m, base,
+                                      out.data_ptr())
+        return out
+
+    @_on_stream
+    def gather(self, src, idx):
+        m = idx.numel()
+        out = self._e(m, src.dtype)
+        if m:
+            self.w.gather_device(src.data_ptr(), idx.data_ptr(), m, src.element_size(),
+                                 out.data_ptr())
+        return out
+
+    @_on_stream
+    def scatter32(self, src, idx):
+        m = idx.numel()
+        out = self._e(m, torch.int32)
+        if m:
+            self.w.scatter32_device(src.data_ptr(), idx.data_ptr(), m, out.data_ptr())
+        return out
+
+    @_on_stream
+    def weave_ranked(self, par, kind, val):
+        n = par.numel()
+        o = {"weave_perm": self._e(n, torch.int32),
+             "visible_bits": self._e((n + 31) // 32, torch.int32),
+             "visible_count": self._e(1, torch.int32), "status": self._e(1, torch.int32)}
+        self.w.weave_ranked_device(n, par.data_ptr(), kind.data_ptr(), val.data_ptr(),
+                                   {k: t.data_ptr() for k, t in o.items()})
+        return o
+
+    def sync(self):
+        torch.cuda.synchronize(self.dev)
+
+
+@dataclass
+class GiantResult:
+    """On the gathering rank: the weave of the whole list.  weave_perm[g] =
+    global input index (rank offset + local index) of the node at weave
+    position g; elsewhere None."""
+    weave_perm: torch.Tensor | None
+    visible_bits: torch.Tensor | None
+    visible_count: int | None
+    status: int | None
+    n_total: int
+    n_owned: int        # ids this rank owned after the sample sort
+    max_ts: int
+
+
+def _a2a(t, send, recv, group):
+    """all_to_all_single with split sizes; gloo works on host tensors."""
+    out = torch.empty(sum(recv), dtype=t.dtype, device=t.device)
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        o = out.cpu()
+        dist.all_to_all_single(o, t.cpu(), recv, send, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, t, recv, send, group=group)
+    return out
+
+
+def _exchange_counts(send, group, device):
+    W = len(send)
+    dev = "cpu" if dist.get_backend(group) == "gloo" else device
+    s = torch.tensor(send, dtype=torch.int64, device=dev)
+    r = torch.empty(W, dtype=torch.int64, device=dev)
+    dist.all_to_all_single(r, s, group=group)
+    return [int(x) for x in r.cpu()]
+
+
+def _all_gather_ints(vals, group, device):
+    dev = "cpu" if dist.get_backend(group) == "gloo" else device
+    W = dist.get_world_size(group)
+    t = torch.tensor(vals, dtype=torch.int64, device=dev)
+    out = [torch.empty_like(t) for _ in range(W)]
+    dist.all_gather(out, t, group=group)
+    return [[int(x) for x in o.cpu()] for o in out]
+
+
+def choose_splitters(samples, weights, W):
+    """W-1 splitters from weighted samples (each stands for `weight` ids):
+    splitter j = the first sample whose cumulative weight reaches j*N/W."""
+    if W <= 1 or len(samples) == 0:
+        return np.zeros(0, np.int64)
+    o = np.argsort(samples, kind="stable")
+    s, cw = samples[o], np.cumsum(weights[o])
+    total = cw[-1]
+    at = np.searchsorted(cw, np.arange(1, W) * total / W, side="left")
+    return s[np.minimum(at, len(s) - 1)].astype(np.int64)
+
+
+def weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift=0, group=None,
+                      root=0, samples=256) -> GiantResult:
+    """Weave one list whose nodes are spread over the ranks of `group`.
+
+    id_key / cause_key: int64 tensors holding the packed u64 keys (< 2^63);
+    kind: uint8.  Every rank calls this; rank `root` receives the weave."""
+    if key_bits > 63:
+        raise ValueError("keys must be < 2^63 (int64 order)")
+    ctx = getattr(ops, "stream_context", contextlib.nullcontext)
+    with ctx():
+        return _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root,
+                                  samples)
+
+
+def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples):
+    W, r = dist.get_world_size(group), dist.get_rank(group)
+    dev = id_key.device
+    n = id_key.numel()
+    ns = [v[0] for v in _all_gather_ints([n], group, dev)]
+    N, in_base = sum(ns), sum(ns[:r])
+    if N >= 0x7FFFFFFE:
+        raise ValueError(f"list of {N} nodes: limit 2^31-2")
+
+    # 1. local id sort
+    sk, si = ops.sort_keys(id_key, key_bits)
+
+    # 2. sample sort: regular samples weighted by the share they stand for
+    s = min(samples, n)
+    if s:
+        pos = ((np.arange(s) + 0.5) * n / s).astype(np.int64)
+        smp = sk[torch.as_tensor(pos, device=dev)].cpu().numpy()
+    else:
+        smp = np.zeros(0, np.int64)
+    counts = _all_gather_ints([s], group, dev)
+    pad = np.zeros(samples, np.int64)
+    pad[:s] = smp
+    gath = _all_gather_ints(list(pad), group, dev)
+    all_s = np.concatenate([np.array(g[:c[0]], np.int64) for g, c in zip(gath, counts)])
+    all_w = np.concatenate([np.full(c[0], ns[j] / max(c[0], 1)) for j, c in enumerate(counts)])
+    split = choose_splitters(all_s, all_w, W)
+    split_t = torch.as_tensor(split, device=dev)
+    # sk is sorted: the ids bound for rank j are one contiguous run
+    bounds = torch.searchsorted(sk, split_t).cpu().tolist() if W > 1 else []
+    edges = [0] + bounds + [n]
+    send = [edges[j + 1] - edges[j] for j in range(W)]
+    recv = _exchange_counts(send, group, dev)
+    org = (si.to(torch.int64) + in_base).to(torch.int32)
+    r_id = _a2a(sk, send, recv, group)
+    r_ca = _a2a(ops.gather(cause_key, si), send, recv, group)
+    r_kd = _a2a(ops.gather(kind, si), send, recv, group)
+    r_org = _a2a(org, send, recv, group)
+    del sk, si, org
+
+    # 3. the owner's run of the global id order
+    ok, oi = ops.sort_keys(r_id, key_bits)
+    oca, okd, oorg = ops.gather(r_ca, oi), ops.gather(r_kd, oi), ops.gather(r_org, oi)
+    del r_id, r_ca, r_kd, r_org, oi
+    n_own = ok.numel()
+    owns = [v[0] for v in _all_gather_ints([n_own], group, dev)]
+    own_base = sum(owns[:r])
+    local_max = int(ok[-1]) >> ts_shift if n_own else 0
+
+    # 4. cause join at the owner of each cause id
+    perm, qsend = ops.partition(oca, split_t)
+    qrecv = _exchange_counts(qsend, group, dev)
+    rq = _a2a(ops.gather(oca, perm), qsend, qrecv, group)
+    ans = ops.lookup(ok, rq, own_base)
+    back = _a2a(ans, qrecv, qsend, group)
+    par = ops.scatter32(back, perm)
+    del perm, rq, ans, back, oca
+
+    # 5. gather the rank-ordered arrays on the root and weave there
+    gsend = [n_own if j == root else 0 for j in range(W)]
+    grecv = [owns[j] if r == root else 0 for j in range(W)]
+    g_par = _a2a(par, gsend, grecv, group)
+    g_kd = _a2a(okd, gsend, grecv, group)
+    g_org = _a2a(oorg, gsend, grecv, group)
+    mx = _all_gather_ints([local_max], group, dev)
+    max_ts = max(v[0] for v in mx)
+    if r != root:
+        return GiantResult(None, None, None, None, N, n_own, max_ts)
+    o = ops.weave_ranked(g_par, g_kd, g_org)
+    return GiantResult(o["weave_perm"], o["visible_bits"], int(o["visible_count"][0]),
+                       int(o["status"][0]), N, n_own, max_ts)

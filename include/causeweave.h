@@ -127,7 +127,8 @@ typedef struct {
 } cw_list_result;
 
 /* Full reweave of a batch of independent CausalLists (N = doc_offsets[n_docs]
- * < 2^32, each document < 2^29 nodes).  `memspace` says where id_key /
+ * < 2^32; in a batch of several documents each is < 2^29 - 1 nodes, a batch of
+ * one document may hold up to 2^31 - 2).  `memspace` says where id_key /
  * cause_key / kind and every result array live (doc_offsets is always host). */
 int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
                    int memspace);
@@ -235,6 +236,54 @@ typedef struct {
 
 /* Host memory only (memspace must be CW_MEM_HOST in this version). */
 int cw_weft_lists(cw_ctx *ctx, const cw_weft_batch *batch, cw_weft_result *result, int memspace);
+
+/* ------------------------------------ the distributed giant list (config 5) ---- */
+/* Building blocks for one list spread over several GPUs (cause_amd/giant.py:
+ * sample sort by RCCL all-to-all, cause lookup at the owner of the cause id,
+ * then the tree and the tour on one GPU).  Device memory only; the calls are
+ * ordered on the context's stream. */
+
+#define CW_NOT_FOUND 0xFFFFFFFFu
+
+/* (sort ::nodes) of one document's ids (list.cljc:28, shared.cljc:128):
+ * keys_out = keys ascending, idx_out[i] = input index of keys_out[i] (stable).
+ * key_bits = 0: the library finds the significant bits.  n < 2^32 - 1. */
+int cw_sort_keys(cw_ctx *ctx, const uint64_t *keys, uint64_t n, uint32_t key_bits,
+                 uint64_t *keys_out, uint32_t *idx_out);
+
+/* out[i] = base + index of queries[i] among the n ascending unique keys
+ * `sorted`, or CW_NOT_FOUND (the cause join of s/insert, shared.cljc:175-178). */
+int cw_lookup_keys(cw_ctx *ctx, const uint64_t *sorted, uint64_t n, const uint64_t *queries,
+                   uint64_t m, uint32_t base, uint32_t *out);
+
+/* Group m keys by bucket among n_split ascending splitters (bucket of x = the
+ * number of splitters <= x; n_split <= 1023): perm lists the key indices
+ * bucket by bucket (stable), counts[0..n_split] (HOST memory) the bucket
+ * sizes.  Synchronous (the counts are read back). */
+int cw_partition_keys(cw_ctx *ctx, const uint64_t *keys, uint64_t m, const uint64_t *splitters,
+                      uint32_t n_split, uint32_t *perm, uint64_t *counts);
+
+/* dst[i] = src[idx[i]], elements of elem_size 1, 4 or 8 bytes. */
+int cw_gather(cw_ctx *ctx, const void *src, const uint32_t *idx, uint64_t m, uint32_t elem_size,
+              void *dst);
+
+/* dst[idx[i]] = src[i] for 4-byte elements (idx a permutation of 0..m-1). */
+int cw_scatter32(cw_ctx *ctx, const uint32_t *src, const uint32_t *idx, uint64_t m, uint32_t *dst);
+
+/* One list handed over in id order (rank r = the r-th smallest id; rank 0 the
+ * root): par[r] = rank of r's cause (par[0] ignored; CW_NOT_FOUND = orphan),
+ * kind[r] as in cw_list_batch.  val[r] = the value emitted for rank r (NULL:
+ * r itself).  result: weave_perm[g] = val of the node at weave position g,
+ * visible_bits, visible_count[0], status[0]; yarn_perm and max_ts must be NULL
+ * (they need the ids: the caller has them).  n <= 2^31 - 2. */
+typedef struct {
+  uint64_t n;
+  const uint32_t *par;
+  const uint8_t *kind;
+  const uint32_t *val;
+} cw_ranked_list;
+
+int cw_weave_ranked(cw_ctx *ctx, const cw_ranked_list *list, cw_list_result *result);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,112 @@
+"""The distributed giant-list weave (cause_amd/giant.py, BASELINE config 5) on
+CPU: gloo ranks, the kernels replaced by the numpy/oracle double
+tests/giant_cpu_ops.py.  Each rank holds a random share of one list's nodes in
+random order; the gathered weave must equal the oracle's weave of the whole
+list (global input index = rank offset + local index)."""
+import dataclasses
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from cause_amd import gen, giant
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def make_list(n, seed):
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n, seed=seed)
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=1)
+    return spec, idk, ck, kd
+
+
+def shares(N, W, seed, empty_rank=None):
+    """A random split of 0..N-1 into W shares (random order inside each)."""
+    rng = np.random.default_rng(seed)
+    owner = rng.integers(0, W, N)
+    if empty_rank is not None:
+        owner[owner == empty_rank] = (empty_rank + 1) % W
+    return [rng.permutation(np.flatnonzero(owner == r)) for r in range(W)]
+
+
+def _worker(rank, world, port, n, seed, samples, empty_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.giant_cpu_ops import CpuOps
+
+        spec, idk, ck, kd = make_list(n, seed)
+        sh = shares(len(idk), world, seed, empty_rank)[rank]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+        lay = spec.layout()
+        res = giant.weave_distributed(CpuOps(), t(idk[sh]), t(ck[sh]),
+                                      torch.from_numpy(kd[sh].copy()), lay.key_bits,
+                                      ts_shift=lay.ts_shift, samples=samples)
+        if rank == 0:
+            q.put((res.weave_perm.numpy().copy(), res.visible_count, res.status, res.n_total,
+                   res.max_ts))
+        q.put(("own", rank, res.n_owned))
+    finally:
+        dist.destroy_process_group()
+
+
+def run(world, n, seed, samples=64, empty_rank=None):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n, seed, samples, empty_rank, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got, owned = None, {}
+    for _ in range(world + 1):
+        m = q.get(timeout=120)
+        if isinstance(m[0], str):
+            owned[m[1]] = m[2]
+        else:
+            got = m
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    return got, owned
+
+
+@pytest.mark.parametrize("world,n,seed,empty", [(2, 3000, 11, None), (3, 5000, 12, None),
+                                                (4, 2000, 13, 2)])
+def test_distributed_weave_matches_oracle(world, n, seed, empty):
+    (wp, vcount, status, N, max_ts), owned = run(world, n, seed, empty_rank=empty)
+    spec, idk, ck, kd = make_list(n, seed)
+    assert N == len(idk) and sum(owned.values()) == N
+    perm, vis, st = oracle.batch_lists(np.array([0, N], np.uint64), idk, ck, kd,
+                                       method=oracle.METHOD_EFF)
+    # global input index -> node of the whole list
+    sh = np.concatenate(shares(N, world, seed, empty))
+    assert status == 0 and not st.any()
+    assert np.array_equal(sh[wp.view(np.uint32)], perm)
+    assert vcount == int(vis.sum())
+    assert max_ts == int(idk.max()) >> spec.layout().ts_shift
+    # the sample sort balances the owners
+    assert max(owned.values()) < 2.0 * N / world
+
+
+def test_choose_splitters_weighted():
+    s = np.arange(100, dtype=np.int64)
+    w = np.ones(100)
+    assert list(giant.choose_splitters(s, w, 4)) == [24, 49, 74]
+    # a rank with 10x the nodes but the same number of samples weighs 10x
+    s2 = np.concatenate([np.arange(0, 50), np.arange(50, 100)]).astype(np.int64)
+    w2 = np.concatenate([np.full(50, 10.0), np.full(50, 1.0)])
+    assert giant.choose_splitters(s2, w2, 2)[0] < 50
+    assert len(giant.choose_splitters(np.zeros(0, np.int64), np.zeros(0), 3)) == 0

@@ -1,0 +1,185 @@
+"""The distributed giant-list weave on the GPU (cause_amd/giant.py, config 5).
+
+1. Each building block behind the C ABI (cw_sort_keys, cw_partition_keys,
+   cw_lookup_keys, cw_gather, cw_scatter32, cw_weave_ranked) against the CPU
+   double tests/giant_cpu_ops.py on the same inputs, bit-exact.
+2. weave_distributed with HipOps: one rank in this process, and two ranks as
+   two worker processes sharing cuda:0 (gloo, host-staged exchange), against
+   the oracle's weave of the whole list.
+"""
+import dataclasses
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+from cause_amd import abi, gen, giant
+from tests.giant_cpu_ops import CpuOps
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    import torch
+
+    with abi.Weaver(0) as w:
+        yield giant.HipOps(w, "cuda:0")
+        torch.cuda.synchronize()
+
+
+def _t(a, dev="cuda:0"):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def _i64(a):
+    return np.ascontiguousarray(a, np.uint64).view(np.int64)
+
+
+@pytest.mark.parametrize("n,bits", [(1, 5), (1000, 12), (5000, 40), (300_000, 33), (70_000, 63)])
+def test_sort_keys(ops, n, bits):
+    rng = np.random.default_rng(n)
+    k = rng.integers(0, 1 << bits, n, dtype=np.uint64)  # duplicates: stability shows
+    ko, io = ops.sort_keys(_t(_i64(k)), bits)
+    rk, ri = CpuOps().sort_keys(__import__("torch").from_numpy(_i64(k)), bits)
+    assert np.array_equal(ko.cpu().numpy(), rk.numpy())
+    assert np.array_equal(io.cpu().numpy(), ri.numpy())
+
+
+@pytest.mark.parametrize("m,ns", [(0, 3), (1, 0), (5000, 1), (100_000, 7), (200_000, 200)])
+def test_partition(ops, m, ns):
+    import torch
+
+    rng = np.random.default_rng(m + ns)
+    k = rng.integers(0, 1 << 40, m, dtype=np.uint64)
+    k[: m // 10] = np.uint64(2**64 - 1)  # nil causes go to the last bucket
+    sp = np.sort(rng.integers(0, 1 << 40, ns, dtype=np.uint64))
+    perm, counts = ops.partition(_t(_i64(k)), torch.from_numpy(_i64(sp)))
+    rp, rc = CpuOps().partition(torch.from_numpy(_i64(k)), torch.from_numpy(_i64(sp)))
+    assert counts == rc
+    assert np.array_equal(perm.cpu().numpy(), rp.numpy())
+
+
+@pytest.mark.parametrize("n,m,base", [(0, 10, 0), (1, 5, 7), (10_000, 50_000, 0),
+                                      (400_000, 100_000, 123_456)])
+def test_lookup(ops, n, m, base):
+    import torch
+
+    rng = np.random.default_rng(n + m)
+    s = np.unique(rng.integers(0, 1 << 36, n, dtype=np.uint64))
+    q = rng.integers(0, 1 << 36, m, dtype=np.uint64)
+    if len(s):
+        hit = rng.integers(0, len(s), m // 2)
+        q[: m // 2] = s[hit]
+    got = ops.lookup(_t(_i64(s)), _t(_i64(q)), base).cpu().numpy()
+    ref = CpuOps().lookup(torch.from_numpy(_i64(s)), torch.from_numpy(_i64(q)), base).numpy()
+    assert np.array_equal(got, ref)
+
+
+def test_gather_scatter(ops):
+    rng = np.random.default_rng(5)
+    n = 100_003
+    idx = rng.permutation(n).astype(np.int32)
+    for dt in (np.uint8, np.int32, np.int64):
+        src = rng.integers(0, 100, n).astype(dt)
+        got = ops.gather(_t(src), _t(idx)).cpu().numpy()
+        assert np.array_equal(got, src[idx])
+    src = rng.integers(0, 1 << 30, n).astype(np.int32)
+    out = ops.scatter32(_t(src), _t(idx)).cpu().numpy()
+    ref = np.empty_like(src)
+    ref[idx] = src
+    assert np.array_equal(out, ref)
+
+
+def ranked_case(n, seed):
+    """One list as (par, kind) in rank order, from the config-2 generator."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n, seed=seed)
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=1)
+    o = np.argsort(idk, kind="stable")
+    rank = np.empty(len(o), np.int64)
+    rank[o] = np.arange(len(o))
+    ck_o = ck[o]
+    pos = np.searchsorted(idk[o], ck_o)
+    par = np.where(ck_o == np.uint64(2**64 - 1), 0xFFFFFFFF, pos).astype(np.uint32)
+    return par.view(np.int32), kd[o].copy(), o.astype(np.int32)
+
+
+@pytest.mark.parametrize("n,seed", [(1, 1), (50, 2), (20_000, 3), (600_000, 4)])
+def test_weave_ranked(ops, n, seed):
+    import torch
+
+    par, kd, val = ranked_case(n, seed)
+    got = ops.weave_ranked(_t(par), _t(kd), _t(val))
+    ref = CpuOps().weave_ranked(torch.from_numpy(par), torch.from_numpy(kd), torch.from_numpy(val))
+    assert int(got["status"][0]) == 0 == int(ref["status"][0])
+    assert np.array_equal(got["weave_perm"].cpu().numpy(), ref["weave_perm"].numpy())
+    assert int(got["visible_count"][0]) == int(ref["visible_count"][0])
+    assert np.array_equal(got["visible_bits"].cpu().numpy(), ref["visible_bits"].numpy())
+
+
+def test_weave_ranked_flags_orphans_and_roots(ops):
+    par, kd, val = ranked_case(2000, 7)
+    p = par.copy()
+    p[100] = -1  # CW_NOT_FOUND
+    got = ops.weave_ranked(_t(p), _t(kd), _t(val))
+    assert int(got["status"][0]) & abi.STATUS_ORPHAN
+    k = kd.copy()
+    k[0] &= ~np.uint8(4)
+    got = ops.weave_ranked(_t(par), _t(k), _t(val))
+    assert int(got["status"][0]) & abi.STATUS_ROOT
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_distributed_one_rank_in_process(ops):
+    import torch
+    import torch.distributed as dist
+
+    from tests.test_giant_dist import make_list
+
+    spec, idk, ck, kd = make_list(100_000, 21)
+    rng = np.random.default_rng(0)
+    sh = rng.permutation(len(idk))
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    g = dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        lay = spec.layout()
+        res = giant.weave_distributed(ops, _t(_i64(idk[sh])), _t(_i64(ck[sh])), _t(kd[sh]),
+                                      lay.key_bits, ts_shift=lay.ts_shift)
+    finally:
+        dist.destroy_process_group()
+    perm, vis, st = oracle.batch_lists(np.array([0, len(idk)], np.uint64), idk, ck, kd,
+                                       method=oracle.METHOD_EFF)
+    assert res.status == 0
+    assert np.array_equal(sh[res.weave_perm.cpu().numpy()], perm)
+    assert res.visible_count == int(vis.sum())
+
+
+def test_distributed_two_ranks_share_the_gpu(tmp_path):
+    """Two worker processes on cuda:0 (gloo: the exchange is staged on the host;
+    with the nccl backend on distinct GPUs it runs over RCCL)."""
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    procs = []
+    for r in range(2):
+        e = dict(env, RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "giant_worker.py"),
+                                       str(tmp_path)], env=e, cwd=ROOT))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    out = json.load(open(tmp_path / "rank0.json"))
+    assert out["ok"], out
