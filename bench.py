@@ -45,6 +45,9 @@ def parse():
                          "5 = one giant list (--giant nodes; replicas on N GPUs)")
     ap.add_argument("--giant", type=int, default=1 << 26, help="--config 5: nodes in the list")
     ap.add_argument("--colls", type=int, default=1_000_000, help="--config 4: collections per GPU")
+    ap.add_argument("--dist", action="store_true",
+                    help="--config 5 on one GPU through the distributed path (sample sort, "
+                         "exchange, gather; always taken when N > 1)")
     return ap.parse_args()
 
 
@@ -105,6 +108,99 @@ def cpu_baseline_maps(spec, budget_s):
     return {"value": done / t_total, "unit": "nodes/s", "cores": 1, "kind": "port",
             "sample": f"{colls} collections x {spec.nodes_per_coll} nodes of the same workload, "
                       f"literal map weave + active-node (map.cljc:21-59) in C, {t_total:.1f} s"}
+
+
+def main_giant_dist(a, world, rank, local, dist, torch, dev):
+    """--config 5 on N GPUs: ONE list of --giant nodes whose nodes are spread
+    over the ranks (rank r holds every N-th node of the generation order).
+    One step = cause_amd.giant.weave_distributed: local sort, sample sort by
+    all_to_all (RCCL), cause join at the owners, gather of the rank-ordered
+    arrays on rank 0 and the tree + tour there.  Strong scaling: the list is
+    the same at every N."""
+    import dataclasses
+
+    from cause_amd import abi, gen, giant
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.giant)
+    lay = spec.layout()
+    t0 = time.time()
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
+    t_gen = time.time() - t0
+    N = len(idk)
+    sel = slice(rank, N, world)
+    g_id = torch.from_numpy(np.ascontiguousarray(idk[sel]).view(np.int64)).to(dev)
+    g_ca = torch.from_numpy(np.ascontiguousarray(ck[sel]).view(np.int64)).to(dev)
+    g_kd = torch.from_numpy(np.ascontiguousarray(kd[sel])).to(dev)
+    if rank != 0 or world > 1 or a.no_cpu:
+        del idk, ck, kd
+    torch.cuda.synchronize()
+    group = None
+    if world == 1:  # one rank: a private gloo group only for the (empty) exchange bookkeeping
+        import socket
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        store = dist.TCPStore("127.0.0.1", port, 1, True)
+        dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    w = abi.Weaver(local)
+    ops = giant.HipOps(w, dev)
+
+    def step():
+        return giant.weave_distributed(ops, g_id, g_ca, g_kd, lay.key_bits, ts_shift=lay.ts_shift,
+                                       group=group)
+
+    res = None
+    for _ in range(a.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    if rank == 0 and res is not None and res.status != 0:
+        raise SystemExit(f"status {res.status}")
+    w.reset_kernel_stats()
+    w.set_profiling(True)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        res = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    w.set_profiling(False)
+    stats = w.kernel_stats()
+    from cause_amd import shard
+
+    dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
+    value = N * a.steps / dt_max
+    if rank == 0:
+        name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
+        achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        cpu = None
+        if world == 1 and not a.no_cpu:
+            cpu = cpu_baseline_prefix(idk, ck, kd, 100_000)
+        line = {
+            "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
+            "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt_max / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
+            "config": {"workload": (f"config5: one CausalList of {N:,} nodes spread over "
+                                    f"{world} rank(s), distributed sample sort + gather"),
+                       "nodes_total": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
+                       "key_bits": lay.key_bits,
+                       "parallelism": f"sample sort x{world} ({dist.get_backend()})"},
+            "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "launches_per_step": launches / a.steps,
+                         "kernel_ms_per_step": ms / a.steps},
+            "cpu_baseline": cpu,
+            "kernels_ms_per_step_rank0": {k: round(v[1] / a.steps, 4) for k, v in
+                                          sorted(stats.items(), key=lambda kv: -kv[1][1])},
+            "kernel_sum_ms_per_step_rank0": sum(v[1] for v in stats.values()) / a.steps,
+            "nodes_owned_rank0": res.n_owned, "gen_s": t_gen,
+        }
+        print(json.dumps(line), flush=True)
+    w.close()
 
 
 def main_maps(a, world, rank, local, dist, torch, dev):
@@ -199,6 +295,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    if a.config == 5 and (world > 1 or a.dist):
+        main_giant_dist(a, world, rank, local, dist, torch, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if a.config == 4:
         main_maps(a, world, rank, local, dist, torch, dev)
         if world > 1:

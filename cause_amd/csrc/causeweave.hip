@@ -3101,19 +3101,34 @@ __global__ __launch_bounds__(256) void k_bucket(const uint64_t *__restrict__ key
                                                 const uint64_t *__restrict__ split, uint32_t ns,
                                                 uint64_t *__restrict__ bucket,
                                                 unsigned long long *__restrict__ counts) {
+  // grid-stride over a few thousand blocks: one global atomic per block and
+  // bucket (a block per 256 keys would serialise on the count words)
   __shared__ unsigned long long cnt[1024];
   for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x) cnt[j] = 0;
   __syncthreads();
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) {
-    const uint64_t x = keys[i];
-    uint32_t lo = 0, hi = ns;  // first splitter > x
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (split[mid] <= x) lo = mid + 1; else hi = mid;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < m; i0 += stride) {
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t my = 0xFFFFFFFFu;
+    if (i < m) {
+      const uint64_t x = keys[i];
+      uint32_t lo = 0, hi = ns;  // first splitter > x
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (split[mid] <= x) lo = mid + 1; else hi = mid;
+      }
+      bucket[i] = lo;
+      my = lo;
     }
-    bucket[i] = lo;
-    atomicAdd(&cnt[lo], 1ull);
+    // few buckets: a ballot per bucket (one LDS atomic per wave and bucket)
+    if (ns < 64) {
+      for (uint32_t b = 0; b <= ns; b++) {
+        const uint64_t bal = __ballot(my == b);
+        if ((threadIdx.x & 63) == 0 && bal) atomicAdd(&cnt[b], (unsigned long long)__popcll(bal));
+      }
+    } else if (i < m) {
+      atomicAdd(&cnt[my], 1ull);
+    }
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j <= ns; j += blockDim.x)
@@ -3260,8 +3275,8 @@ int partition_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t m64, const uin
   HIPCHK(c, hipMemsetAsync(dc, 0, (size_t)(ns + 1) * 8, c->stream));
   {
     Launch L(c, "bucket", (double)m * 16);
-    hipLaunchKernelGGL(k_bucket, dim3((m + 255) / 256), dim3(256), 0, c->stream, keys, m, split, ns, bk,
-                       dc);
+    hipLaunchKernelGGL(k_bucket, dim3(std::min<uint32_t>((m + 255) / 256, 4096)), dim3(256), 0,
+                       c->stream, keys, m, split, ns, bk, dc);
   }
   if (check_launch(c, "bucket")) return -1;
   uint64_t *ko;

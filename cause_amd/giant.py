@@ -148,6 +148,8 @@ class GiantResult:
 
 def _a2a(t, send, recv, group):
     """all_to_all_single with split sizes; gloo works on host tensors."""
+    if dist.get_world_size(group) == 1:
+        return t
     out = torch.empty(sum(recv), dtype=t.dtype, device=t.device)
     if dist.get_backend(group) == "gloo" and t.is_cuda:
         o = out.cpu()
@@ -160,6 +162,8 @@ def _a2a(t, send, recv, group):
 
 def _exchange_counts(send, group, device):
     W = len(send)
+    if W == 1:
+        return list(send)
     dev = "cpu" if dist.get_backend(group) == "gloo" else device
     s = torch.tensor(send, dtype=torch.int64, device=dev)
     r = torch.empty(W, dtype=torch.int64, device=dev)
@@ -241,10 +245,14 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
     r_org = _a2a(org, send, recv, group)
     del sk, si, org
 
-    # 3. the owner's run of the global id order
-    ok, oi = ops.sort_keys(r_id, key_bits)
-    oca, okd, oorg = ops.gather(r_ca, oi), ops.gather(r_kd, oi), ops.gather(r_org, oi)
-    del r_id, r_ca, r_kd, r_org, oi
+    # 3. the owner's run of the global id order (one rank: already sorted)
+    if W == 1:
+        ok, oca, okd, oorg = r_id, r_ca, r_kd, r_org
+    else:
+        ok, oi = ops.sort_keys(r_id, key_bits)
+        oca, okd, oorg = ops.gather(r_ca, oi), ops.gather(r_kd, oi), ops.gather(r_org, oi)
+        del oi
+    del r_id, r_ca, r_kd, r_org
     n_own = ok.numel()
     owns = [v[0] for v in _all_gather_ints([n_own], group, dev)]
     own_base = sum(owns[:r])
