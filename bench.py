@@ -51,12 +51,41 @@ def parse():
     return ap.parse_args()
 
 
+class heartbeat:
+    """Prints a progress line to stderr every `every` seconds while a long host
+    step (the generator of a giant list) runs."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.time()
+        while not self.stop.wait(self.every):
+            print(f"[bench] {self.what}: {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *a):
+        self.stop.set()
+        self.t.join()
+
+
 def cpu_baseline_prefix(idk, ck, kd, prefix):
     """Config 5: the literal fold is quadratic, so it runs on the id-order prefix
     of `prefix` nodes of the same list (causally closed: causes are older)."""
     import oracle
 
-    o = np.argsort(idk, kind="stable")[:prefix]
+    if len(idk) > prefix:  # the prefix without sorting the whole list
+        thr = np.partition(idk, prefix - 1)[prefix - 1]
+        sel = np.flatnonzero(idk <= thr)
+        o = sel[np.argsort(idk[sel], kind="stable")][:prefix]
+    else:
+        o = np.argsort(idk, kind="stable")
     t0 = time.perf_counter()
     _, st = oracle.list_weave(idk[o], ck[o], kd[o], oracle.METHOD_LITERAL)
     t = time.perf_counter() - t0
@@ -124,7 +153,8 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.giant)
     lay = spec.layout()
     t0 = time.time()
-    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
+    with heartbeat("generating the input"):
+        off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
     t_gen = time.time() - t0
     N = len(idk)
     sel = slice(rank, N, world)
@@ -328,7 +358,8 @@ def main():
         workload = "config2: independent CausalLists, full reweave"
     layout = spec.layout()
     t0 = time.time()
-    off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16)
+    with heartbeat("generating the input"):
+        off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16)
     N = len(idk)
     t_gen = time.time() - t0
     g_id = torch.from_numpy(idk.view(np.int64)).to(dev)

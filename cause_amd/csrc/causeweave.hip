@@ -2675,11 +2675,18 @@ int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool force_giant =
 // skind, sval (the value emitted for each rank; nullptr = the rank itself).
 // skey != nullptr: ::lamport-ts from the largest sorted id (otherwise the
 // front end wrote it).  kbm: the front end's special/hide bitmaps or nullptr.
+// spare: nullptr or two free buffers of >= 8 N bytes each (the id sort's
+// ping-pong pair), which the giant tree's group-key sort then reuses.
 int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *par,
                const uint8_t *skind, const uint32_t *sval, const uint32_t *kbm,
-               const uint64_t *skey, uint32_t ts_shift, cw_list_result *out) {
+               const uint64_t *skey, uint32_t ts_shift, cw_list_result *out,
+               void *spareA = nullptr, void *spareB = nullptr) {
   auto &t = c->tab;
   const dim3 B256(256);
+  if (giant && out->max_ts && skey) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
+    hipLaunchKernelGGL(k_max_ts1, dim3(1), dim3(64), 0, c->stream, skey, N, ts_shift, out->max_ts);
+    if (check_launch(c, "max_ts")) return -1;
+  }
   uint32_t *nsc = scratch_t<uint32_t>(c, "nsc", N);
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
   uint64_t *link = scratch_t<uint64_t>(c, "link", N);  // u32 or u64 links; room for the yarn sort
@@ -2700,9 +2707,18 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   if (giant) {
     const uint32_t gbits = ceil_log2(2ull * N + 2);
     const uint32_t root_key = gbits >= 32 ? 0xFFFFFFFFu : (1u << gbits) - 1;
-    uint32_t *gkA = scratch_t<uint32_t>(c, "g_keyA", N), *gkB = scratch_t<uint32_t>(c, "g_keyB", N);
-    uint32_t *gvA = scratch_t<uint32_t>(c, "g_valA", N), *gvB = scratch_t<uint32_t>(c, "g_valB", N);
-    uint32_t *gk = scratch_t<uint32_t>(c, "g_key", N);
+    // group keys: sort input in thr (written only after the sort), ping-pong
+    // pairs in the spare buffers when the caller has them
+    uint32_t *gk = thr, *gkA, *gvA, *gkB, *gvB;
+    if (spareA && spareB) {
+      gkA = (uint32_t *)spareA;
+      gvA = gkA + N;
+      gkB = (uint32_t *)spareB;
+      gvB = gkB + N;
+    } else {
+      gkA = scratch_t<uint32_t>(c, "g_keyA", N), gkB = scratch_t<uint32_t>(c, "g_keyB", N);
+      gvA = scratch_t<uint32_t>(c, "g_valA", N), gvB = scratch_t<uint32_t>(c, "g_valB", N);
+    }
     if (!gkA || !gkB || !gvA || !gvB || !gk) return fail(c, "out of device memory (giant tree)");
     const dim3 GN((N + 255) / 256);
     {
@@ -2824,11 +2840,6 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
                          ba2, bb2, Weff, sbase, nullptr, order);
     }
     if (check_launch(c, "rank")) return -1;
-    if (out->max_ts && skey) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
-      hipLaunchKernelGGL(k_max_ts1, dim3(1), dim3(64), 0, c->stream, skey, N, ts_shift,
-                         out->max_ts);
-      if (check_launch(c, "max_ts")) return -1;
-    }
   } else {
     Launch L(c, "rank", (double)t.Wtot * 12);
     hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
@@ -2979,8 +2990,11 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }  // general front end
 
     // 3-9. tree, walk, rank, emit, visibility
+    // without yarns the id-sort buffers are free once the ids are joined
+    const bool spare = !want_yarns;
     if (weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
-                   front_done ? nullptr : skey, bt->ts_shift, out))
+                   front_done ? nullptr : skey, bt->ts_shift, out, spare ? skA : nullptr,
+                   spare ? skB : nullptr))
       return -1;
 
     // 10. yarns: stable partition of the id order by site rank
