@@ -902,7 +902,10 @@ __global__ __launch_bounds__(NT) void k_tree(
     }
   };
   stamp(-1);
-  __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T], ptab[TILE_T];
+  __shared__ uint32_t tkey[TILE_T], trank[TILE_T], tns[TILE_T];
+  // ptab[x] (the group's last node of earlier tiles, by original position) is
+  // read by the thread that then writes tns[x]: the two share one array
+  uint32_t *const ptab = tns;
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
   __shared__ uint32_t run[64];
   // special / hide bit per rank (LDS when the document fits bm_words words)
