@@ -1674,6 +1674,222 @@ __global__ __launch_bounds__(256) void k_emit(
   if (threadIdx.x == 0 && vtotal) atomicAdd(&vcount[d], vtotal);
 }
 
+// --- fused tour for documents of < 2^16 nodes: walk, rank and emit in LDS --------
+// The whole successor list of one document (u16 per node), its render and
+// splitter bits and the sublist tables (u16) stay in LDS, one workgroup per
+// document:
+//   pass 1  every sublist (splitter to splitter) for its length and successor;
+//           each lane runs its own walker state machine and takes the next
+//           sublist from an LDS counter as soon as one ends, so a wave never
+//           waits for its longest walk;
+//   jump    suffix sums over the sublists by pointer jumping -> positions;
+//   pass 2  the same walks again, the node index of every position to HBM
+//           scratch (u16 stores, no load on the walk's path);
+//   pass 3  sval (u16) staged where the successors were, then coalesced over
+//           positions: weave_perm = sval of the node, render byte.
+// Replaces k_walk + k_rank + k_emit and their slot buffer.
+constexpr uint32_t TOUR_END = 0xFFFFu;
+constexpr uint32_t TOUR_LDS_MAX = 159 * 1024;  // dynamic LDS of k_tour (static: < 1 KiB)
+
+__host__ __device__ inline uint32_t tour_lds_bytes(uint32_t nmax, uint32_t log2k) {
+  const uint32_t S = (nmax + (1u << log2k) - 1) >> log2k;
+  // succ u16 (later sval u16), render + splitter bits, acc/nx u16
+  return 4 * ((nmax + 1) / 2 + 2 * ((nmax + 31) / 32) + S);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
+                                             const uint32_t *__restrict__ sval,
+                                             const uint32_t *__restrict__ doc_off,
+                                             const uint32_t *__restrict__ doc_log2k,
+                                             const uint64_t *__restrict__ skey, uint32_t ts_shift,
+                                             uint64_t *__restrict__ max_ts,
+                                             uint32_t *__restrict__ perm, uint8_t *__restrict__ vis8,
+                                             uint32_t *__restrict__ vcount,
+                                             uint32_t *__restrict__ status, uint16_t *inv,
+                                             unsigned long long *__restrict__ tprof) {
+  constexpr uint32_t SPT = 8;  // sublists per thread in the jumping rounds: S <= SPT * NT
+  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
+  __shared__ uint32_t wtot[NT / 64];
+  __shared__ uint32_t bad_s, next_j;
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
+    if (tprof) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tacc[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  stamp(-1);
+  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  if (tid == 0 && max_ts) max_ts[d] = n ? (skey[base + n - 1] >> ts_shift) : 0ull;
+  if (n == 0) return;
+  const uint32_t S = (n + (1u << log2k) - 1) >> log2k, nw = (n + 31) / 32;
+  uint16_t *succ = reinterpret_cast<uint16_t *>(sm);
+  uint32_t *vbm = sm + (n + 1) / 2, *sbm = vbm + nw;
+  uint16_t *acc = reinterpret_cast<uint16_t *>(sbm + nw), *nx = acc + S;
+  if (tid == 0) {
+    bad_s = 0;
+    next_j = NT;  // the first NT walkers are handed out by thread index
+  }
+  // load: successor (SUCC_END -> TOUR_END), render and splitter bits (ballots),
+  // 8 loads in flight per lane
+  constexpr uint32_t LU = 8;
+  for (uint32_t r0 = wv * 64; r0 < n; r0 += NT * LU) {
+    uint32_t L[LU];
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t r = r0 + k * NT + lane;
+      L[k] = r < n ? link[base + r] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t rb = r0 + k * NT, r = rb + lane, u = L[k] & LINK_IDX;
+      if (r < n) succ[r] = (uint16_t)(u < n ? u : TOUR_END);
+      const uint64_t vm = __ballot(r < n && (L[k] & LINK_VIS));
+      const uint64_t sp = __ballot(r < n && (L[k] & LINK_SPLIT));
+      if (lane == 0 && rb < n) {
+        vbm[rb >> 5] = (uint32_t)vm;
+        sbm[rb >> 5] = (uint32_t)sp;
+        if ((rb >> 5) + 1 < nw) {
+          vbm[(rb >> 5) + 1] = (uint32_t)(vm >> 32);
+          sbm[(rb >> 5) + 1] = (uint32_t)(sp >> 32);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(0);
+  auto split_at = [&](uint32_t u) { return (sbm[u >> 5] >> (u & 31)) & 1u; };
+  bool bad = false;
+  // pass 1: per-lane walker state machines over the sublists
+  {
+    uint32_t j = tid, u = 0, cnt = 0;
+    bool live = j < S;
+    if (live) {
+      u = succ[split_node(d, j, log2k, n)];
+      cnt = 1;
+    }
+    while (live) {
+      const bool end = u == TOUR_END || u >= n || split_at(u) || cnt > n;
+      if (end) {
+        bad |= (u != TOUR_END && u >= n) || cnt > n;
+        acc[j] = (uint16_t)min(cnt, 0xFFFFu);
+        nx[j] = (uint16_t)(u < n ? (u >> log2k) : TOUR_END);
+        j = atomicAdd(&next_j, 1u);
+        live = j < S;
+        if (live) {
+          u = succ[split_node(d, j, log2k, n)];
+          cnt = 1;
+        }
+      } else {
+        cnt++;
+        u = succ[u];
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) next_j = NT;
+  stamp(1);
+  // suffix sums along the sublist list by pointer jumping: acc[j] = nodes from
+  // sublist j to the end of the tour (<= n < 2^16)
+  for (uint32_t round = 0; (1u << round) < 2 * S; round++) {
+    uint32_t na[SPT], nn[SPT];
+#pragma unroll
+    for (uint32_t k = 0; k < SPT; k++) {
+      const uint32_t j = tid + k * NT;
+      if (j < S) {
+        const uint32_t q = nx[j];
+        na[k] = acc[j] + (q < S ? acc[q] : 0u);
+        nn[k] = q < S ? nx[q] : TOUR_END;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < SPT; k++) {
+      const uint32_t j = tid + k * NT;
+      if (j < S) {
+        acc[j] = (uint16_t)min(na[k], 0xFFFFu);
+        nx[j] = (uint16_t)nn[k];
+      }
+    }
+    __syncthreads();
+  }
+  stamp(2);
+  if (tid == 0 && acc[0] != n) bad_s = 1;  // the root's sublist starts the tour
+  // pass 2: the node at each position (n - acc[j] onwards) as u16 to HBM
+  // scratch: fire-and-forget stores keep the walk free of load latency
+  {
+    uint32_t j = tid, u = 0, pos = 0;
+    bool live = j < S;
+    if (live) {
+      u = split_node(d, j, log2k, n);
+      pos = n - min((uint32_t)acc[j], n);
+    }
+    while (live) {
+      if (pos < n) inv[base + pos] = (uint16_t)u;
+      else bad = true;
+      pos++;
+      u = succ[u];
+      if (u == TOUR_END || u >= n || split_at(u) || pos >= n) {
+        j = atomicAdd(&next_j, 1u);
+        live = j < S;
+        if (live) {
+          u = split_node(d, j, log2k, n);
+          pos = n - min((uint32_t)acc[j], n);
+        }
+      }
+    }
+  }
+  // the stores above are read below by other waves of this workgroup (one CU,
+  // one L1; the lines were not cached before): the barrier orders them
+  __syncthreads();
+  stamp(3);
+  // pass 3: sval as u16 where the successors were, then coalesced over positions
+  uint16_t *sv = succ;
+  for (uint32_t r0 = tid; r0 < n; r0 += NT * LU) {
+    uint32_t x[LU];
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t r = r0 + k * NT;
+      x[k] = r < n ? (sval ? sval[base + r] : r) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++)
+      if (r0 + k * NT < n) sv[r0 + k * NT] = (uint16_t)x[k];
+  }
+  __syncthreads();
+  uint32_t nvis = 0;
+  for (uint32_t g0 = tid; g0 < n; g0 += LU * NT) {
+    uint32_t u8[LU];
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t g = g0 + k * NT;
+      u8[k] = g < n ? inv[base + g] : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t g = g0 + k * NT, u = u8[k] < n ? u8[k] : 0u;
+      if (g < n) {
+        const uint32_t v = (vbm[u >> 5] >> (u & 31)) & 1u;
+        perm[base + g] = sv[u];
+        vis8[base + g] = (uint8_t)v;
+        nvis += v;
+      }
+    }
+  }
+  uint32_t total;
+  block_exscan<NT>(nvis, wtot, &total);
+  if (__syncthreads_or(bad) || bad_s) {
+    if (tid == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
+  }
+  if (tid == 0) vcount[d] = total;
+  stamp(4);
+  if (tprof && tid == 0)
+    for (int ph = 0; ph < 6; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+}
+
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
                                                    uint32_t *__restrict__ bits) {
   const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2285,6 +2501,7 @@ struct cw_ctx {
     uint32_t T = 0, Wtot = 0, Bw = 0, Be = 0, nmax = 0, Btot = 0, Wmax = 0, Wofftot = 0;
     uint32_t pack_dmax = 0;  // most documents in one sort pack (k_pack_sort)
     uint64_t slots = 0;
+    bool tour = false;       // every document goes through k_tour (LDS walk + rank + emit)
   } tab;
   bool tab_on_device = false;
   bool last_giant = false;
@@ -2299,6 +2516,8 @@ struct cw_ctx {
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 20;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
+  uint32_t tour = 1;               // CW_TOUR: fused LDS tour for documents of < 2^16 nodes
+  uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
 };
 
 namespace {
@@ -2430,6 +2649,12 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
   uint32_t wtot = 0, stot = 0;
   t.nmax = 0;
   t.Wmax = 0;
+  uint64_t nmax = 0;
+  for (uint64_t d = 0; d < D; d++) nmax = std::max<uint64_t>(nmax, off[d + 1] - off[d]);
+  // the fused LDS tour: documents of < 2^16 nodes whose list fits the LDS
+  t.tour = c->tour && !giant && nmax <= TOUR_END &&
+           tour_lds_bytes((uint32_t)nmax, c->tour_log2k) <= TOUR_LDS_MAX &&
+           ((nmax + (1u << c->tour_log2k) - 1) >> c->tour_log2k) <= 8 * 1024;
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
     t.doc_off[d] = b;
@@ -2446,7 +2671,7 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     }
     // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
-    uint32_t log2k = c->min_log2k, log2cap = c->min_log2cap;
+    uint32_t log2k = t.tour ? c->tour_log2k : c->min_log2k, log2cap = c->min_log2cap;
     auto subl = [&]() {
       return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
@@ -2792,75 +3017,105 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
             acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
   }
 
-  // 6. walk: sublists of the preorder successor list
-  HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
-  {
-    Launch L(c, "walk", (double)N * (4 + 4));
-    hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
-                       c->walk_lds, c->stream, (const void *)link, thr,
-                       dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
-                       dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
-                       (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
-                       out->status, c->walk_span);
-  }
-  if (check_launch(c, "walk")) return -1;
-
-  // 7. rank sublists (+ max lamport-ts per document)
-  if (giant) {
-    if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-    HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
-    // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
-    const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
-    uint32_t K3 = 1;
-    while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
-    const uint32_t S3 = (S2 + K3 - 1) / K3;
-    const bool three = K3 > 1;
-    uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
-    uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
-    uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
-    if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
-    uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
-    uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
-             *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
+  if (t.tour && !giant) {
+    // 6-8. walk, rank and emit of every document in LDS
+    unsigned long long *tprof = nullptr;
+    if (c->tree_prof) {
+      tprof = scratch_t<unsigned long long>(c, "tprof2", (size_t)D * 8);
+      HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
+    }
+    uint16_t *inv = scratch_t<uint16_t>(c, "tour_inv", N);
+    if (!inv) return fail(c, "out of device memory (tour)");
     {
-      Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
-      hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
-                         wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
-      if (three) {
-        hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
-                           S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
-        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
-                           sn3, S3, N, Weff, nb3, tb3, out->status);
-        hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
-                           nb3, tb3, S2, ba2, bb2, nullptr);
-      } else {
-        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
-                           sn2, S2, N, Weff, ba2, bb2, out->status);
+      Launch L(c, "tour", (double)N * (4 + 4 + 4 + 1 + 2 + 2));
+      hipLaunchKernelGGL(k_tour<1024>, dim3((uint32_t)D), dim3(1024),
+                         (size_t)tour_lds_bytes(t.nmax, c->tour_log2k), c->stream,
+                         (const uint32_t *)link, sval, doc_off, doc_log2k, skey, ts_shift,
+                         skey ? out->max_ts : nullptr, out->weave_perm, vis8, out->visible_count,
+                         out->status, inv, tprof);
+    }
+    if (check_launch(c, "tour")) return -1;
+    if (tprof) {
+      std::vector<unsigned long long> h((size_t)D * 8);
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(h.data(), tprof, (size_t)D * 64, hipMemcpyDeviceToHost));
+      double a[6] = {0};
+      for (uint64_t d = 0; d < D; d++)
+        for (int ph = 0; ph < 6; ph++) a[ph] += (double)h[d * 8 + ph];
+      fprintf(stderr, "tour phases (memtime ticks per doc): load %.0f pass1 %.0f jump %.0f pass2 %.0f "
+              "pass3 %.0f\n", a[0] / D, a[1] / D, a[2] / D, a[3] / D, a[4] / D);
+    }
+  } else {
+    // 6. walk: sublists of the preorder successor list
+    HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
+    {
+      Launch L(c, "walk", (double)N * (4 + 4));
+      hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
+                         c->walk_lds, c->stream, (const void *)link, thr,
+                         dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
+                         dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
+                         out->status, c->walk_span);
+    }
+    if (check_launch(c, "walk")) return -1;
+
+    // 7. rank sublists (+ max lamport-ts per document)
+    if (giant) {
+      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
+      // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
+      const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
+      uint32_t K3 = 1;
+      while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
+      const uint32_t S3 = (S2 + K3 - 1) / K3;
+      const bool three = K3 > 1;
+      uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
+      uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
+      uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
+      if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
+      uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
+      uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
+               *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
+      {
+        Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
+        hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
+                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
+        if (three) {
+          hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
+                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
+          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
+                             sn3, S3, N, Weff, nb3, tb3, out->status);
+          hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
+                             nb3, tb3, S2, ba2, bb2, nullptr);
+        } else {
+          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
+                             sn2, S2, N, Weff, ba2, bb2, out->status);
+        }
+        hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
+                           ba2, bb2, Weff, sbase, nullptr, order);
       }
-      hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
-                         ba2, bb2, Weff, sbase, nullptr, order);
+      if (check_launch(c, "rank")) return -1;
+    } else {
+      Launch L(c, "rank", (double)t.Wtot * 12);
+      hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
+                         wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, ts_shift, sbase,
+                         order, skey ? out->max_ts : nullptr, out->status);
     }
     if (check_launch(c, "rank")) return -1;
-  } else {
-    Launch L(c, "rank", (double)t.Wtot * 12);
-    hipLaunchKernelGGL(k_rank, dim3((uint32_t)D), B256, (size_t)t.Wmax * 8, c->stream, wcnt,
-                       wnext, walk_first, doc_W, dyn_ctr, doc_off, skey, ts_shift, sbase,
-                       order, skey ? out->max_ts : nullptr, out->status);
-  }
-  if (check_launch(c, "rank")) return -1;
 
-  // 8. emit
-  {
-    Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
-    hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
-                       (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
-                       dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
-                       dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
-                       out->visible_count, out->status);
+    // 8. emit
+    {
+      Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
+      hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
+                         dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
+                         dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
+                         out->visible_count, out->status);
+    }
+    if (check_launch(c, "emit")) return -1;
   }
-  if (check_launch(c, "emit")) return -1;
 
   // 9. visibility bitmap
   if (out->visible_bits) {
@@ -3854,6 +4109,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 20);
+  c->tour = knob("CW_TOUR", 1);
+  c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

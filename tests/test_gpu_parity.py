@@ -22,7 +22,8 @@ pytestmark = pytest.mark.gpu
 # Front ends: "front" = rank directories for every document (CW_FRONT_MIN_AVG=0
 # also sends tiny documents through it), "radix" = segmented radix sort + join.
 FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"}, "radix": {"CW_FRONT": "0"},
-          "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"}}  # no LDS pack sorts
+          "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"},  # no LDS pack sorts
+          "hbm-walk": {"CW_TOUR": "0"}}  # walk + rank + emit instead of the LDS tour
 
 
 @pytest.fixture(scope="module", params=sorted(FRONTS))
@@ -238,9 +239,13 @@ def test_duplicate_ids_beside_clean_documents(weaver):
         assert np.array_equal(gvis[b:e], vis[b:e])
 
 
-KNOBS = [{}, {"CW_LOG2CAP": "5"}, {"CW_LOG2K": "4", "CW_LOG2CAP": "5"},
-         {"CW_MAX_DIGIT": "8"}, {"CW_WALK_THREADS": "256", "CW_WALK_SPAN": "512"},
-         {"CW_WALK_THREADS": "1024", "CW_WALK_SPAN": "2048"},
+# walk / slot geometry only matters on the HBM walk path (CW_TOUR=0); the
+# fused LDS tour takes its own splitter density (CW_TOUR_LOG2K)
+_W = {"CW_TOUR": "0"}
+KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2CAP="5"),
+         {"CW_MAX_DIGIT": "8"}, dict(_W, CW_WALK_THREADS="256", CW_WALK_SPAN="512"),
+         dict(_W, CW_WALK_THREADS="1024", CW_WALK_SPAN="2048"),
+         {"CW_TOUR_LOG2K": "3"}, {"CW_TOUR_LOG2K": "4"}, {"CW_TOUR_LOG2K": "7"},
          {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"}, {"CW_TREE": "0"}, {"CW_TREE": "1"}]
 
 
@@ -257,7 +262,7 @@ def test_config2_documents_any_geometry(knobs, monkeypatch):
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"CW_LOG2CAP": "5"}], ids=["default", "cap32"])
+@pytest.mark.parametrize("knobs", [{}, {"CW_TOUR": "0"}], ids=["default", "hbm-walk"])
 def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
     """The whole bench workload (10,000 config-2 documents, 5e8 nodes) against
     the oracle, every document, plus permutation validity."""
