@@ -1678,16 +1678,16 @@ __global__ __launch_bounds__(256) void k_emit(
 // The whole successor list of one document (u16 per node), its render and
 // splitter bits and the sublist tables (u16) stay in LDS, one workgroup per
 // document:
-//   pass 1  every sublist (splitter to splitter) for its length and successor;
-//           each lane runs its own walker state machine and takes the next
-//           sublist from an LDS counter as soon as one ends, so a wave never
-//           waits for its longest walk;
-//   jump    suffix sums over the sublists by pointer jumping -> positions;
-//   pass 2  the same walks again, the node index of every position to HBM
-//           scratch (u16 stores, no load on the walk's path);
-//   pass 3  sval (u16) staged where the successors were, then coalesced over
-//           positions: weave_perm = sval of the node, render byte.
-// Replaces k_walk + k_rank + k_emit and their slot buffer.
+//   walk   every sublist (splitter to splitter) for its length and successor
+//          sublist; each lane runs its own walker state machine and takes the
+//          next sublist from an LDS counter as soon as one ends (a wave never
+//          waits for its longest walk); each node's (sublist, index) goes to
+//          HBM scratch with fire-and-forget stores;
+//   jump   suffix sums over the sublists by pointer jumping -> sublist bases;
+//   place  coalesced over nodes: position = base + index, sval (u16) into an
+//          LDS weave where the successors were, render bits by position;
+//   write  weave_perm and render bytes, coalesced.
+// Replaces k_walk + k_rank + k_emit and their slot buffer in HBM.
 constexpr uint32_t TOUR_END = 0xFFFFu;
 constexpr uint32_t TOUR_LDS_MAX = 159 * 1024;  // dynamic LDS of k_tour (static: < 1 KiB)
 
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
                                              uint64_t *__restrict__ max_ts,
                                              uint32_t *__restrict__ perm, uint8_t *__restrict__ vis8,
                                              uint32_t *__restrict__ vcount,
-                                             uint32_t *__restrict__ status, uint16_t *inv,
+                                             uint32_t *__restrict__ status, uint32_t *loc,
                                              unsigned long long *__restrict__ tprof) {
   constexpr uint32_t SPT = 8;  // sublists per thread in the jumping rounds: S <= SPT * NT
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
@@ -1763,12 +1763,15 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   stamp(0);
   auto split_at = [&](uint32_t u) { return (sbm[u >> 5] >> (u & 31)) & 1u; };
   bool bad = false;
-  // pass 1: per-lane walker state machines over the sublists
+  // pass 1: per-lane walker state machines over the sublists; every node's
+  // (sublist, index inside it) goes to HBM scratch (fire-and-forget stores)
   {
     uint32_t j = tid, u = 0, cnt = 0;
     bool live = j < S;
     if (live) {
-      u = succ[split_node(d, j, log2k, n)];
+      const uint32_t v = split_node(d, j, log2k, n);
+      loc[base + v] = j << 16;
+      u = succ[v];
       cnt = 1;
     }
     while (live) {
@@ -1780,10 +1783,13 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
         j = atomicAdd(&next_j, 1u);
         live = j < S;
         if (live) {
-          u = succ[split_node(d, j, log2k, n)];
+          const uint32_t v = split_node(d, j, log2k, n);
+          loc[base + v] = j << 16;
+          u = succ[v];
           cnt = 1;
         }
       } else {
+        loc[base + u] = (j << 16) | cnt;
         cnt++;
         u = succ[u];
       }
@@ -1818,66 +1824,45 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   }
   stamp(2);
   if (tid == 0 && acc[0] != n) bad_s = 1;  // the root's sublist starts the tour
-  // pass 2: the node at each position (n - acc[j] onwards) as u16 to HBM
-  // scratch: fire-and-forget stores keep the walk free of load latency
-  {
-    uint32_t j = tid, u = 0, pos = 0;
-    bool live = j < S;
-    if (live) {
-      u = split_node(d, j, log2k, n);
-      pos = n - min((uint32_t)acc[j], n);
-    }
-    while (live) {
-      if (pos < n) inv[base + pos] = (uint16_t)u;
-      else bad = true;
-      pos++;
-      u = succ[u];
-      if (u == TOUR_END || u >= n || split_at(u) || pos >= n) {
-        j = atomicAdd(&next_j, 1u);
-        live = j < S;
-        if (live) {
-          u = split_node(d, j, log2k, n);
-          pos = n - min((uint32_t)acc[j], n);
-        }
-      }
-    }
-  }
-  // the stores above are read below by other waves of this workgroup (one CU,
-  // one L1; the lines were not cached before): the barrier orders them
+  // place: coalesced over nodes, position = sublist base + index; the weave
+  // (sval as u16) and its render bits are assembled in LDS where the
+  // successors and splitter bits were, then written out coalesced.  (The
+  // scratch stores above are read by other waves of this workgroup: one CU,
+  // one L1, lines not cached before; the barriers order them.)
+  uint16_t *out = succ;
+  uint32_t *pvis = sbm;
+  for (uint32_t w = tid; w < nw; w += NT) pvis[w] = 0;
   __syncthreads();
-  stamp(3);
-  // pass 3: sval as u16 where the successors were, then coalesced over positions
-  uint16_t *sv = succ;
   for (uint32_t r0 = tid; r0 < n; r0 += NT * LU) {
-    uint32_t x[LU];
+    uint32_t lc[LU], x[LU];
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT;
+      lc[k] = r < n ? loc[base + r] : 0u;
       x[k] = r < n ? (sval ? sval[base + r] : r) : 0u;
     }
 #pragma unroll
-    for (uint32_t k = 0; k < LU; k++)
-      if (r0 + k * NT < n) sv[r0 + k * NT] = (uint16_t)x[k];
+    for (uint32_t k = 0; k < LU; k++) {
+      const uint32_t r = r0 + k * NT;
+      if (r >= n) continue;
+      const uint32_t j = lc[k] >> 16;
+      const uint32_t pos = (j < S ? n - min((uint32_t)acc[j], n) : n) + (lc[k] & 0xFFFFu);
+      if (pos >= n) {
+        bad = true;
+        continue;
+      }
+      out[pos] = (uint16_t)x[k];
+      if ((vbm[r >> 5] >> (r & 31)) & 1u) atomicOr(&pvis[pos >> 5], 1u << (pos & 31));
+    }
   }
   __syncthreads();
+  stamp(3);
   uint32_t nvis = 0;
-  for (uint32_t g0 = tid; g0 < n; g0 += LU * NT) {
-    uint32_t u8[LU];
-#pragma unroll
-    for (uint32_t k = 0; k < LU; k++) {
-      const uint32_t g = g0 + k * NT;
-      u8[k] = g < n ? inv[base + g] : 0u;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < LU; k++) {
-      const uint32_t g = g0 + k * NT, u = u8[k] < n ? u8[k] : 0u;
-      if (g < n) {
-        const uint32_t v = (vbm[u >> 5] >> (u & 31)) & 1u;
-        perm[base + g] = sv[u];
-        vis8[base + g] = (uint8_t)v;
-        nvis += v;
-      }
-    }
+  for (uint32_t g = tid; g < n; g += NT) {
+    const uint32_t v = (pvis[g >> 5] >> (g & 31)) & 1u;
+    perm[base + g] = out[g];
+    vis8[base + g] = (uint8_t)v;
+    nvis += v;
   }
   uint32_t total;
   block_exscan<NT>(nvis, wtot, &total);
@@ -3024,15 +3009,15 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       tprof = scratch_t<unsigned long long>(c, "tprof2", (size_t)D * 8);
       HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
     }
-    uint16_t *inv = scratch_t<uint16_t>(c, "tour_inv", N);
-    if (!inv) return fail(c, "out of device memory (tour)");
+    uint32_t *loc = scratch_t<uint32_t>(c, "tour_loc", N);
+    if (!loc) return fail(c, "out of device memory (tour)");
     {
-      Launch L(c, "tour", (double)N * (4 + 4 + 4 + 1 + 2 + 2));
+      Launch L(c, "tour", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
       hipLaunchKernelGGL(k_tour<1024>, dim3((uint32_t)D), dim3(1024),
                          (size_t)tour_lds_bytes(t.nmax, c->tour_log2k), c->stream,
                          (const uint32_t *)link, sval, doc_off, doc_log2k, skey, ts_shift,
                          skey ? out->max_ts : nullptr, out->weave_perm, vis8, out->visible_count,
-                         out->status, inv, tprof);
+                         out->status, loc, tprof);
     }
     if (check_launch(c, "tour")) return -1;
     if (tprof) {
@@ -3042,8 +3027,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       double a[6] = {0};
       for (uint64_t d = 0; d < D; d++)
         for (int ph = 0; ph < 6; ph++) a[ph] += (double)h[d * 8 + ph];
-      fprintf(stderr, "tour phases (memtime ticks per doc): load %.0f pass1 %.0f jump %.0f pass2 %.0f "
-              "pass3 %.0f\n", a[0] / D, a[1] / D, a[2] / D, a[3] / D, a[4] / D);
+      fprintf(stderr, "tour phases (memtime ticks per doc): load %.0f walk %.0f jump %.0f place %.0f "
+              "write %.0f\n", a[0] / D, a[1] / D, a[2] / D, a[3] / D, a[4] / D);
     }
   } else {
     // 6. walk: sublists of the preorder successor list
