@@ -604,11 +604,13 @@ __device__ __forceinline__ uint32_t fr_rank(const uint4 *__restrict__ dir, uint3
   return q.x + (w > 0 ? __popc(q.y) : 0u) + (w > 1 ? __popc(q.z) : 0u) + __popc(wv & (m - 1));
 }
 
-// One workgroup per document: key range (min/max), bitmap in LDS (a bit set
-// twice is a duplicate id, shared.cljc:166-171), group prefix counts, copy to
-// the document's directory slot.  Also ::lamport-ts = max ts (refresh-ts,
-// shared.cljc:243-249).  A range wider than a slot marks the document FR_BIG
-// and counts it in big[0]; big[1] = the largest group count.
+// One workgroup per document, one pass over its ids: bitmap in LDS over the
+// key range [0, slot) (a bit set twice is a duplicate id, shared.cljc:166-171;
+// the root [0 "0" 0] is the smallest id, so the range starts at 0 in every
+// well-formed document), the largest id (::lamport-ts = max ts, refresh-ts,
+// shared.cljc:243-249), group prefix counts, copy to the document's directory
+// slot.  An id past the slot marks the document FR_BIG and counts it in
+// big[0]; big[1] = the largest group count.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key,
                                              const uint32_t *__restrict__ doc_off,
@@ -619,7 +621,7 @@ __global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key
                                              uint32_t *__restrict__ status,
                                              uint32_t *__restrict__ big) {
   extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
-  __shared__ uint64_t rmin[NT / 64], rmax[NT / 64];
+  __shared__ uint64_t rmax[NT / 64];
   __shared__ uint32_t wtot[NT / 64];
   const uint32_t d = blockIdx.x, tid = threadIdx.x, base = doc_off[d];
   const uint32_t n = doc_off[d + 1] - base;
@@ -627,55 +629,55 @@ __global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key
     if (tid == 0) dgroups[d] = 0;
     return;
   }
-  uint64_t mn = ~0ull, mx = 0;
-  for (uint32_t i = tid; i < n; i += NT) {
-    const uint64_t k = id_key[base + i];
-    mn = min(mn, k);
-    mx = max(mx, k);
+  for (uint32_t g = tid; g < slot_groups; g += NT) sdir[g] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
+  const uint64_t lim = (uint64_t)slot_groups * FR_GROUP_BITS;
+  uint64_t mx = 0;
+  bool dup = false, far = false;
+  constexpr uint32_t U = 4;
+  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+    uint64_t x[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      x[u] = i < n ? id_key[base + i] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      if (i0 + u * NT >= n) continue;
+      mx = max(mx, x[u]);
+      if (x[u] >= lim) {
+        far = true;
+        continue;
+      }
+      const uint32_t xi = (uint32_t)x[u];
+      const uint32_t g = xi / FR_GROUP_BITS, b = xi - g * FR_GROUP_BITS, m = 1u << (b & 31);
+      const uint32_t old = atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
+      dup |= (old & m) != 0;
+    }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    mn = min(mn, (uint64_t)__shfl_xor(mn, o, 64));
-    mx = max(mx, (uint64_t)__shfl_xor(mx, o, 64));
-  }
-  if ((tid & 63) == 0) {
-    rmin[tid >> 6] = mn;
-    rmax[tid >> 6] = mx;
-  }
-  __syncthreads();
-  mn = rmin[0];
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, o, 64));
+  if ((tid & 63) == 0) rmax[tid >> 6] = mx;
+  const bool any_far = __syncthreads_or(far);
   mx = rmax[0];
 #pragma unroll
-  for (int w = 1; w < NT / 64; w++) {
-    mn = min(mn, rmin[w]);
-    mx = max(mx, rmax[w]);
-  }
+  for (int w = 1; w < NT / 64; w++) mx = max(mx, rmax[w]);
   if (tid == 0 && max_ts) max_ts[d] = mx >> ts_shift;
-  const uint64_t span = mx - mn;  // R - 1
-  if (span >= (uint64_t)slot_groups * FR_GROUP_BITS) {
+  if (any_far) {
     if (tid == 0) {
       dgroups[d] = FR_BIG;
       atomicAdd(&big[0], 1u);
     }
     return;
   }
-  const uint32_t G = (uint32_t)(span / FR_GROUP_BITS) + 1;
+  const uint32_t G = (uint32_t)(mx / FR_GROUP_BITS) + 1;
   if (tid == 0) {
-    dkmin[d] = mn;
+    dkmin[d] = 0;
     dgroups[d] = G;
     atomicMax(&big[1], G);
   }
-  for (uint32_t g = tid; g < G; g += NT) sdir[g] = make_uint4(0u, 0u, 0u, 0u);
-  __syncthreads();
-  uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
-  bool dup = false;
-  for (uint32_t i = tid; i < n; i += NT) {
-    const uint32_t x = (uint32_t)(id_key[base + i] - mn);
-    const uint32_t g = x / FR_GROUP_BITS, b = x - g * FR_GROUP_BITS, m = 1u << (b & 31);
-    const uint32_t old = atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
-    dup |= (old & m) != 0;
-  }
-  __syncthreads();
   // group prefix counts: each thread owns a contiguous run of groups
   const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
   uint32_t cnt = 0;
