@@ -2489,6 +2489,7 @@ struct cw_ctx {
     uint32_t pack_dmax = 0;  // most documents in one sort pack (k_pack_sort)
     uint64_t slots = 0;
     bool tour = false;       // every document goes through k_tour (LDS walk + rank + emit)
+    uint32_t tour_log2k = 3;  // its splitter blocks
   } tab;
   bool tab_on_device = false;
   bool last_giant = false;
@@ -2639,9 +2640,15 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
   uint64_t nmax = 0;
   for (uint64_t d = 0; d < D; d++) nmax = std::max<uint64_t>(nmax, off[d + 1] - off[d]);
   // the fused LDS tour: documents of < 2^16 nodes whose list fits the LDS
-  t.tour = c->tour && !giant && nmax <= TOUR_END &&
-           tour_lds_bytes((uint32_t)nmax, c->tour_log2k) <= TOUR_LDS_MAX &&
-           ((nmax + (1u << c->tour_log2k) - 1) >> c->tour_log2k) <= 8 * 1024;
+  // (the splitter blocks grow until the tables fit next to the successors)
+  t.tour = false;
+  t.tour_log2k = c->tour_log2k;
+  if (c->tour && !giant && nmax <= TOUR_END) {
+    while (t.tour_log2k < 8 && (tour_lds_bytes((uint32_t)nmax, t.tour_log2k) > TOUR_LDS_MAX ||
+                                ((nmax + (1u << t.tour_log2k) - 1) >> t.tour_log2k) > 8 * 1024))
+      t.tour_log2k++;
+    t.tour = tour_lds_bytes((uint32_t)nmax, t.tour_log2k) <= TOUR_LDS_MAX;
+  }
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
     t.doc_off[d] = b;
@@ -2658,7 +2665,7 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     }
     // splitter block size K = 2^log2k and slot capacity 2^log2cap: static
     // sublists 2*ceil(n/K) plus continued ones (<= ceil(n/cap)) fit the LDS rank
-    uint32_t log2k = t.tour ? c->tour_log2k : c->min_log2k, log2cap = c->min_log2cap;
+    uint32_t log2k = t.tour ? t.tour_log2k : c->min_log2k, log2cap = c->min_log2cap;
     auto subl = [&]() {
       return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
@@ -3016,7 +3023,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     {
       Launch L(c, "tour", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
       hipLaunchKernelGGL(k_tour<1024>, dim3((uint32_t)D), dim3(1024),
-                         (size_t)tour_lds_bytes(t.nmax, c->tour_log2k), c->stream,
+                         (size_t)tour_lds_bytes(t.nmax, t.tour_log2k), c->stream,
                          (const uint32_t *)link, sval, doc_off, doc_log2k, skey, ts_shift,
                          skey ? out->max_ts : nullptr, out->weave_perm, vis8, out->visible_count,
                          out->status, loc, tprof);

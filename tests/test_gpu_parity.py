@@ -249,6 +249,21 @@ KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2C
          {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"}, {"CW_TREE": "0"}, {"CW_TREE": "1"}]
 
 
+@pytest.mark.parametrize("n", [59_204, 60_000, 65_534, 65_535])
+def test_tour_document_size_limits(n):
+    """Documents at the fused tour's limits: the splitter blocks grow so the
+    LDS tables fit (n = 65,535 is the largest u16 document; 65,536 nodes with
+    the root go through the HBM walk)."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n - 1)
+    off, idk, ck, kd = gen.generate(spec, 0, 3)
+    with abi.Weaver(0) as w:
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n)
+    off, idk, ck, kd = gen.generate(spec, 0, 2)
+    with abi.Weaver(0) as w:
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+
+
 @pytest.mark.parametrize("knobs", KNOBS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()) or "default")
 def test_config2_documents_any_geometry(knobs, monkeypatch):
     """Full-size config-2 documents (50,001 nodes) under every launch geometry
