@@ -2431,13 +2431,25 @@ __global__ __launch_bounds__(1024) void k_scan_add(uint32_t *__restrict__ out, u
 __global__ __launch_bounds__(256) void k_seg_off(const uint32_t *__restrict__ seg_start, uint32_t S,
                                                  uint32_t N, uint64_t *__restrict__ seg_off,
                                                  uint32_t *__restrict__ maxlen) {
-  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
-  if (sg > S) return;
-  const uint64_t o = sg < S ? (uint64_t)seg_start[sg] + sg : (uint64_t)N + S;
-  seg_off[sg] = o;
-  if (sg < S) {
-    const uint32_t e = sg + 1 < S ? seg_start[sg + 1] + sg + 1 : N + S;
-    atomicMax(maxlen, (uint32_t)(e - o));
+  // grid-stride over a fixed grid, one atomic per block: atomics on one word
+  // serialise (a per-segment atomic took 7.5 ms for config 4's 4.2e7 key weaves)
+  __shared__ uint32_t wmax[4];
+  uint32_t len = 0;
+  for (uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x; sg <= S; sg += gridDim.x * blockDim.x) {
+    const uint64_t o = sg < S ? (uint64_t)seg_start[sg] + sg : (uint64_t)N + S;
+    seg_off[sg] = o;
+    if (sg < S) {
+      const uint32_t e = sg + 1 < S ? seg_start[sg + 1] + sg + 1 : N + S;
+      len = max(len, (uint32_t)(e - o));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) len = max(len, (uint32_t)__shfl_xor(len, o, 64));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = len;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+    if (m) atomicMax(maxlen, m);
   }
 }
 
@@ -3745,13 +3757,19 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
                        lcause, lkind, lmap);
   }
   if (check_launch(c, "m_segbuild")) return -1;
-  hipLaunchKernelGGL(k_seg_roots, dim3((uint32_t)((S + 255) / 256)), dim3(256), 0, c->stream,
-                     seg_start, (uint32_t)S, lid, lcause, lkind, lmap);
+  {
+    Launch L(c, "m_segroots", (double)S * 25);
+    hipLaunchKernelGGL(k_seg_roots, dim3((uint32_t)((S + 255) / 256)), dim3(256), 0, c->stream,
+                       seg_start, (uint32_t)S, lid, lcause, lkind, lmap);
+  }
   if (check_launch(c, "m_segroots")) return -1;
 
   // key weave s = list document [seg_start[s] + s, seg_start[s+1] + s + 1)
-  hipLaunchKernelGGL(k_seg_off, dim3((uint32_t)((S + 256) / 256)), dim3(256), 0, c->stream,
-                     seg_start, (uint32_t)S, N, seg_off, small + 1);
+  {
+    Launch L(c, "m_segoff", (double)S * 12);
+    hipLaunchKernelGGL(k_seg_off, dim3((uint32_t)std::min<uint64_t>((S + 256) / 256, 2048)), dim3(256),
+                       0, c->stream, seg_start, (uint32_t)S, N, seg_off, small + 1);
+  }
   if (check_launch(c, "m_segoff")) return -1;
   HIPCHK(c, hipMemcpyAsync(c->pin_small, small + 1, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
