@@ -3200,7 +3200,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       if (!dir || !dkmin || !dgroups || !big) return fail(c, "out of device memory (rank directory)");
       HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
       {
-        Launch L(c, "fdir", (double)N * 16 + (double)N / 6.0 * 1.0);
+        Launch L(c, "fdir", (double)N * 8 + (double)N / 6.0 * 1.0);  // ids once + directory
         hipLaunchKernelGGL(k_fdir<1024>, dim3((uint32_t)D), dim3(1024), (size_t)SG * 16, c->stream,
                            id_key, doc_off, SG, dir, dkmin, dgroups, out->max_ts, bt->ts_shift,
                            out->status, big);
