@@ -195,6 +195,7 @@ class Weaver:
         if rc != 0 or not h:
             raise WeaveError(f"cw_ctx_create(device={device}) failed: no usable HIP device")
         self._h = h
+        self.device = device
 
     def close(self):
         if getattr(self, "_h", None):
@@ -285,6 +286,23 @@ class Weaver:
     def sort_keys_device(self, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr):
         self._check(self._L.cw_sort_keys(self._h, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr),
                     "cw_sort_keys")
+
+    def sort_keys(self, keys, key_bits=0):
+        """Host arrays: (sorted keys, input index of each) through cw_sort_keys
+        (device buffers from torch; the call is synchronous)."""
+        import torch
+
+        k = np.ascontiguousarray(keys, np.uint64)
+        n = len(k)
+        if n == 0:
+            return k.copy(), np.zeros(0, np.uint32)
+        dev = torch.device("cuda", self.device)
+        kin = torch.from_numpy(k.view(np.int64)).to(dev)
+        kout = torch.empty_like(kin)
+        iout = torch.empty(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize(dev)
+        self.sort_keys_device(kin.data_ptr(), n, key_bits, kout.data_ptr(), iout.data_ptr())
+        return kout.cpu().numpy().view(np.uint64), iout.cpu().numpy().view(np.uint32)
 
     def lookup_keys_device(self, sorted_ptr, n, q_ptr, m, base, out_ptr):
         self._check(self._L.cw_lookup_keys(self._h, sorted_ptr, n, q_ptr, m, base, out_ptr),
