@@ -412,7 +412,7 @@ def main():
     # PCIe-inclusive rate (not the headline value): inputs from pinned host
     # buffers, the weave, weave_perm + visible bits back, serialised
     e2e = None
-    if a.config == 2 and not a.no_h2d:
+    if a.config == 2 and not a.no_h2d and world == 1:  # (N > 1: 8.5 GB pinned per rank)
         h_in = [torch.from_numpy(x).pin_memory() for x in
                 (idk.view(np.int64), ck.view(np.int64), kd)]
         h_perm = torch.empty(N, dtype=torch.int32).pin_memory()
