@@ -2525,7 +2525,7 @@ struct cw_ctx {
   uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
-  uint32_t giant_min = 1u << 20;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
+  uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
   uint32_t tour = 1;               // CW_TOUR: fused LDS tour for documents of < 2^16 nodes
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
 };
@@ -4134,7 +4134,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_pad = knob("CW_TREE_PAD", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->pack_sort = knob("CW_PACK_SORT", 1);
-  c->giant_min = knob("CW_GIANT_MIN", 1u << 20);
+  c->giant_min = knob("CW_GIANT_MIN", 1u << 16);
   c->tour = knob("CW_TOUR", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
