@@ -2939,16 +2939,23 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *fcN = scratch_t<uint32_t>(c, "fcN", N);
   uint64_t *link = scratch_t<uint64_t>(c, "link", N);  // u32 or u64 links; room for the yarn sort
   uint32_t *thr = scratch_t<uint32_t>(c, "thr", N);
-  uint32_t *slots = scratch_t<uint32_t>(c, "slots", t.slots);
-  uint32_t *dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
   uint8_t *vis8 = scratch_t<uint8_t>(c, "vis8", (size_t)N + 64);
-  uint32_t *wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
-  uint32_t *wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
-  uint32_t *sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
-  uint32_t *order = scratch_t<uint32_t>(c, "order", t.Wtot);
-  if (!nsc || !fcS || !fcN || !link || !thr || !slots || !dyn_ctr || !vis8 || !wcnt || !wnext ||
-      !sbase || !order)
+  if (!nsc || !fcS || !fcN || !link || !thr || !vis8)
     return fail(c, "out of device memory (N=%u)", N);
+  // the HBM walk's sublist buffers (the fused tour keeps its sublists in LDS)
+  const bool hbm_walk = !(t.tour && !giant);
+  uint32_t *slots = nullptr, *dyn_ctr = nullptr, *wcnt = nullptr, *wnext = nullptr,
+           *sbase = nullptr, *order = nullptr;
+  if (hbm_walk) {
+    slots = scratch_t<uint32_t>(c, "slots", t.slots);
+    dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
+    wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
+    wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
+    sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
+    order = scratch_t<uint32_t>(c, "order", t.Wtot);
+    if (!slots || !dyn_ctr || !wcnt || !wnext || !sbase || !order)
+      return fail(c, "out of device memory (walk, N=%u)", N);
+  }
   uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
   uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
   // 3-5. effective parents, sibling order, links
