@@ -794,6 +794,7 @@ __global__ __launch_bounds__(NT) void k_frank(
 }
 
 constexpr uint32_t KBM_WORDS = 2 * TILE / 32;  // per tile: special bits, then hide bits
+constexpr uint32_t FRONT_FUSED_SG = 2560;       // k_front's directory: 40 KiB, 245,760 keys
 
 // Pass 2, one block per window (window w of document d covers ranks
 // [4096 w, 4096 (w+1)), the ranks of tile w): gather the window's records from
@@ -872,6 +873,203 @@ __global__ __launch_bounds__(NT) void k_fplace(
       o[TILE / 32 + 1] = (uint32_t)(hm >> 32);
     }
   }
+}
+
+// --- fused front end for documents of < 2^16 nodes (one workgroup per document) --
+// k_fdir + k_frank + k_fplace in one pass over LDS: the rank directory of the
+// document, then every node's rank and cause rank (s/insert's checks,
+// shared.cljc:163-178) with par (u16) and the class bits placed by rank in LDS;
+// par, skind and the per-tile special/hide bitmaps are written out coalesced;
+// then the input index of every rank (sval, u16 in LDS) from the ranks kept in
+// a u16 scratch.  No window records, no second kernel.  A document whose ids
+// leave the directory slot counts in big[0] and the host reruns the batch on
+// the three-kernel front end.  LDS: front_lds_bytes().
+__host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) {
+  return sg * 16 + 4 * ((nmax + 1) / 2) + 8 * ((nmax + 31) / 32);
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_front(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ tile_first, uint32_t sg, uint32_t *__restrict__ par,
+    uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
+    uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
+    uint32_t *__restrict__ status, uint32_t *__restrict__ big,
+    unsigned long long *__restrict__ tprof) {
+  extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
+    if (tprof) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tacc[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  stamp(-1);
+  __shared__ uint64_t rmax[NT / 64];
+  __shared__ uint32_t wtot[NT / 64];
+  __shared__ uint32_t bst;
+  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, nw = (n + 31) / 32;
+  if (n == 0) return;
+  uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
+  uint16_t *p16 = reinterpret_cast<uint16_t *>(sdir + sg);  // par, then sval, by rank
+  uint32_t *clsA = reinterpret_cast<uint32_t *>(p16) + (n + 1) / 2, *clsB = clsA + nw;
+  for (uint32_t g = tid; g < sg; g += NT) sdir[g] = make_uint4(0u, 0u, 0u, 0u);
+  for (uint32_t w = tid; w < nw; w += NT) clsA[w] = clsB[w] = 0;
+  if (tid == 0) bst = 0;
+  __syncthreads();
+  // 1. directory bits over [0, slot) (the root, ts 0, is the smallest id)
+  const uint64_t lim = (uint64_t)sg * FR_GROUP_BITS;
+  uint64_t mx = 0;
+  bool dup = false, far = false;
+  constexpr uint32_t U = 4;
+  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+    uint64_t x[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      x[u] = i < n ? id_key[base + i] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      if (i0 + u * NT >= n) continue;
+      mx = max(mx, x[u]);
+      if (x[u] >= lim) {
+        far = true;
+        continue;
+      }
+      const uint32_t xi = (uint32_t)x[u];
+      const uint32_t g = xi / FR_GROUP_BITS, b = xi - g * FR_GROUP_BITS, m = 1u << (b & 31);
+      const uint32_t old = atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
+      dup |= (old & m) != 0;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint64_t)__shfl_xor(mx, o, 64));
+  if (lane == 0) rmax[tid >> 6] = mx;
+  const bool any_far = __syncthreads_or(far);
+  mx = rmax[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; w++) mx = max(mx, rmax[w]);
+  if (tid == 0 && max_ts) max_ts[d] = mx >> ts_shift;
+  if (any_far) {
+    if (tid == 0) atomicAdd(&big[0], 1u);
+    return;
+  }
+  stamp(0);
+  const uint32_t G = (uint32_t)(mx / FR_GROUP_BITS) + 1;
+  {  // group prefix counts
+    const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
+    uint32_t cnt = 0;
+    for (uint32_t g = g0; g < g1; g++) {
+      const uint4 q = sdir[g];
+      cnt += __popc(q.y) + __popc(q.z) + __popc(q.w);
+    }
+    uint32_t run = block_exscan<NT>(cnt, wtot, nullptr);
+    for (uint32_t g = g0; g < g1; g++) {
+      const uint4 q = sdir[g];
+      sw[g * 4] = run;
+      run += __popc(q.y) + __popc(q.z) + __popc(q.w);
+    }
+  }
+  __syncthreads();
+  // 2. ranks, checks, par and class bits by rank
+  const uint64_t xend = (uint64_t)G * FR_GROUP_BITS;
+  uint32_t st = 0;
+  // the next group's loads are issued before this group is ranked
+  uint64_t qk[U], qc[U];
+  uint8_t qd[U];
+  auto load_group = [&](uint32_t i0) {
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      qk[u] = i < n ? id_key[base + i] : 0ull;
+      qc[u] = i < n ? cause_key[base + i] : 0ull;
+      qd[u] = i < n ? kind[base + i] : 0;
+    }
+  };
+  load_group(tid);
+  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+    uint64_t k[U], c[U];
+    uint8_t kd[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      k[u] = qk[u];
+      c[u] = qc[u];
+      kd[u] = qd[u];
+    }
+    if (i0 + U * NT < n) load_group(i0 + U * NT);
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      if (i >= n) continue;
+      bool pres;
+      const uint32_t r = fr_rank(sdir, (uint32_t)k[u], &pres);
+      uint32_t p = 0;
+      if (r == 0) {
+        if (!(kd[u] & KIND_ROOT)) st |= CW_STATUS_ROOT;
+      } else {
+        if (kd[u] & KIND_ROOT) st |= CW_STATUS_ROOT;
+        bool cp = false;
+        uint32_t cr = 0;
+        if (c[u] < xend) cr = fr_rank(sdir, (uint32_t)c[u], &cp);
+        if (!cp) st |= CW_STATUS_ORPHAN;
+        else if (c[u] >= k[u]) st |= CW_STATUS_NON_LAMPORT;
+        else p = cr;
+      }
+      if (r < n) {  // (duplicates can push ranks past the end; flagged above)
+        p16[r] = (uint16_t)p;
+        const uint32_t cls = kd[u] & KIND_CLASS;
+        if (cls & 1) atomicOr(&clsA[r >> 5], 1u << (r & 31));
+        if (cls & 2) atomicOr(&clsB[r >> 5], 1u << (r & 31));
+      }
+      rank16[base + i] = (uint16_t)min(r, 0xFFFFu);
+    }
+  }
+  if (st) atomicOr(&bst, st);
+  __syncthreads();
+  stamp(1);
+  // par, skind, special/hide bitmaps per 4096-rank tile, coalesced
+  for (uint32_t r = tid; r < n; r += NT) {
+    par[base + r] = p16[r];
+    const uint32_t a = (clsA[r >> 5] >> (r & 31)) & 1u, b = (clsB[r >> 5] >> (r & 31)) & 1u;
+    skind[base + r] = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
+  }
+  uint32_t *kb = kbm + (size_t)tile_first[d] * KBM_WORDS;
+  for (uint32_t w = tid; w < nw; w += NT) {  // word w of the document = word w & 127 of tile w >> 7
+    const uint32_t a = clsA[w], b = clsB[w];
+    uint32_t *o = kb + (size_t)(w >> 7) * KBM_WORDS + (w & 127);
+    o[0] = a | b;            // special
+    o[TILE / 32] = a ^ b;    // hide / h.hide
+  }
+  if (tid == 0 && bst) atomicOr(&status[d], bst);
+  if (__syncthreads_or(dup) && tid == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
+  stamp(2);
+  // 3. the input index of every rank (the rank scratch was written by this
+  // workgroup: one CU, one L1, lines not cached before; the barrier orders it)
+  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+    uint32_t r[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      r[u] = i < n ? rank16[base + i] : 0xFFFFu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (r[u] < n) p16[r[u]] = (uint16_t)(i0 + u * NT);
+  }
+  __syncthreads();
+  stamp(3);
+  for (uint32_t r = tid; r < n; r += NT) {
+    const uint32_t v = p16[r];
+    sval[base + r] = v;
+    if (skey) skey[base + r] = id_key[base + (v < n ? v : 0u)];  // ids in rank order (yarns)
+  }
+  stamp(4);
+  if (tprof && tid == 0)
+    for (int ph = 0; ph < 6; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
 }
 
 // --- tree: effective parents, sibling order, links (one workgroup per document) --
@@ -2527,6 +2725,7 @@ struct cw_ctx {
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
   uint32_t tour = 1;               // CW_TOUR: fused LDS tour for documents of < 2^16 nodes
+  uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
 };
 
@@ -3197,7 +3396,53 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     // 1-2 (dense ids). id order and join through per-document rank directories
     bool front_done = false;
     uint32_t *kbm = nullptr;  // special / hide bitmaps per tile (front end -> tree)
-    if (c->front && N >= (uint64_t)c->front_min_avg * D && t.nmax <= 64 * TILE) {
+    // fused front end: documents of < 2^16 nodes whose ids fit a 40 KiB directory
+    if (c->front && c->front_fused && N >= (uint64_t)c->front_min_avg * D &&
+        t.nmax <= 0xFFFFu && front_lds_bytes(t.nmax, FRONT_FUSED_SG) <= 159 * 1024) {
+      uint32_t *big = scratch_t<uint32_t>(c, "fr_big", 4);
+      uint16_t *rank16 = scratch_t<uint16_t>(c, "fr_rank16", N);
+      kbm = scratch_t<uint32_t>(c, "fr_kbm", (size_t)t.T * KBM_WORDS);
+      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+      if (!big || !rank16 || !kbm) return fail(c, "out of device memory (front)");
+      HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
+      sval = svA;
+      skey = want_yarns ? skA : nullptr;
+      unsigned long long *tprof_f = nullptr;
+      if (c->tree_prof) {
+        tprof_f = scratch_t<unsigned long long>(c, "tprof3", (size_t)D * 8);
+        HIPCHK(c, hipMemsetAsync(tprof_f, 0, (size_t)D * 64, c->stream));
+      }
+      {
+        Launch L(c, "front", (double)N * (8 + 8 + 1 + 2 + 4 + 1 + 2 + 4 + (skey ? 16 : 0)) + (double)N * 8);
+        hipLaunchKernelGGL(k_front<1024>, dim3((uint32_t)D), dim3(1024),
+                           (size_t)front_lds_bytes(t.nmax, FRONT_FUSED_SG), c->stream, id_key,
+                           cause_key, kind, doc_off, dev_tab(c, "t_tile_first"), FRONT_FUSED_SG, par,
+                           skind, sval, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status, big,
+                           tprof_f);
+      }
+      if (check_launch(c, "front")) return -1;
+      if (tprof_f) {
+        std::vector<unsigned long long> h((size_t)D * 8);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(h.data(), tprof_f, (size_t)D * 64, hipMemcpyDeviceToHost));
+        double a[6] = {0};
+        for (uint64_t dd = 0; dd < D; dd++)
+          for (int ph = 0; ph < 6; ph++) a[ph] += (double)h[dd * 8 + ph];
+        fprintf(stderr, "front phases (memtime ticks per doc): dir %.0f rank %.0f write %.0f sval %.0f "
+                "svwrite %.0f\n", a[0] / D, a[1] / D, a[2] / D, a[3] / D, a[4] / D);
+      }
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, big, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (c->pin_small[0] == 0) {
+        front_done = true;
+      } else {  // a document's ids leave the small directory: the three-kernel front end
+        HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
+        sval = nullptr;
+        skey = nullptr;
+        kbm = nullptr;
+      }
+    }
+    if (!front_done && c->front && N >= (uint64_t)c->front_min_avg * D && t.nmax <= 64 * TILE) {
       const uint32_t SG = c->front_slot_groups;
       uint4 *dir = scratch_t<uint4>(c, "fr_dir", (size_t)D * SG);
       uint64_t *dkmin = scratch_t<uint64_t>(c, "fr_kmin", D);
@@ -4143,6 +4388,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 16);
   c->tour = knob("CW_TOUR", 1);
+  c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);

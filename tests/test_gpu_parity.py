@@ -20,8 +20,12 @@ pytestmark = pytest.mark.gpu
 
 
 # Front ends: "front" = rank directories for every document (CW_FRONT_MIN_AVG=0
-# also sends tiny documents through it), "radix" = segmented radix sort + join.
-FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"}, "radix": {"CW_FRONT": "0"},
+# also sends tiny documents through it; the fused k_front where it applies),
+# "front3" = the three-kernel directory front end, "radix" = segmented radix
+# sort + join.
+FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"},
+          "front3": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0", "CW_FRONT_FUSED": "0"},
+          "radix": {"CW_FRONT": "0"},
           "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"},  # no LDS pack sorts
           "hbm-walk": {"CW_TOUR": "0"}}  # walk + rank + emit instead of the LDS tour
 
