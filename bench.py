@@ -321,10 +321,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
+    dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
     if a.config == 5 and (world > 1 or a.dist):
         main_giant_dist(a, world, rank, local, dist, torch, dev)
