@@ -117,6 +117,24 @@ def cpu_baseline(spec, budget_s, max_docs=64):
                       f"in C, {t_total:.1f} s"}
 
 
+def cpu_baseline_parallel(spec, docs=2000, threads=16):
+    """A stronger CPU reference point than the literal fold: the effective-tree
+    preorder (oracle/weave_oracle.c) over `docs` documents of this
+    workload on `threads` host threads (the box's CPU share)."""
+    import oracle
+    from cause_amd import gen
+
+    off, idk, ck, kd = gen.generate(spec, 0, docs, nthreads=threads)
+    t0 = time.perf_counter()
+    oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF, nthreads=threads,
+                       with_vis=True)
+    t = time.perf_counter() - t0
+    return {"value": len(idk) / t, "unit": "nodes/s", "cores": threads, "kind": "port",
+            "sample": f"{docs} documents x {spec.doc_size} nodes of the same workload, "
+                      f"effective-tree preorder + visibility (SURVEY F5/F6) in C on "
+                      f"{threads} threads, {t:.2f} s"}
+
+
 def cpu_baseline_maps(spec, budget_s):
     """The literal c.map/weave fold (oracle/weave_oracle.c or_map_fold_literal,
     map.cljc:21-59) on one core, collection by collection, until ~budget_s."""
@@ -482,6 +500,10 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if world == 1 and not a.no_cpu and a.config == 2:
+            par = cpu_baseline_parallel(spec)
+            line["cpu_baseline_parallel"] = par
+            line["speedup_vs_cpu_parallel"] = value / par["value"]
         print(json.dumps(line), flush=True)
     w.close()
     if world > 1:
