@@ -1914,7 +1914,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
                                              const uint32_t *__restrict__ doc_log2k,
                                              const uint64_t *__restrict__ skey, uint32_t ts_shift,
                                              uint64_t *__restrict__ max_ts,
-                                             uint32_t *__restrict__ perm, uint8_t *__restrict__ vis8,
+                                             uint32_t *__restrict__ perm, uint32_t *__restrict__ vbits,
                                              uint32_t *__restrict__ vcount,
                                              uint32_t *__restrict__ status, uint32_t *loc,
                                              unsigned long long *__restrict__ tprof) {
@@ -2068,11 +2068,26 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   __syncthreads();
   stamp(3);
   uint32_t nvis = 0;
-  for (uint32_t g = tid; g < n; g += NT) {
-    const uint32_t v = (pvis[g >> 5] >> (g & 31)) & 1u;
-    perm[base + g] = out[g];
-    vis8[base + g] = (uint8_t)v;
-    nvis += v;
+  for (uint32_t g = tid; g < n; g += NT) perm[base + g] = out[g];
+  for (uint32_t w = tid; w < nw; w += NT) nvis += __popc(pvis[w]);
+  if (vbits) {
+    // the render bits straight into the batch's bitmap: global word W holds
+    // positions [32 W, 32 W + 32); the two end words are shared with the
+    // neighbouring documents (atomicOr on a zeroed bitmap)
+    const uint32_t W0 = base >> 5, W1 = (base + n - 1) >> 5;
+    for (uint32_t W = W0 + tid; W <= W1; W += NT) {
+      const uint32_t lo = max(W << 5, base), hi = min((W << 5) + 32, base + n);
+      const uint32_t g = lo - base, len = hi - lo, w0 = g >> 5, off = g & 31;
+      uint32_t x = pvis[w0] >> off;
+      if (off && w0 + 1 < nw) x |= pvis[w0 + 1] << (32 - off);
+      if (len < 32) x &= (1u << len) - 1;
+      x <<= lo - (W << 5);
+      if (W == W0 || W == W1) {
+        if (x) atomicOr(&vbits[W], x);
+      } else {
+        vbits[W] = x;
+      }
+    }
   }
   uint32_t total;
   block_exscan<NT>(nvis, wtot, &total);
@@ -3257,8 +3272,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       hipLaunchKernelGGL(k_tour<1024>, dim3((uint32_t)D), dim3(1024),
                          (size_t)tour_lds_bytes(t.nmax, t.tour_log2k), c->stream,
                          (const uint32_t *)link, sval, doc_off, doc_log2k, skey, ts_shift,
-                         skey ? out->max_ts : nullptr, out->weave_perm, vis8, out->visible_count,
-                         out->status, loc, tprof);
+                         skey ? out->max_ts : nullptr, out->weave_perm, out->visible_bits,
+                         out->visible_count, out->status, loc, tprof);
     }
     if (check_launch(c, "tour")) return -1;
     if (tprof) {
@@ -3343,8 +3358,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     if (check_launch(c, "emit")) return -1;
   }
 
-  // 9. visibility bitmap
-  if (out->visible_bits) {
+  // 9. visibility bitmap (the fused tour wrote it)
+  if (out->visible_bits && !(t.tour && !giant)) {
     const uint32_t words = (N + 31) / 32;
     Launch L(c, "packbits", (double)N + (double)words * 4);
     hipLaunchKernelGGL(k_pack_bits, dim3((words + 255) / 256), B256, 0, c->stream, vis8, N,
