@@ -1072,6 +1072,23 @@ __global__ __launch_bounds__(NT) void k_front(
     for (int ph = 0; ph < 6; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
 }
 
+// dst bits [off, off + nbits) |= src bits [0, nbits) (dst zeroed beforehand).
+__global__ __launch_bounds__(256) void k_or_bits_at(const uint32_t *__restrict__ src, uint32_t nbits,
+                                                    uint32_t *__restrict__ dst, uint32_t off) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i * 32 >= nbits) return;
+  uint32_t x = src[i];
+  const uint32_t len = min(32u, nbits - i * 32);
+  if (len < 32) x &= (1u << len) - 1;
+  if (!x) return;
+  const uint32_t p = off + i * 32, w = p >> 5, sh = p & 31;
+  atomicOr(&dst[w], x << sh);
+  if (sh) {
+    const uint32_t hi = x >> (32 - sh);
+    if (hi) atomicOr(&dst[w + 1], hi);
+  }
+}
+
 // --- tree: effective parents, sibling order, links (one workgroup per document) --
 // Effective parent: a special keeps its cause, a non-special climbs
 // through special causes.  Siblings are ordered specials by descending id, then
@@ -1769,7 +1786,10 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
                                                    uint32_t n, uint32_t Weff, uint32_t *__restrict__ nb,
                                                    uint32_t *__restrict__ tb,
                                                    uint32_t *__restrict__ status) {
+  // the top level (<= 8192 elements) ranked by pointer jumping in LDS: suffix
+  // sums of nodes and sublists along the list, element 0 (the root's) first
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // next, count, sublists
+  constexpr uint32_t PT = 8;  // elements per thread: S2 <= 8192
   uint32_t *nx = sm, *cn = sm + S2, *sb = sm + 2 * S2;
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
     nx[i] = snext[i];
@@ -1777,22 +1797,36 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
     sb[i] = ssub[i];
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // the super list in order: <= 8192 steps in LDS
-    uint32_t q = 0, run = 0, trun = 0, steps = 0;
-    while (q != NX_END && q < S2 && steps++ <= S2) {
-      const uint32_t a = run, b = trun;
-      run += cn[q];
-      trun += sb[q];
-      cn[q] = a;
-      sb[q] = b;
-      q = nx[q];
+  for (uint32_t round = 0; (1u << round) < 2 * S2; round++) {
+    uint32_t a[PT], b[PT], q2[PT];
+#pragma unroll
+    for (uint32_t k = 0; k < PT; k++) {
+      const uint32_t i = threadIdx.x + k * blockDim.x;
+      if (i < S2) {
+        const uint32_t q = nx[i];
+        const bool on = q < S2;
+        a[k] = cn[i] + (on ? cn[q] : 0u);
+        b[k] = sb[i] + (on ? sb[q] : 0u);
+        q2[k] = on ? nx[q] : NX_END;
+      }
     }
-    if (run != n || trun != Weff || q != NX_END) atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < PT; k++) {
+      const uint32_t i = threadIdx.x + k * blockDim.x;
+      if (i < S2) {
+        cn[i] = a[k];
+        sb[i] = b[k];
+        nx[i] = q2[k];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  if (threadIdx.x == 0 && (S2 == 0 || cn[0] != n || sb[0] != Weff))
+    atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
-    nb[i] = cn[i];
-    tb[i] = sb[i];
+    nb[i] = n - min(cn[i], n);
+    tb[i] = Weff - min(sb[i], Weff);
   }
 }
 
@@ -2740,6 +2774,8 @@ struct cw_ctx {
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
   uint32_t tour = 1;               // CW_TOUR: fused LDS tour for documents of < 2^16 nodes
+  uint32_t giant_docs_max = 32;    // CW_GIANT_DOCS: batches of up to this many large documents
+                                   // go through the giant path document by document
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
 };
@@ -3059,7 +3095,7 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scan", tag);
-    if (D == 1 && t.T > 2 * GSCAN_CHUNK) {
+    if (D == 1 && t.T > 16) {
       // one document of many tiles: chunked scan over all workgroups
       const uint32_t nc = (t.T + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
       uint32_t *cs = scratch_t<uint32_t>(c, "gscan_cs", (size_t)nc * nb);
@@ -3517,7 +3553,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (!bkt) return fail(c, "out of device memory (bucket index)");
     {
       Launch L(c, "index", (double)N * 8 + (double)t.Btot * 4);
-      if (D == 1 && N > (1u << 20))  // one large document: a thread per id
+      if (D == 1 && N > (1u << 16))  // one large document: a thread per id
         hipLaunchKernelGGL(k_index_flat, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, bkt,
                            out->status);
       else
@@ -3614,7 +3650,51 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
     cause = dca;
     kind = dk;
   }
-  if (weave_lists_device(c, bt, id, cause, kind, &dres)) return -1;
+  // A few large documents would leave the per-document tree with a handful of
+  // workgroups on a 256-CU GPU: weave them one by one on the all-parallel
+  // giant-document path instead (render bits merged at each document's offset).
+  uint64_t big_docs = 0;
+  for (uint64_t d = 0; d < D; d++)
+    big_docs += (bt->doc_offsets[d + 1] - bt->doc_offsets[d]) >= c->giant_min;
+  if (D > 1 && D <= c->giant_docs_max && big_docs * 2 >= D) {
+    if (dres.visible_bits)
+      HIPCHK(c, hipMemsetAsync(dres.visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
+    for (uint64_t d = 0; d < D; d++) {
+      const uint64_t b = bt->doc_offsets[d], nd = bt->doc_offsets[d + 1] - b;
+      if (nd == 0) {
+        HIPCHK(c, hipMemsetAsync(dres.status + d, 0, 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(dres.visible_count + d, 0, 4, c->stream));
+        if (dres.max_ts) HIPCHK(c, hipMemsetAsync(dres.max_ts + d, 0, 8, c->stream));
+        continue;
+      }
+      const uint64_t off1[2] = {0, nd};
+      if (ensure_tables(c, 1, off1)) return -1;
+      cw_list_batch sb = *bt;
+      sb.n_docs = 1;
+      sb.doc_offsets = off1;
+      cw_list_result sr{};
+      sr.weave_perm = dres.weave_perm + b;
+      sr.visible_count = dres.visible_count + d;
+      sr.max_ts = dres.max_ts ? dres.max_ts + d : nullptr;
+      sr.status = dres.status + d;
+      sr.yarn_perm = dres.yarn_perm ? dres.yarn_perm + b : nullptr;
+      uint32_t *vb = nullptr;
+      if (dres.visible_bits) {
+        vb = scratch_t<uint32_t>(c, "gd_bits", (nd + 31) / 32 + 1);
+        if (!vb) return fail(c, "out of device memory (bits)");
+      }
+      sr.visible_bits = vb;
+      if (weave_lists_device(c, &sb, id + b, cause + b, kind + b, &sr)) return -1;
+      if (vb) {
+        const uint32_t words = (uint32_t)((nd + 31) / 32);
+        hipLaunchKernelGGL(k_or_bits_at, dim3((words + 255) / 256), dim3(256), 0, c->stream, vb,
+                           (uint32_t)nd, dres.visible_bits, (uint32_t)b);
+        if (check_launch(c, "or_bits")) return -1;
+      }
+    }
+  } else if (weave_lists_device(c, bt, id, cause, kind, &dres)) {
+    return -1;
+  }
 
   if (memspace == CW_MEM_HOST) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4403,6 +4483,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 16);
   c->tour = knob("CW_TOUR", 1);
+  c->giant_docs_max = knob("CW_GIANT_DOCS", 32);
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);

@@ -364,6 +364,37 @@ def test_giant_path_shapes(giant_weaver):
                 method=oracle.METHOD_LINKED)
 
 
+def test_few_large_documents_per_document_giant_path():
+    """A batch of a few large documents goes through the giant path one
+    document at a time (render bits merged at unaligned offsets); a small one
+    in the middle and an empty one too."""
+    docs = []
+    for n, seed in ((150_000, 1), (70_001, 2), (3_000, 3), (90_000, 4)):
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n, seed=seed)
+        off, idk, ck, kd = gen.generate(spec, 0, 1)
+        docs.append((idk, ck, kd))
+    off = np.zeros(len(docs) + 2, np.uint64)
+    for i, (idk, _, _) in enumerate(docs):
+        off[i + 1] = off[i] + len(idk)
+    off[-1] = off[-2]  # an empty document at the end
+    idk = np.concatenate([d[0] for d in docs])
+    ck = np.concatenate([d[1] for d in docs])
+    kd = np.concatenate([d[2] for d in docs])
+    lay = dataclasses.replace(gen.CONFIG2, nodes_per_doc=150_000).layout()
+    with abi.Weaver(0) as w:
+        res = w.weave_lists(off, idk, ck, kd, lay)
+    perm, vis, st, vcount, max_ts = oracle_batch(off, idk, ck, kd, lay, oracle.METHOD_LINKED)
+    D = len(off) - 1
+    assert res.status[-1] & abi.STATUS_ROOT
+    assert not res.status[:-1].any()
+    for d in range(D - 1):
+        b, e = int(off[d]), int(off[d + 1])
+        assert np.array_equal(res.weave_perm[b:e], perm[b:e]), d
+    assert np.array_equal(res.visible(), vis.astype(bool))
+    assert np.array_equal(res.visible_count[:-1], vcount[:-1])
+    assert np.array_equal(res.max_ts[:-1], max_ts[:-1])
+
+
 def test_giant_document_default_threshold(weaver):
     """A 3M-node config-2-shaped list: over the default threshold, so the giant
     tree, the chunked radix scan and the flat bucket index all run."""
