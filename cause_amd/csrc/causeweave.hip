@@ -3653,10 +3653,16 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   // A few large documents would leave the per-document tree with a handful of
   // workgroups on a 256-CU GPU: weave them one by one on the all-parallel
   // giant-document path instead (render bits merged at each document's offset).
-  uint64_t big_docs = 0;
-  for (uint64_t d = 0; d < D; d++)
-    big_docs += (bt->doc_offsets[d + 1] - bt->doc_offsets[d]) >= c->giant_min;
-  if (D > 1 && D <= c->giant_docs_max && big_docs * 2 >= D) {
+  // (estimated times: the per-document tree sweeps ~22 ns a node in one
+  // workgroup, all documents at once; the giant path costs ~0.4 ms a call plus
+  // ~0.3 ns a node, documents one after another)
+  double t_tree = 0, t_giant = 0;
+  for (uint64_t d = 0; d < D; d++) {
+    const double nd = (double)(bt->doc_offsets[d + 1] - bt->doc_offsets[d]);
+    t_tree = std::max(t_tree, nd * 22e-9);
+    t_giant += 0.4e-3 + nd * 0.3e-9;
+  }
+  if (D > 1 && D <= c->giant_docs_max && t_giant < t_tree) {
     if (dres.visible_bits)
       HIPCHK(c, hipMemsetAsync(dres.visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
     for (uint64_t d = 0; d < D; d++) {
