@@ -595,13 +595,18 @@ __device__ __forceinline__ uint32_t fr_word(const uint4 &q, uint32_t w) {
 }
 
 // x = key - kmin < groups * 96.  present: bit x is set; returns the rank.
+// (masks instead of picking a word by index: an indexed uint4 lands in scratch)
 __device__ __forceinline__ uint32_t fr_rank(const uint4 *__restrict__ dir, uint32_t x,
                                             bool *present) {
-  const uint32_t g = x / FR_GROUP_BITS, b = x - g * FR_GROUP_BITS, w = b >> 5, m = 1u << (b & 31);
+  const uint32_t g = x / FR_GROUP_BITS, b = x - g * FR_GROUP_BITS;
   const uint4 q = dir[g];
-  const uint32_t wv = fr_word(q, w);
-  *present = (wv & m) != 0;
-  return q.x + (w > 0 ? __popc(q.y) : 0u) + (w > 1 ? __popc(q.z) : 0u) + __popc(wv & (m - 1));
+  const uint32_t sh = b & 31, below = (1u << sh) - 1, bit = 1u << sh;
+  const uint32_t m0 = b >= 32 ? 0xFFFFFFFFu : below;
+  const uint32_t m1 = b >= 64 ? 0xFFFFFFFFu : (b >= 32 ? below : 0u);
+  const uint32_t m2 = b >= 64 ? below : 0u;
+  const uint32_t hit = b < 32 ? (q.y & bit) : (b < 64 ? (q.z & bit) : (q.w & bit));
+  *present = hit != 0;
+  return q.x + __popc(q.y & m0) + __popc(q.z & m1) + __popc(q.w & m2);
 }
 
 // One workgroup per document, one pass over its ids: bitmap in LDS over the
