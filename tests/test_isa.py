@@ -1,0 +1,52 @@
+"""Code-object checks on the built library (CPU only): no kernel of
+libcauseweave.so uses scratch or spills registers.
+
+A run-time index into a small register array (a uint4 picked by word number,
+a lambda capturing arrays by reference) silently becomes a private-memory
+array; k_front's rank pass ran 3x slower that way.  The metadata notes of the
+gfx950 code object say so per kernel (.private_segment_fixed_size)."""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "cause_amd", "libcauseweave.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def _kernel_meta(tmp_path):
+    objdump, readelf = os.path.join(LLVM, "llvm-objdump"), os.path.join(LLVM, "llvm-readelf")
+    if not (os.path.exists(objdump) and os.path.exists(readelf)):
+        pytest.skip("llvm tools not present")
+    if not os.path.exists(LIB):
+        pytest.skip("libcauseweave.so not built")
+    lib = tmp_path / "lib.so"
+    shutil.copy(LIB, lib)
+    subprocess.run([objdump, "--offloading", str(lib)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    cos = [f for f in os.listdir(tmp_path) if "gfx950" in f]
+    assert cos, "no gfx950 code object in libcauseweave.so"
+    notes = subprocess.run([readelf, "--notes", str(tmp_path / cos[0])], check=True,
+                           capture_output=True, text=True).stdout
+    kernels, cur = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m and m.group(1).startswith("_Z"):
+            cur = kernels.setdefault(m.group(1), {})
+            continue
+        m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|sgpr_spill_count):\s+(\d+)",
+                     line)
+        if m and cur is not None:
+            cur[m.group(1)] = int(m.group(2))
+    return kernels
+
+
+def test_no_kernel_uses_scratch(tmp_path):
+    kernels = _kernel_meta(tmp_path)
+    assert any("k_tree" in k for k in kernels) and any("k_front" in k for k in kernels)
+    bad = {k: v for k, v in kernels.items() if any(v.get(f, 0) for f in
+           ("private_segment_fixed_size", "vgpr_spill_count", "sgpr_spill_count"))}
+    assert not bad, f"kernels using scratch: {bad}"
