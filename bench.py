@@ -39,11 +39,16 @@ def parse():
                     help="budget of the cpu_baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive pass")
-    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 4, 5],
+    ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="BASELINE.json configs[config-1]: 2 = the headline batch "
                          "(default), 1 = one 100k-node list (latency; replicas on N GPUs), "
+                         "3 = --stream-docs documents streamed from host memory in --docs "
+                         "batches (sharded over N GPUs), "
                          "4 = CausalMap collections (10^6 x 100 nodes per GPU), "
                          "5 = one giant list (--giant nodes; replicas on N GPUs)")
+    ap.add_argument("--stream-docs", type=int, default=1_000_000,
+                    help="--config 3: documents in the whole job (all GPUs)")
+    ap.add_argument("--depth", type=int, default=2, help="--config 3: pipeline slots")
     ap.add_argument("--giant", type=int, default=1 << 26, help="--config 5: nodes in the list")
     ap.add_argument("--colls", type=int, default=1_000_000, help="--config 4: collections per GPU")
     ap.add_argument("--dist", action="store_true",
@@ -331,6 +336,100 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     w.close()
 
 
+def main_stream(a, world, rank, local, dist, torch, dev):
+    """--config 3: --stream-docs documents, generated on the host into pinned
+    memory and streamed through the GPU in --docs batches (cause_amd/stream.py:
+    fill -> H2D -> weave -> D2H, --depth slots).  Documents are sharded
+    contiguously over the ranks (total fixed: strong scaling, no collectives).
+    value = device-resident rate (nodes / the weaves' own time, every batch);
+    end_to_end = nodes / wall time of the whole pipeline (generation, PCIe both
+    ways and the weave overlapped)."""
+    from cause_amd import abi, gen, shard, stream
+    import dataclasses
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
+    layout = spec.layout()
+    T, B, n = a.stream_docs, a.docs, spec.doc_size
+    d0, d1 = rank * T // world, (rank + 1) * T // world
+    nb = (d1 - d0 + B - 1) // B
+    w = abi.Weaver(local)
+    st_bad = [0]
+    vis_total = [0]
+
+    def fill(i, views):
+        b0 = d0 + i * B
+        b1 = min(d1, b0 + B)
+        off, *_ = gen.generate(spec, b0, b1, nthreads=16, out=views)
+        return off
+
+    def consume(o):
+        st_bad[0] += int(np.count_nonzero(o.status))
+        vis_total[0] += int(o.visible_count.sum(dtype=np.uint64))
+
+    s = stream.BatchStreamer(w, dev, B * n, B, layout, depth=a.depth)
+    s.run(min(a.warmup, nb), fill)          # warm-up batches (not timed)
+    w.reset_kernel_stats()
+    w.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    with heartbeat(f"streaming {d1 - d0:,} documents in {nb} batches"):
+        st = s.run(nb, fill, consume)
+    if world > 1:
+        dist.barrier()
+    w.set_profiling(False)
+    stats = w.kernel_stats()
+    if st_bad[0]:
+        raise SystemExit(f"rank {rank}: {st_bad[0]} documents out of domain")
+    t_dev = sum(st.weave_ms) / 1e3
+    t_dev_max = shard.reduce_max_time(t_dev, dist, dev) if world > 1 else t_dev
+    wall_max = shard.reduce_max_time(st.wall_s, dist, dev) if world > 1 else st.wall_s
+    total = T * n
+    name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
+    achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc) and B == 10_000 and a.nodes == 50_000:
+        entry = json.load(open(pmc)).get(name)
+        traffic = entry["bytes"] if entry else None
+    if rank == 0:
+        cpu = None
+        if world == 1 and not a.no_cpu:
+            cpu = cpu_baseline(spec, a.cpu_seconds, max_docs=64)
+        pcie = total // world * (8 + 8 + 1 + 4) + total // world // 8
+        line = {
+            "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
+            "value": total / t_dev_max, "unit": "nodes/s", "n_gpus": world, "steps": nb,
+            "warmup": min(a.warmup, nb), "ms_per_step": t_dev_max / nb * 1e3,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic (generated on the host per batch)",
+            "config": {"workload": (f"config3: {T:,} CausalLists streamed from host memory in "
+                                    f"{B:,}-document batches"),
+                       "docs_total": T, "docs_per_batch": B, "nodes_per_doc": n,
+                       "sites": spec.n_sites, "p_hide": spec.p_hide, "p_show": spec.p_show,
+                       "p_conj": spec.p_conj, "key_bits": layout.key_bits,
+                       "pipeline_depth": a.depth, "parallelism": f"docs sharded x{world}"},
+            "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic, "launches_per_step": launches / nb,
+                         "kernel_ms_per_step": ms / nb},
+            "cpu_baseline": cpu,
+            "end_to_end": {"value": total / wall_max, "unit": "nodes/s", "wall_s": wall_max,
+                           "pcie_bytes_per_gpu": pcie,
+                           "h2d_ms_per_batch": float(np.mean(st.h2d_ms)),
+                           "weave_ms_per_batch": float(np.mean(st.weave_ms)),
+                           "d2h_ms_per_batch": float(np.mean(st.d2h_ms)),
+                           "host_fill_s_per_batch": st.fill_s / nb,
+                           "note": "host generation (16 threads), H2D, weave and D2H "
+                                   "overlapped over the slots; rank-0 figures"},
+            "visible_nodes": vis_total[0],
+        }
+        if cpu:
+            line["speedup_vs_cpu_baseline"] = line["value"] / cpu["value"]
+        print(json.dumps(line), flush=True)
+    del s
+    w.close()
+
+
 def main():
     a = parse()
     import torch
@@ -346,6 +445,11 @@ def main():
 
     if a.config == 5 and (world > 1 or a.dist):
         main_giant_dist(a, world, rank, local, dist, torch, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    if a.config == 3:
+        main_stream(a, world, rank, local, dist, torch, dev)
         if world > 1:
             dist.destroy_process_group()
         return
