@@ -54,7 +54,76 @@ def parse():
     ap.add_argument("--dist", action="store_true",
                     help="--config 5 on one GPU through the distributed path (sample sort, "
                          "exchange, gather; always taken when N > 1)")
+    ap.add_argument("--check", action="store_true",
+                    help="after timing, every rank compares its outputs with the CPU oracle "
+                         "(configs 2 and 4; the JSON line gets a 'check' object)")
     return ap.parse_args()
+
+
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` without a launcher: start N ranks (one process
+    per GPU) through torch.distributed.run as a CHILD process, before this
+    process touches the GPU, and return its exit code.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1", "--master-port",
+           str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def check_lists(off, idk, ck, kd, perm, bits, vcount, status):
+    """--check: this rank's config-2 outputs vs the oracle (effective-tree
+    preorder in C, itself pinned to the literal fold by the tests): mismatching
+    documents."""
+    import oracle
+
+    want, vis, st = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF, nthreads=16)
+    got = perm.cpu().numpy().view(np.uint32)
+    gvis = np.unpackbits(bits.cpu().numpy().view(np.uint8), bitorder="little")[:len(got)]
+    gst = status.cpu().numpy().view(np.uint32)
+    gvc = vcount.cpu().numpy().view(np.uint32)
+    bad = 0
+    for d in range(len(off) - 1):
+        lo, hi = int(off[d]), int(off[d + 1])
+        ok = (gst[d] == st[d] and np.array_equal(got[lo:hi], want[lo:hi]) and
+              np.array_equal(gvis[lo:hi], vis[lo:hi]) and int(gvc[d]) == int(vis[lo:hi].sum()))
+        bad += 0 if ok else 1
+    return bad
+
+
+def check_maps(off, idk, ck, ci, kd, o, S):
+    """--check: this rank's config-4 key weaves and active nodes vs the literal
+    c.map/weave fold (oracle/weave_oracle.c): mismatching collections."""
+    import oracle
+
+    h = {k: v.cpu().numpy() for k, v in o.items()}
+    so, sc, sk = h["seg_offsets"].view(np.uint64), h["seg_coll"].view(np.uint32), h["seg_key"].view(np.uint64)
+    sa, sp, gst = h["seg_active"], h["seg_perm"].view(np.uint32), h["status"].view(np.uint32)
+    got = [dict() for _ in range(len(off) - 1)]
+    for s in range(S):
+        kw = sp[int(so[s]):int(so[s + 1])]
+        got[int(sc[s])][int(sk[s])] = (int(sa[s]), kw[1:].tolist() if kw[0] == 0xFFFFFFFF else None)
+    tok, idk_bit, nil = np.uint64(1 << 63), 1 << 63, (1 << 64) - 1
+    bad = 0
+    for d in range(len(off) - 1):
+        a, b = int(off[d]), int(off[d + 1])
+        c = np.where(ci[a:b] == 1, ck[a:b], ck[a:b] | tok)
+        nk, npos, skk, saa = oracle.map_weave(idk[a:b], c, ci[a:b], kd[a:b], 0)
+        order = np.lexsort((npos, nk))
+        groups = {}
+        for j in order:
+            groups.setdefault(int(nk[j]), []).append(int(j))
+        api = lambda k: nil if k == nil else (k & ~idk_bit if k & idk_bit else idk_bit | k)
+        want = {api(int(k)): (int(act), groups.get(int(k), [])) for k, act in zip(skk, saa)}
+        bad += 0 if (gst[d] == 0 and got[d] == want) else 1
+    return bad
 
 
 class heartbeat:
@@ -298,7 +367,7 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        step()
+        S = step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -309,6 +378,12 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     value = N * world * a.steps / dt_max
     name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
     achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    check = None
+    if a.check:
+        bad = check_maps(off, idk, ck, ci, kd, o, S)
+        tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
+        check = {"collections_checked": tot[1], "mismatches": tot[0],
+                 "against": "literal c.map/weave fold + active-node (oracle, C)"}
     if rank == 0:
         cpu = cpu_baseline_maps(spec, a.cpu_seconds) if (world == 1 and not a.no_cpu) else None
         line = {
@@ -332,6 +407,8 @@ def main_maps(a, world, rank, local, dist, torch, dev):
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if check:
+            line["check"] = check
         print(json.dumps(line), flush=True)
     w.close()
 
@@ -432,16 +509,26 @@ def main_stream(a, world, rank, local, dist, torch, dev):
 
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus and rank == 0:
+        print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={world}: using {world} ranks",
+              file=sys.stderr)
+    # more ranks than GPUs (a rehearsal on a one-GPU box): ranks share devices
+    # and the bookkeeping collectives go over gloo (RCCL needs a GPU per rank)
+    ndev = torch.cuda.device_count()
+    shared = world > max(ndev, 1)
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)  # before the process group: RCCL binds the current device
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group("gloo" if shared or not torch.cuda.is_available() else "nccl")
 
     if a.config == 5 and (world > 1 or a.dist):
         main_giant_dist(a, world, rank, local, dist, torch, dev)
@@ -530,6 +617,12 @@ def main():
     dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
     total_nodes = N * world * a.steps
     value = total_nodes / dt_max
+    check = None
+    if a.check:
+        bad = check_lists(off, idk, ck, kd, perm, bits, vcount, status)
+        tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
+        check = {"documents_checked": tot[1], "mismatches": tot[0],
+                 "against": "effective-tree preorder + visibility (oracle, C)"}
 
     # PCIe-inclusive rate (not the headline value): inputs from pinned host
     # buffers, the weave, weave_perm + visible bits back, serialised
@@ -604,6 +697,8 @@ def main():
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]
+        if check:
+            line["check"] = check
         if world == 1 and not a.no_cpu and a.config == 2:
             par = cpu_baseline_parallel(spec)
             line["cpu_baseline_parallel"] = par

@@ -123,7 +123,7 @@ def lib():
         L.cw_weft_lists.restype = C.c_int
         P, U64, U32 = C.c_void_p, C.c_uint64, C.c_uint32
         L.cw_sort_keys.argtypes = [P, P, U64, U32, P, P]
-        L.cw_lookup_keys.argtypes = [P, P, U64, P, U64, U32, P]
+        L.cw_lookup_keys.argtypes = [P, P, U64, P, U64, U32, P, P]
         L.cw_partition_keys.argtypes = [P, P, U64, P, U32, P, P]
         L.cw_gather.argtypes = [P, P, P, U64, U32, P]
         L.cw_scatter32.argtypes = [P, P, P, U64, P]
@@ -304,9 +304,9 @@ class Weaver:
         self.sort_keys_device(kin.data_ptr(), n, key_bits, kout.data_ptr(), iout.data_ptr())
         return kout.cpu().numpy().view(np.uint64), iout.cpu().numpy().view(np.uint32)
 
-    def lookup_keys_device(self, sorted_ptr, n, q_ptr, m, base, out_ptr):
-        self._check(self._L.cw_lookup_keys(self._h, sorted_ptr, n, q_ptr, m, base, out_ptr),
-                    "cw_lookup_keys")
+    def lookup_keys_device(self, sorted_ptr, n, q_ptr, m, base, out_ptr, status_ptr=None):
+        self._check(self._L.cw_lookup_keys(self._h, sorted_ptr, n, q_ptr, m, base, out_ptr,
+                                           status_ptr), "cw_lookup_keys")
 
     def partition_keys_device(self, keys_ptr, m, split_ptr, n_split, perm_ptr) -> np.ndarray:
         counts = np.zeros(n_split + 1, np.uint64)
@@ -379,11 +379,12 @@ class Weaver:
         b, off = self._batch(off, _ptr(i), _ptr(c), _ptr(k), layout)
         wb = CwWeftBatch(b, cut.ctypes.data_as(C.POINTER(C.c_uint64)))
         ko = np.zeros(D + 1, np.uint64)
-        src = np.zeros(max(N, 1), np.uint32)
-        w = ListResult(np.zeros(max(N, 1), np.uint32), np.zeros((N + 31) // 32 + 1, np.uint32),
+        cap = max(N + (D << layout.site_bits), 1)  # + one [id] node per named site
+        src = np.zeros(cap, np.uint32)
+        w = ListResult(np.zeros(cap, np.uint32), np.zeros((cap + 31) // 32 + 1, np.uint32),
                        np.zeros(max(D, 1), np.uint32), np.zeros(max(D, 1), np.uint64),
                        np.zeros(max(D, 1), np.uint32),
-                       np.zeros(max(N, 1), np.uint32) if (yarns and layout.site_bits) else None)
+                       np.zeros(cap, np.uint32) if (yarns and layout.site_bits) else None)
         r = CwWeftResult(ko.ctypes.data_as(C.POINTER(C.c_uint64)), _ptr(src),
                          CwListResult(_ptr(w.weave_perm), _ptr(w.visible_bits),
                                       _ptr(w.visible_count), _ptr(w.max_ts), _ptr(w.status),

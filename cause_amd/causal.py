@@ -108,9 +108,10 @@ def weave_lists(cts):
     for d, (ct, nodes) in enumerate(zip(cts, docs)):
         lo, hi = int(b.offsets[d]), int(b.offsets[d + 1])
         st = int(res.status[d])
-        if st & abi.STATUS_ORPHAN:
-            raise CauseError("The cause of this node is not in the tree.", {"cause-must-exist"})
-        if st:
+        # c.list/weave's full reweave never throws: absent / non-Lamport / nil
+        # causes and a missing root get the literal fold's weave (the library's
+        # exact path); only a repeated id is impossible for a ::nodes map
+        if st & (abi.STATUS_DUP | abi.STATUS_INTERNAL):
             raise CauseError(f"document outside the weave's domain (status {st})", {"weave-domain"})
         new = dict(ct)
         new["weave"] = [nodes[p] for p in res.weave_perm[lo:hi]]
@@ -261,33 +262,46 @@ def insert_bulk(ct, nodes):
 
 def weft_lists(items):
     """s/weft (shared.cljc:268-293) for many (ct, ids-to-cut-yarns) list pairs in
-    ONE GPU call (cw_weft_lists): time travel to the cut, then the full reweave."""
+    ONE GPU call (cw_weft_lists): time travel to the cut, then the full reweave.
+    A cut id that is not a node keeps its site's whole yarn plus the
+    one-element node ``(id,)`` (``(new-node [id nil])``), last in that yarn."""
     docs = [[(i, b[0], b[1]) for i, b in ct["nodes"].items()] for ct, _ in items]
-    pk = pack.pack_lists(docs, min_site_bits=1)  # cw_weft_lists indexes cuts by site rank
+    cuts = []
+    for ct, ids in items:
+        last = {}
+        for i in ids:  # (assoc-in [::yarns site] ..): the last id of a site wins
+            if i != ROOT_ID:
+                last[i[1]] = i
+        cuts.append(last)
+    pk = pack.pack_lists(docs, min_site_bits=1,  # cw_weft_lists indexes cuts by site rank
+                         extra_ids=[list(c.values()) for c in cuts])
     lay = pk.layout
     S = 1 << lay.site_bits
     cut = np.zeros(len(items) << lay.site_bits, np.uint64)
-    for d, ((ct, ids), pd) in enumerate(zip(items, pk.docs)):
-        for i in ids:
-            if i == ROOT_ID or i[1] not in pd.site_rank:
-                continue  # a site with no node keeps nothing (its yarn is empty)
-            cut[d * S + pd.site_rank[i[1]]] = lay.pack(i[0], pd.site_rank[i[1]], i[2])
+    for d, (last, pd) in enumerate(zip(cuts, pk.docs)):
+        for site, i in last.items():
+            cut[d * S + pd.site_rank[site]] = lay.pack(i[0], pd.site_rank[site], i[2])
     res = weaver().weft_lists(pk.offsets, pk.id_key, pk.cause_key, pk.kind, lay, cut)
     vis = res.weave.visible()
     out = []
-    for d, ((ct, ids), nodes) in enumerate(zip(items, docs)):
+    for d, ((ct, ids), nodes, last, pd) in enumerate(zip(items, docs, cuts, pk.docs)):
         st = int(res.weave.status[d])
-        if st:
+        if st & (abi.STATUS_DUP | abi.STATUS_INTERNAL):
             raise CauseError(f"weft outside the weave's domain (status {st})", {"weave-domain"})
         lo, hi = int(res.offsets[d]), int(res.offsets[d + 1])
-        kept = [nodes[s] for s in res.src[lo:hi]]
+        # the [id] nodes come after the kept nodes, in site-rank order
+        bogus = iter(sorted((i for i in last.values() if i not in ct["nodes"]),
+                            key=lambda i: pd.site_rank[i[1]]))
+        kept = [nodes[s] if s != 0xFFFFFFFF else (next(bogus),) for s in res.src[lo:hi]]
         new = new_list_ct(site_id=ct["site_id"], uuid=ct["uuid"])
-        new["nodes"] = {n[0]: (n[1], n[2]) for n in kept}
+        new["nodes"] = {n[0]: tuple(n[1:]) for n in kept}
         new["weave"] = [kept[p] for p in res.weave.weave_perm[lo:hi]]
         new["_visible"] = [bool(v) for v in vis[lo:hi]]
         yarns = {}
         for p in res.weave.yarn_perm[lo:hi]:
             yarns.setdefault(kept[p][0][1], []).append(kept[p])
+        for y in yarns.values():  # (conj yarn-prefix [id]): the [id] node is last
+            y.sort(key=lambda n: len(n) == 1)
         new["yarns"] = yarns
         new["lamport_ts"] = max(i[0] for i in ids if i != ROOT_ID)
         out.append(new)
@@ -322,8 +336,8 @@ def causal_list_to_list(ct):
 
 
 def causal_list_to_edn(ct):
-    """list.cljc:57-66"""
-    return [n[2] for n in causal_list_to_list(ct)]
+    """list.cljc:57-66: (peek node) of every rendered node"""
+    return [n[-1] for n in causal_list_to_list(ct)]
 
 
 def count(ct):

@@ -1050,6 +1050,9 @@ __global__ __launch_bounds__(NT) void k_front(
     o[TILE / 32] = a ^ b;    // hide / h.hide
   }
   if (tid == 0 && bst) atomicOr(&status[d], bst);
+  // documents for the exact path (exact.hip): counted here, read back with big[0]
+  if (tid == 0 && (bst & (CW_STATUS_ROOT | CW_STATUS_ORPHAN | CW_STATUS_NON_LAMPORT)))
+    atomicAdd(&big[1], 1u);
   if (__syncthreads_or(dup) && tid == 0) atomicOr(&status[d], (uint32_t)CW_STATUS_DUP);
   stamp(2);
   // 3. the input index of every rank (the rank scratch was written by this
@@ -2468,8 +2471,14 @@ __global__ void k_or_status(const uint32_t *__restrict__ a, uint32_t *__restrict
   if (d < D) b[d] |= a[d];
 }
 
-// Weft (s/weft, shared.cljc:268-293): keep the root and, per site, the nodes
-// up to and including the site's cut id; count pass, then write pass at koff.
+// Weft (s/weft, shared.cljc:268-293): keep the root and, per named site, the
+// site's yarn up to its cut id: (take-while #(not= id (first %)) yarn) then
+// (conj (new-node [id (get ::nodes id)])).  When the cut id is a node that is
+// the yarn's ids <= cut (yarns are id-sorted).  When it is not, take-while
+// keeps the WHOLE yarn and (new-node [id nil]) = (into [id] nil) = [id] is a
+// one-element node: cause nil, (peek node) = the id itself.  Such a node goes
+// after the kept nodes (id = cut, cause nil, kind normal, ksrc = UINT32_MAX)
+// and the document gets CW_STATUS_WEFT.  Count pass, then write pass at koff.
 template <int NT>
 __global__ __launch_bounds__(NT) void k_weft_select(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
@@ -2485,6 +2494,12 @@ __global__ __launch_bounds__(NT) void k_weft_select(
   const uint64_t *dc = cut + ((size_t)d << site_bits);
   for (uint32_t i = threadIdx.x; i < 32; i += NT) found[i] = 0;
   __syncthreads();
+  for (uint32_t i = threadIdx.x; i < n; i += NT) {  // which cut ids are nodes
+    const uint64_t k = id_key[base + i];
+    const uint32_t site = (uint32_t)(k >> site_shift) & smask;
+    if (dc[site] != 0 && k == dc[site]) atomicOr(&found[site >> 5], 1u << (site & 31));
+  }
+  __syncthreads();
   uint32_t run = 0;
   for (uint32_t i0 = 0; i0 < n; i0 += NT) {
     const uint32_t i = i0 + threadIdx.x;
@@ -2494,8 +2509,8 @@ __global__ __launch_bounds__(NT) void k_weft_select(
       k = id_key[base + i];
       const uint32_t site = (uint32_t)(k >> site_shift) & smask;
       const uint64_t c = dc[site];
-      keep = (kind[base + i] & KIND_ROOT) || (c != 0 && k <= c);
-      if (pass == 0 && c != 0 && k == c) atomicOr(&found[site >> 5], 1u << (site & 31));
+      const bool hit = (found[site >> 5] >> (site & 31)) & 1u;
+      keep = (kind[base + i] & KIND_ROOT) || (c != 0 && (!hit || k <= c));
     }
     uint32_t tot;
     const uint32_t pos = run + block_exscan<NT>(keep ? 1u : 0u, wtot, &tot);
@@ -2508,16 +2523,25 @@ __global__ __launch_bounds__(NT) void k_weft_select(
     }
     run += tot;
   }
-  if (pass == 0) {
-    __syncthreads();
-    bool missing = false;
-    for (uint32_t s = threadIdx.x; s < S; s += NT)
-      missing |= dc[s] != 0 && !((found[s >> 5] >> (s & 31)) & 1u);
-    missing = __syncthreads_or(missing);
-    if (threadIdx.x == 0) {
-      kcount[d] = run;
-      kstatus[d] = missing ? (uint32_t)CW_STATUS_WEFT : 0u;
+  // the [id] nodes of cut ids that are not nodes, in site order
+  uint32_t miss = 0;
+  for (uint32_t s0 = 0; s0 < S; s0 += NT) {
+    const uint32_t s = s0 + threadIdx.x;
+    const bool m = s < S && dc[s] != 0 && !((found[s >> 5] >> (s & 31)) & 1u);
+    uint32_t tot;
+    const uint32_t pos = run + miss + block_exscan<NT>(m ? 1u : 0u, wtot, &tot);
+    if (pass == 1 && m) {
+      const uint32_t o = koff[d] + pos;
+      kid[o] = dc[s];
+      kcause[o] = CW_NIL;
+      kkind[o] = 0;
+      ksrc[o] = 0xFFFFFFFFu;
     }
+    miss += tot;
+  }
+  if (pass == 0 && threadIdx.x == 0) {
+    kcount[d] = run + miss;
+    kstatus[d] = miss ? (uint32_t)CW_STATUS_WEFT : 0u;
   }
 }
 
@@ -2783,6 +2807,7 @@ struct cw_ctx {
                                    // go through the giant path document by document
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
+  bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
 };
 
 namespace {
@@ -3422,6 +3447,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
   if (out->visible_bits && N)
     HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
+  c->x_hint = true;  // unknown unless the fused front end counts the flagged documents
 
   uint32_t key_bits = bt->key_bits;
   if (key_bits == 0 && N && find_key_bits(c, id_key, N, &key_bits)) return -1;
@@ -3487,10 +3513,11 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         fprintf(stderr, "front phases (memtime ticks per doc): dir %.0f rank %.0f write %.0f sval %.0f "
                 "svwrite %.0f\n", a[0] / D, a[1] / D, a[2] / D, a[3] / D, a[4] / D);
       }
-      HIPCHK(c, hipMemcpyAsync(c->pin_small, big, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, big, 8, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       if (c->pin_small[0] == 0) {
         front_done = true;
+        c->x_hint = c->pin_small[1] != 0;  // flagged documents, for the exact path
       } else {  // a document's ids leave the small directory: the three-kernel front end
         HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
         sval = nullptr;
@@ -3601,6 +3628,12 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   return 0;
 }
 
+}  // namespace
+
+#include "exact.hip"
+
+namespace {
+
 int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace) {
   if (!bt || !res) return fail(c, "null batch/result");
   const uint64_t D = bt->n_docs;
@@ -3661,13 +3694,19 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   // (estimated times: the per-document tree sweeps ~22 ns a node in one
   // workgroup, all documents at once; the giant path costs ~0.4 ms a call plus
   // ~0.3 ns a node, documents one after another)
+  // A document below giant_min goes through its one-document sub-call on the
+  // per-document tree (one workgroup), so it counts at that rate.
   double t_tree = 0, t_giant = 0;
+  uint64_t nd_max = 0;
   for (uint64_t d = 0; d < D; d++) {
-    const double nd = (double)(bt->doc_offsets[d + 1] - bt->doc_offsets[d]);
+    const uint64_t n = bt->doc_offsets[d + 1] - bt->doc_offsets[d];
+    const double nd = (double)n;
+    nd_max = std::max(nd_max, n);
     t_tree = std::max(t_tree, nd * 22e-9);
-    t_giant += 0.4e-3 + nd * 0.3e-9;
+    t_giant += n >= c->giant_min ? 0.4e-3 + nd * 0.3e-9 : 0.1e-3 + nd * 22e-9;
   }
-  if (D > 1 && D <= c->giant_docs_max && t_giant < t_tree) {
+  bool x_hint = false;
+  if (D > 1 && D <= c->giant_docs_max && nd_max >= c->giant_min && t_giant < t_tree) {
     if (dres.visible_bits)
       HIPCHK(c, hipMemsetAsync(dres.visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
     for (uint64_t d = 0; d < D; d++) {
@@ -3696,6 +3735,7 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
       }
       sr.visible_bits = vb;
       if (weave_lists_device(c, &sb, id + b, cause + b, kind + b, &sr)) return -1;
+      x_hint |= c->x_hint;
       if (vb) {
         const uint32_t words = (uint32_t)((nd + 31) / 32);
         hipLaunchKernelGGL(k_or_bits_at, dim3((words + 255) / 256), dim3(256), 0, c->stream, vb,
@@ -3703,9 +3743,12 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
         if (check_launch(c, "or_bits")) return -1;
       }
     }
-  } else if (weave_lists_device(c, bt, id, cause, kind, &dres)) {
-    return -1;
+  } else {
+    if (weave_lists_device(c, bt, id, cause, kind, &dres)) return -1;
+    x_hint = c->x_hint;
   }
+  // documents outside the fast path's domain: the literal fold (exact.hip)
+  if (exact_fixup(c, bt, id, cause, kind, &dres, x_hint)) return -1;
 
   if (memspace == CW_MEM_HOST) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -3802,8 +3845,8 @@ __global__ __launch_bounds__(256) void k_lookup(const uint64_t *__restrict__ ske
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= m) return;
   const uint64_t kmin = skey[0], kmax = skey[n - 1], x = q[i];
-  uint32_t r = CW_NOT_FOUND;
-  if (x >= kmin && x <= kmax) {
+  uint32_t r = x == CW_NIL ? CW_NIL_RANK : CW_NOT_FOUND;
+  if (x >= kmin && x <= kmax && x != CW_NIL) {
     const uint32_t sh = bucket_shift(kmax - kmin, n), h = (uint32_t)((x - kmin) >> sh);
     uint32_t lo = bkt[h], hi = bkt[h + 1];
     while (lo < hi) {
@@ -3825,7 +3868,8 @@ __global__ __launch_bounds__(256) void k_ranked_check(const uint32_t *__restrict
   if (r < n) {
     const bool root = (kind[r] & KIND_ROOT) != 0;
     if ((r == 0) != root) st |= CW_STATUS_ROOT;
-    if (r > 0 && par[r] >= r) st |= par[r] == CW_NOT_FOUND ? CW_STATUS_ORPHAN : CW_STATUS_NON_LAMPORT;
+    if (r > 0 && par[r] >= r)
+      st |= par[r] >= CW_NIL_RANK ? CW_STATUS_ORPHAN : CW_STATUS_NON_LAMPORT;
   }
   if (__syncthreads_or(st != 0)) {
     if (st) atomicOr(status, st);
@@ -3859,9 +3903,9 @@ int sort_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t n64, uint32_t key_b
 }
 
 int lookup_keys_impl(cw_ctx *c, const uint64_t *sorted, uint64_t n64, const uint64_t *q,
-                     uint64_t m, uint32_t base, uint32_t *out) {
-  if (m == 0) return 0;
-  if (!q || !out || (n64 && !sorted)) return fail(c, "null array");
+                     uint64_t m, uint32_t base, uint32_t *out, uint32_t *status) {
+  if (m == 0 && (!status || n64 == 0)) return 0;
+  if ((m && (!q || !out)) || (n64 && !sorted)) return fail(c, "null array");
   if (n64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)n64);
   HIPCHK(c, hipSetDevice(c->device));
   if (n64 == 0) {
@@ -3870,13 +3914,17 @@ int lookup_keys_impl(cw_ctx *c, const uint64_t *sorted, uint64_t n64, const uint
   }
   const uint32_t n = (uint32_t)n64;
   uint32_t *bkt = scratch_t<uint32_t>(c, "lk_bkt", (size_t)std::max(n >> 2, 1u) + 2);
-  uint32_t *st = scratch_t<uint32_t>(c, "lk_status", 1);
+  // repeated ids (the same id held by two ranks meets at its owner) go to the
+  // caller's status word, or to a scratch word nobody reads
+  uint32_t *st = status ? status : scratch_t<uint32_t>(c, "lk_status", 1);
   if (!bkt || !st) return fail(c, "out of device memory (lookup)");
+  if (!status) HIPCHK(c, hipMemsetAsync(st, 0, 4, c->stream));
   {
     Launch L(c, "lk_index", (double)n * 8);
     hipLaunchKernelGGL(k_index_flat, dim3((n + 255) / 256), dim3(256), 0, c->stream, sorted, n, bkt, st);
   }
   if (check_launch(c, "lk_index")) return -1;
+  if (m == 0) return 0;
   {
     Launch L(c, "lookup", (double)m * (8 + 4 + 8 + 8));
     hipLaunchKernelGGL(k_lookup, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, c->stream, sorted,
@@ -3970,6 +4018,13 @@ int weave_ranked_impl(cw_ctx *c, const cw_ranked_list *in, cw_list_result *out) 
                      in->kind, n, out->status);
   if (check_launch(c, "ranked_check")) return -1;
   if (weave_tail(c, 1, n, true, in->par, in->kind, in->val, nullptr, nullptr, 0, out)) return -1;
+  {  // flagged (orphan / non-Lamport / root): the literal fold (exact.hip)
+    if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, out->status, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((c->pin_small[0] & X_MASK) && !(c->pin_small[0] & CW_STATUS_DUP) && exact_ranked(c, in, out))
+      return -1;
+  }
   if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->prof) return collect_prof(c);
   return 0;
@@ -4335,6 +4390,7 @@ int merge_lists_impl(cw_ctx *c, const cw_merge_batch *bt, cw_merge_result *res, 
       (W.max_ts && !lr.max_ts) || (W.yarn_perm && !lr.yarn_perm))
     return fail(c, "out of device memory (merge outputs)");
   if (weave_lists_device(c, &lb, mid, mca, mkd, &lr)) return -1;
+  if (exact_fixup(c, &lb, mid, mca, mkd, &lr, c->x_hint)) return -1;
   hipLaunchKernelGGL(k_or_status, dim3((uint32_t)((D + 255) / 256)), dim3(256), 0, c->stream, mst,
                      lr.status, (uint32_t)D);
   if (check_launch(c, "or_status")) return -1;
@@ -4380,9 +4436,12 @@ int weft_lists_impl(cw_ctx *c, const cw_weft_batch *bt, cw_weft_result *res, int
   uint64_t *cut = scratch_t<uint64_t>(c, "w_cut", std::max<size_t>(NC, 1));
   uint32_t *doff = scratch_t<uint32_t>(c, "w_off", D + 1), *koff = scratch_t<uint32_t>(c, "w_koff", D + 1);
   uint32_t *kcnt = scratch_t<uint32_t>(c, "w_kcnt", D + 1), *kst = scratch_t<uint32_t>(c, "w_kst", D + 1);
-  uint64_t *kid = scratch_t<uint64_t>(c, "w_kid", Ns), *kca = scratch_t<uint64_t>(c, "w_kca", Ns);
-  uint8_t *kkd = scratch_t<uint8_t>(c, "w_kkd", Ns);
-  uint32_t *ksrc = scratch_t<uint32_t>(c, "w_ksrc", Ns);
+  // kept nodes: at most the document's nodes plus one [id] node per named site
+  const size_t NKcap = Ns + NC;
+  if (N + NC >= 0xFFFFFFFFull) return fail(c, "batch too large");
+  uint64_t *kid = scratch_t<uint64_t>(c, "w_kid", NKcap), *kca = scratch_t<uint64_t>(c, "w_kca", NKcap);
+  uint8_t *kkd = scratch_t<uint8_t>(c, "w_kkd", NKcap);
+  uint32_t *ksrc = scratch_t<uint32_t>(c, "w_ksrc", NKcap);
   if (!id || !ca || !kd || !cut || !doff || !koff || !kcnt || !kst || !kid || !kca || !kkd || !ksrc)
     return fail(c, "out of device memory (weft)");
   if (!grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
@@ -4429,6 +4488,7 @@ int weft_lists_impl(cw_ctx *c, const cw_weft_batch *bt, cw_weft_result *res, int
       (W.max_ts && !lr.max_ts) || (W.yarn_perm && !lr.yarn_perm))
     return fail(c, "out of device memory (weft outputs)");
   if (weave_lists_device(c, &lb, kid, kca, kkd, &lr)) return -1;
+  if (exact_fixup(c, &lb, kid, kca, kkd, &lr, c->x_hint)) return -1;
   hipLaunchKernelGGL(k_or_status, dim3((uint32_t)((D + 255) / 256)), dim3(256), 0, c->stream, kst,
                      lr.status, (uint32_t)D);
   if (check_launch(c, "or_status")) return -1;
@@ -4591,10 +4651,10 @@ int cw_sort_keys(cw_ctx *c, const uint64_t *keys, uint64_t n, uint32_t key_bits,
 }
 
 int cw_lookup_keys(cw_ctx *c, const uint64_t *sorted, uint64_t n, const uint64_t *queries,
-                   uint64_t m, uint32_t base, uint32_t *out) {
+                   uint64_t m, uint32_t base, uint32_t *out, uint32_t *status) {
   if (!c) return -1;
   c->err.clear();
-  if (lookup_keys_impl(c, sorted, n, queries, m, base, out)) return -1;
+  if (lookup_keys_impl(c, sorted, n, queries, m, base, out, status)) return -1;
   if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }

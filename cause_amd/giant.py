@@ -93,13 +93,16 @@ class HipOps:
 
     @_on_stream
     def lookup(self, sorted_keys, queries, base):
+        """(global rank of each query or NOT_FOUND, CW_STATUS_DUP if the owner's
+        sorted ids repeat one)."""
         m = queries.numel()
         out = self._e(m, torch.int32)
-        if m:
+        st = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        if m or sorted_keys.numel():
             self.w.lookup_keys_device(sorted_keys.data_ptr() if sorted_keys.numel() else 0,
-                                      sorted_keys.numel(), queries.data_ptr(), m, base,
-                                      out.data_ptr())
-        return out
+                                      sorted_keys.numel(), queries.data_ptr() if m else 0, m,
+                                      base, out.data_ptr() if m else 0, st.data_ptr())
+        return out, int(st.item())
 
     @_on_stream
     def gather(self, src, idx):
@@ -262,7 +265,7 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
     perm, qsend = ops.partition(oca, split_t)
     qrecv = _exchange_counts(qsend, group, dev)
     rq = _a2a(ops.gather(oca, perm), qsend, qrecv, group)
-    ans = ops.lookup(ok, rq, own_base)
+    ans, dup = ops.lookup(ok, rq, own_base)
     back = _a2a(ans, qrecv, qsend, group)
     par = ops.scatter32(back, perm)
     del perm, rq, ans, back, oca
@@ -273,10 +276,13 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
     g_par = _a2a(par, gsend, grecv, group)
     g_kd = _a2a(okd, gsend, grecv, group)
     g_org = _a2a(oorg, gsend, grecv, group)
-    mx = _all_gather_ints([local_max], group, dev)
+    mx = _all_gather_ints([local_max, dup], group, dev)
     max_ts = max(v[0] for v in mx)
+    dups = 0
+    for v in mx:  # an id held twice meets itself at its owner (shared.cljc:166-171)
+        dups |= v[1]
     if r != root:
         return GiantResult(None, None, None, None, N, n_own, max_ts)
     o = ops.weave_ranked(g_par, g_kd, g_org)
     return GiantResult(o["weave_perm"], o["visible_bits"], int(o["visible_count"][0]),
-                       int(o["status"][0]), N, n_own, max_ts)
+                       int(o["status"][0]) | dups, N, n_own, max_ts)

@@ -105,12 +105,14 @@ class PackedDoc:
     site_rank: dict
 
 
-def layout_for(docs) -> KeyLayout:
+def layout_for(docs, extra_ids=None) -> KeyLayout:
     """Smallest layout that holds every id and id-cause of ``docs``
-    (each doc: iterable of nodes ``(id, cause, value)``)."""
+    (each doc: iterable of nodes ``(id, cause, value)``), plus ``extra_ids[d]``
+    (ids that must pack in document d without being nodes, e.g. weft cuts)."""
     mts = msite = mtx = 0
-    for nodes in docs:
+    for d, nodes in enumerate(docs):
         ids = [n[0] for n in nodes] + [n[1] for n in nodes if is_id(n[1])]
+        ids += list(extra_ids[d]) if extra_ids else []
         sites = {i[1] for i in ids}
         msite = max(msite, len(sites) - 1 if sites else 0)
         for ts, _, tx in ids:
@@ -124,16 +126,20 @@ def layout_for(docs) -> KeyLayout:
     return lay
 
 
-def pack_doc(nodes, layout: KeyLayout) -> PackedDoc:
-    """Pack one document's nodes (``(id, cause, value)`` tuples, any order)."""
+def pack_doc(nodes, layout: KeyLayout, extra_ids=()) -> PackedDoc:
+    """Pack one document's nodes (``(id, cause, value)`` tuples, any order;
+    weft's one-element ``(id,)`` node has cause nil and its id as value)."""
     nodes = list(nodes)
-    ids = [n[0] for n in nodes] + [n[1] for n in nodes if is_id(n[1])]
+    ids = [n[0] for n in nodes] + [n[1] for n in nodes if len(n) > 1 and is_id(n[1])]
+    ids += list(extra_ids)
     rank = intern_sites(ids)
     n = len(nodes)
     idk = np.empty(n, np.uint64)
     ck = np.empty(n, np.uint64)
     kd = np.empty(n, np.uint8)
-    for i, (nid, cause, value) in enumerate(nodes):
+    for i, nd in enumerate(nodes):
+        nid = nd[0]
+        cause, value = (nd[1], nd[-1]) if len(nd) > 1 else (None, nid)
         idk[i] = layout.pack(nid[0], rank[nid[1]], nid[2])
         if cause is None:
             ck[i] = NIL
@@ -158,13 +164,14 @@ class PackedBatch:
     docs: list             # PackedDoc per document
 
 
-def pack_lists(docs, min_site_bits: int = 0) -> PackedBatch:
-    """Pack a batch of list documents (each an iterable of nodes incl. root)."""
+def pack_lists(docs, min_site_bits: int = 0, extra_ids=None) -> PackedBatch:
+    """Pack a batch of list documents (each an iterable of nodes incl. root);
+    ``extra_ids[d]``: ids that must pack in document d without being nodes."""
     docs = [list(d) for d in docs]
-    lay = layout_for(docs)
+    lay = layout_for(docs, extra_ids)
     if lay.site_bits < min_site_bits:
         lay = KeyLayout(lay.ts_bits, min_site_bits, lay.tx_bits)
-    packed = [pack_doc(d, lay) for d in docs]
+    packed = [pack_doc(d, lay, extra_ids[j] if extra_ids else ()) for j, d in enumerate(docs)]
     off = np.zeros(len(docs) + 1, np.uint64)
     off[1:] = np.cumsum([len(d) for d in docs], dtype=np.uint64)
     cat = lambda f, dt: (np.concatenate([getattr(p, f) for p in packed]) if packed

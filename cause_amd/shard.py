@@ -27,11 +27,16 @@ def doc_range(rank: int, world: int, docs_per_rank: int | None = None,
     return begin, begin + q + (1 if rank < r else 0)
 
 
+def _dev(dist, device):
+    """gloo reduces host tensors (it also carries ranks that share one GPU)."""
+    return device if dist.get_backend() == "nccl" else None
+
+
 def reduce_max_time(seconds: float, dist, device=None) -> float:
     """MAX over ranks of a per-rank wall time (the bench's whole-job time)."""
     import torch
 
-    t = torch.tensor([seconds], dtype=torch.float64, device=device)
+    t = torch.tensor([seconds], dtype=torch.float64, device=_dev(dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -40,6 +45,6 @@ def reduce_sum(values, dist, device=None):
     """SUM over ranks of a list of integers (e.g. nodes woven, checksums)."""
     import torch
 
-    t = torch.tensor(list(values), dtype=torch.int64, device=device)
+    t = torch.tensor(list(values), dtype=torch.int64, device=_dev(dist, device))
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return [int(x) for x in t.tolist()]

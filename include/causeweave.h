@@ -213,14 +213,19 @@ int cw_merge_lists(cw_ctx *ctx, const cw_merge_batch *batch, cw_merge_result *re
                    int memspace);
 
 /* ----------------------------------------------------------------- weft ---- */
-/* s/weft (shared.cljc:268-293), time travel: per document, each named site's
- * yarn up to and including its cut id, the root, nothing of the other sites,
- * then the full reweave.  cut[(d << site_bits) | site_rank] is the packed cut
- * id of that site, or 0 for a site that is not named (its nodes are dropped).
- * A cut id that is not a node of the document sets CW_STATUS_WEFT (the
- * reference then weaves a [id nil nil] node).  Cuts that do not preserve
- * causality leave orphans: CW_STATUS_ORPHAN (the reference's "gibberish
- * trees").  ::lamport-ts of the result is the largest cut ts (max_ts). */
+/* s/weft (shared.cljc:268-293), time travel: per document, the root and each
+ * named site's yarn up to and including its cut id, nothing of the other
+ * sites, then the full reweave.  cut[(d << site_bits) | site_rank] is the
+ * packed cut id of that site, or 0 for a site that is not named (its nodes are
+ * dropped).  A cut id that is not a node of the document keeps the site's
+ * whole yarn (take-while never stops) plus the node (new-node [id nil]) =
+ * [id] -- cause nil, its value (peek) the id itself -- which kept_src marks
+ * UINT32_MAX; the document gets CW_STATUS_WEFT and its weave is still the
+ * reference's (exact path).  Cuts that do not preserve causality leave
+ * orphans ("gibberish trees"): CW_STATUS_ORPHAN, woven like the reference.
+ * ::lamport-ts of the result is the largest cut ts (max_ts is the largest kept
+ * id's ts: the caller takes the cuts' max).  Kept arrays need room for
+ * N + (n_docs << site_bits) nodes. */
 typedef struct {
   cw_list_batch nodes;   /* site_bits must be 1..10                           */
   const uint64_t *cut;   /* HOST memory [n_docs << site_bits]                */
@@ -228,8 +233,9 @@ typedef struct {
 
 typedef struct {
   uint64_t *kept_offsets; /* HOST memory [n_docs+1]                          */
-  uint32_t *kept_src;     /* [N]: doc-local input index of each kept node, in
-                             input order                                      */
+  uint32_t *kept_src;     /* [N + (n_docs << site_bits)]: doc-local input index of
+                             each kept node, in input order, then UINT32_MAX for
+                             each [id] node of a cut id that is not a node        */
   cw_list_result weave;   /* laid out by kept_offsets; weave_perm holds indices
                              into kept_src                                     */
 } cw_weft_result;
@@ -244,6 +250,7 @@ int cw_weft_lists(cw_ctx *ctx, const cw_weft_batch *batch, cw_weft_result *resul
  * ordered on the context's stream. */
 
 #define CW_NOT_FOUND 0xFFFFFFFFu
+#define CW_NIL_RANK 0xFFFFFFFEu /* the rank of a nil cause (cw_lookup_keys of CW_NIL) */
 
 /* (sort ::nodes) of one document's ids (list.cljc:28, shared.cljc:128):
  * keys_out = keys ascending, idx_out[i] = input index of keys_out[i] (stable).
@@ -251,10 +258,13 @@ int cw_weft_lists(cw_ctx *ctx, const cw_weft_batch *batch, cw_weft_result *resul
 int cw_sort_keys(cw_ctx *ctx, const uint64_t *keys, uint64_t n, uint32_t key_bits,
                  uint64_t *keys_out, uint32_t *idx_out);
 
-/* out[i] = base + index of queries[i] among the n ascending unique keys
- * `sorted`, or CW_NOT_FOUND (the cause join of s/insert, shared.cljc:175-178). */
+/* out[i] = base + index of queries[i] among the n ascending keys `sorted`, or
+ * CW_NOT_FOUND (the cause join of s/insert, shared.cljc:175-178).  status
+ * (device memory, or NULL): OR'ed with CW_STATUS_DUP when `sorted` repeats a
+ * key -- an id held twice (::nodes is a map, shared.cljc:62, 166-171); the
+ * check runs even when m = 0. */
 int cw_lookup_keys(cw_ctx *ctx, const uint64_t *sorted, uint64_t n, const uint64_t *queries,
-                   uint64_t m, uint32_t base, uint32_t *out);
+                   uint64_t m, uint32_t base, uint32_t *out, uint32_t *status);
 
 /* Group m keys by bucket among n_split ascending splitters (bucket of x = the
  * number of splitters <= x; n_split <= 1023): perm lists the key indices

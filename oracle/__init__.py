@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
-METHOD_LITERAL, METHOD_LINKED, METHOD_EFF = 0, 1, 2
+METHOD_LITERAL, METHOD_LINKED, METHOD_EFF, METHOD_GENERAL = 0, 1, 2, 3
 
 
 def lib():
@@ -30,7 +30,8 @@ def lib():
             raise RuntimeError(f"{path} missing: run `make oracle`")
         L = C.CDLL(path)
         u64p, u32p, u8p = (C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_uint8))
-        for name in ("or_list_fold_literal", "or_list_fold_linked", "or_list_eff_preorder"):
+        for name in ("or_list_fold_literal", "or_list_fold_linked", "or_list_eff_preorder",
+                     "or_list_fold_general"):
             f = getattr(L, name)
             f.restype = C.c_uint32
             f.argtypes = [C.c_size_t, u64p, u64p, u8p, u32p]
@@ -65,7 +66,7 @@ def list_weave(id_key, cause_key, kind, method=METHOD_LITERAL):
     n = len(i)
     out = np.zeros(n, np.uint32)
     f = {METHOD_LITERAL: lib().or_list_fold_literal, METHOD_LINKED: lib().or_list_fold_linked,
-         METHOD_EFF: lib().or_list_eff_preorder}[method]
+         METHOD_EFF: lib().or_list_eff_preorder, METHOD_GENERAL: lib().or_list_fold_general}[method]
     st = f(n, _p(i, C.c_uint64), _p(c, C.c_uint64), _p(k, C.c_uint8), _p(out, C.c_uint32))
     return out, int(st)
 

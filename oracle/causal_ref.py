@@ -77,11 +77,12 @@ def first(x):
 
 
 def second(x):
-    return None if x is None else x[1]
+    return None if x is None or len(x) < 2 else x[1]
 
 
 def peek_node(x):
-    return None if x is None else x[2]
+    """(peek node): the value -- the id itself for weft's one-element [id] node."""
+    return None if x is None else x[-1]
 
 
 def valid_id(x) -> bool:
@@ -165,7 +166,8 @@ def new_map_ct(site_id=None, uuid=None, rng=random):
 
 
 def _node_of(i, body):
-    return (i, body[0], body[1])
+    """(new-node [k v]) = (into [k] v), shared.cljc:78-79 (body () -> [id])."""
+    return (i,) + tuple(body)
 
 
 def spin_sequential(ct, nodes):
@@ -229,14 +231,15 @@ def refresh_caches(weave_fn, ct):
 def yarns_to_nodes(ct):
     """shared.cljc:251-257"""
     out = dict(ct)
-    out["nodes"] = {n[0]: (n[1], n[2]) for y in ct["yarns"].values() for n in y}
+    out["nodes"] = {n[0]: tuple(n[1:]) for y in ct["yarns"].values() for n in y}
     return out
 
 
 def weft(weave_fn, new_ct_fn, ct, ids):
     """shared.cljc:268-293: each named site's yarn up to and including its cut
-    id (``(new-node [id (get nodes id)])``: a missing id becomes [id nil nil]),
-    then yarns->nodes and the full reweave."""
+    id, then yarns->nodes and the full reweave.  A cut id that is not a node
+    keeps the whole yarn (take-while never stops) and adds
+    ``(new-node [id nil])`` = ``(into [id] nil)`` = the one-element node [id]."""
     filtered = [i for i in ids if i != ROOT_ID]
     new = new_ct_fn()
     yarns = dict(new["yarns"])
@@ -247,7 +250,7 @@ def weft(weave_fn, new_ct_fn, ct, ids):
                 break
             pre.append(n)
         body = ct["nodes"].get(i)
-        pre.append((i, body[0], body[1]) if body is not None else (i, None, None))
+        pre.append(_node_of(i, body if body is not None else ()))
         yarns[i[1]] = pre
     new["yarns"] = yarns
     new["site_id"] = ct["site_id"]
@@ -345,7 +348,7 @@ def causal_to_edn(v):
 def causal_list_to_edn(ct):
     """list.cljc:57-66"""
     w = ct["weave"]
-    return [causal_to_edn(n[2]) for k, n in enumerate(w)
+    return [causal_to_edn(peek_node(n)) for k, n in enumerate(w)
             if not hide_q(n, w[k + 1] if k + 1 < len(w) else None)]
 
 

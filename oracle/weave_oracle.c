@@ -216,6 +216,55 @@ uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause
   return st;
 }
 
+/* The full reweave restated for ANY causes (the rule exact.hip's k_xfold
+ * implements; derived from shared.cljc:194-241 with ids folded in ascending
+ * order, so clauses B and C of weave-later? never hold): a node goes right
+ * after its cause, or at the front when the cause is nil, or right before an
+ * already woven node it causes -- whichever split comes first; a non-special
+ * node then skips specials not caused by it; with no such split it is
+ * appended.  Checked against the literal fold on out-of-domain histories. */
+uint32_t or_list_fold_general(size_t n, const uint64_t *id, const uint64_t *cause,
+                              const uint8_t *kind, uint32_t *out_perm) {
+  lnode *s = sorted_nodes(n, id, cause, kind);
+  uint32_t st = doc_status(s, n);
+  const uint32_t END = UINT32_MAX, HEAD = UINT32_MAX - 1, NIL = UINT32_MAX - 2;
+  uint32_t *par = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint32_t *next = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+  uint8_t *early = (uint8_t *)calloc(n ? n : 1, 1);
+  for (size_t r = 0; r < n; r++) {
+    size_t c = find_id(s, n, s[r].cause);
+    par[r] = s[r].cause == OR_NIL ? NIL : (c == n ? END : (uint32_t)c);
+    if (c < n && c > r) early[c] = 1;
+  }
+  uint32_t head = END, tail = END;
+  for (uint32_t m = 0; m < n; m++) {
+    uint32_t c = par[m], p = END;
+    if (c == NIL) p = HEAD;
+    else if (early[m]) {
+      uint32_t prev = HEAD;
+      for (uint32_t v = head; v != END; prev = v, v = next[v]) {
+        if (par[v] == m) { p = prev; break; }
+        if (v == c) { p = v; break; }
+      }
+    } else if (c < m) p = c;
+    if (p == END) p = tail == END ? HEAD : tail;
+    else if (!is_special(s[m].kind))
+      for (;;) {
+        uint32_t q = p == HEAD ? head : next[p];
+        if (q == END || !is_special(s[q].kind) || par[q] == m) break;
+        p = q;
+      }
+    uint32_t q = p == HEAD ? head : next[p];
+    next[m] = q;
+    if (p == HEAD) head = m; else next[p] = m;
+    if (q == END) tail = m;
+  }
+  size_t k = 0;
+  for (uint32_t v = head; v != END; v = next[v]) out_perm[k++] = s[v].idx;
+  free(par); free(next); free(early); free(s);
+  return st;
+}
+
 /* preorder of the effective tree, walked with the same
  * (first child, next sibling, parent) links the HIP Euler walk uses. */
 uint32_t or_list_eff_preorder(size_t n, const uint64_t *id, const uint64_t *cause,
@@ -325,7 +374,8 @@ static void *batch_worker(void *arg) {
     uint32_t st;
     if (J->method == 0) st = or_list_fold_literal(n, J->id + b, J->cause + b, J->kind + b, J->perm + b);
     else if (J->method == 1) st = or_list_fold_linked(n, J->id + b, J->cause + b, J->kind + b, J->perm + b);
-    else st = or_list_eff_preorder(n, J->id + b, J->cause + b, J->kind + b, J->perm + b);
+    else if (J->method == 2) st = or_list_eff_preorder(n, J->id + b, J->cause + b, J->kind + b, J->perm + b);
+    else st = or_list_fold_general(n, J->id + b, J->cause + b, J->kind + b, J->perm + b);
     if (J->vis) or_list_visible_literal(n, J->id + b, J->cause + b, J->kind + b, J->perm + b, J->vis + b);
     if (J->status) J->status[d] = st;
   }

@@ -67,6 +67,12 @@ uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause
 uint32_t or_list_eff_preorder(size_t n, const uint64_t *id, const uint64_t *cause,
                               const uint8_t *kind, uint32_t *out_perm);
 
+/* The full reweave for ANY causes (orphans, non-Lamport causes, nil causes, a
+ * missing root): the rule of the product's exact path, stated on sorted nodes
+ * and checked against or_list_fold_literal by the tests. */
+uint32_t or_list_fold_general(size_t n, const uint64_t *id, const uint64_t *cause,
+                              const uint8_t *kind, uint32_t *out_perm);
+
 /* Literal hide? over a weave (list.cljc:48-55 with partition 2 1 [nil],
  * list.cljc:57-66): vis[p] = 1 iff the node at weave position p is rendered. */
 void or_list_visible_literal(size_t n, const uint64_t *id, const uint64_t *cause,
@@ -78,7 +84,7 @@ void or_list_yarns(size_t n, const uint64_t *id, unsigned site_shift, uint64_t s
                    uint32_t *yarn_perm);
 
 /* ---- batches ---------------------------------------------------------------
- * method: 0 literal, 1 linked, 2 effective-tree.  offsets[ndocs+1] index the
+ * method: 0 literal, 1 linked, 2 effective-tree, 3 general.  offsets[ndocs+1] index the
  * flat arrays.  out_perm is doc-local (input index inside the document);
  * out_vis[g] is per weave position (one byte each); out_status[d]. */
 int or_batch_lists(size_t ndocs, const uint64_t *offsets, const uint64_t *id,

@@ -35,7 +35,9 @@ class CpuOps:
         ok = (i < len(s)) & (s[np.minimum(i, max(len(s) - 1, 0))] == q) if len(s) else \
             np.zeros(len(q), bool)
         out = np.where(ok, i + base, NOT_FOUND).astype(np.uint32)
-        return torch.from_numpy(out.view(np.int32))
+        out[q == np.uint64(2**64 - 1)] = 0xFFFFFFFE  # CW_NIL_RANK: a nil cause
+        dup = 2 if len(s) > 1 and bool((s[1:] == s[:-1]).any()) else 0  # CW_STATUS_DUP
+        return torch.from_numpy(out.view(np.int32)), dup
 
     def gather(self, src, idx):
         return src[idx.long()]

@@ -101,6 +101,45 @@ def test_distributed_weave_matches_oracle(world, n, seed, empty):
     assert max(owned.values()) < 2.0 * N / world
 
 
+def _dup_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.giant_cpu_ops import CpuOps
+
+        spec, idk, ck, kd = make_list(3000, 31)
+        sh = shares(len(idk), world, 31)[rank]
+        if rank == 1:  # rank 1 also holds a copy of a node rank 0 owns
+            sh = np.concatenate([sh, shares(len(idk), world, 31)[0][:1]])
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+        lay = spec.layout()
+        res = giant.weave_distributed(CpuOps(), t(idk[sh]), t(ck[sh]),
+                                      torch.from_numpy(kd[sh].copy()), lay.key_bits,
+                                      ts_shift=lay.ts_shift, samples=64)
+        if rank == 0:
+            q.put(res.status)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_weave_flags_an_id_held_by_two_ranks():
+    """The same id on two ranks is a duplicate of the one ::nodes map
+    (shared.cljc:166-171): the owner sees it repeated and the root's status has
+    CW_STATUS_DUP, as the single-GPU path reports."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_dup_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    status = q.get(timeout=120)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert status & 2  # CW_STATUS_DUP
+
+
 def test_choose_splitters_weighted():
     s = np.arange(100, dtype=np.int64)
     w = np.ones(100)

@@ -1,0 +1,173 @@
+"""The exact path on the GPU: documents outside the fast path's domain get the
+reference's literal weave (list.cljc:26-28 -> shared.cljc:225-241), bit-exact
+against oracle METHOD_LITERAL -- order, rendered bits, counts, ::lamport-ts,
+yarns -- with their status bits kept (exact.hip).
+
+Inputs (tests/outdomain.py): absent causes, causes with a larger id, nil
+causes, no root, ids below the root, non-id causes; in tiny reference-style
+histories, the reference's edge cases, config-2-shaped documents up to the
+full 50,001 nodes, next to in-domain documents in the same batch, through every
+front end, host and device memory, and cw_weave_ranked.
+"""
+import dataclasses
+import random
+
+import numpy as np
+import pytest
+
+import oracle
+from cause_amd import abi, gen, pack
+from oracle import causal_ref as R
+from tests import outdomain as X
+from tests import refgen as G
+from tests.test_gpu_parity import check_batch, oracle_batch, weaver  # noqa: F401 (fixture)
+
+pytestmark = pytest.mark.gpu
+
+
+def test_reference_style_histories_every_corruption(weaver):
+    rng = random.Random(4)
+    docs = []
+    for kinds in [(k,) for k in X.KINDS] + [X.KINDS]:
+        for steps in (5, 9, 20, 60):
+            for _ in range(6):
+                nodes, _ = G.random_history(rng, steps)
+                d = X.corrupt([R.ROOT_NODE] + nodes, rng, kinds, rate=0.2)
+                rng.shuffle(d)
+                docs.append(d)
+    for case in G.EDGE_CASES:
+        for k in X.KINDS:
+            docs.append(X.corrupt([R.ROOT_NODE] + list(case), rng, (k,), rate=0.3))
+    b = pack.pack_lists(docs)
+    res = check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    assert (res.status != 0).mean() > 0.8
+
+
+def test_stress_histories_corrupted(weaver):
+    rng = random.Random(8)
+    docs = []
+    for n in (50, 300, 1200):
+        for p_special in (0.1, 0.4):
+            nodes = G.stress_history(rng, n, p_special=p_special, p_conj=0.2, tx_chain=0.1)
+            docs.append(X.corrupt(nodes, rng, X.KINDS, rate=0.03))
+            docs.append(nodes)  # in-domain neighbours
+    b = pack.pack_lists(docs)
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+@pytest.mark.parametrize("n,D", [(3000, 20), (50_000, 6)])
+def test_config2_documents_corrupted(weaver, n, D):
+    """Config-2-shaped documents, every other one broken (the bits of flagged
+    and clean documents share words at the boundaries)."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=n, seed=n + D)
+    off, idk, ck, kd = gen.generate(spec, 0, D, nthreads=8)
+    rng = np.random.default_rng(n)
+    parts = []
+    for d in range(D):
+        a, b = int(off[d]), int(off[d + 1])
+        one = (np.array([0, b - a], np.uint64), idk[a:b], ck[a:b], kd[a:b])
+        if d % 2:
+            one = X.corrupt_packed(*one, rng, rate=0.01)
+        parts.append(one)
+    sizes = [int(p[0][-1]) for p in parts]
+    off2 = np.zeros(D + 1, np.uint64)
+    off2[1:] = np.cumsum(sizes)
+    cat = lambda j: np.concatenate([p[j] for p in parts])
+    res = check_batch(weaver, off2, cat(1), cat(2), cat(3), spec.layout())
+    assert (res.status[1::2] != 0).all() and not res.status[0::2].any()
+
+
+def test_giant_document_corrupted():
+    """One document above the giant-path threshold (one-document batch): the
+    tree runs on the all-parallel path, the fold on one lane."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=150_000, seed=9)
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=8)
+    off, idk, ck, kd = X.corrupt_packed(off, idk, ck, kd, np.random.default_rng(2),
+                                        rate=0.001, which="mixed")
+    with abi.Weaver(0) as w:
+        res = check_batch(w, off, idk, ck, kd, spec.layout())
+    assert res.status[0] & (abi.STATUS_ORPHAN | abi.STATUS_NON_LAMPORT)
+
+
+def test_device_memory_async_corrupted():
+    """Device pointers, the context on a torch stream in async mode: the exact
+    path runs inside the same call (ordered on that stream)."""
+    import torch
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=4000, seed=5)
+    off, idk, ck, kd = gen.generate(spec, 0, 12, nthreads=8)
+    off, idk, ck, kd = X.corrupt_packed(off, idk, ck, kd, np.random.default_rng(3))
+    lay = spec.layout()
+    N, D = len(idk), len(off) - 1
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    g = [t(idk.view(np.int64)), t(ck.view(np.int64)), t(kd)]
+    o = {"weave_perm": torch.empty(N, dtype=torch.int32, device=dev),
+         "visible_bits": torch.empty((N + 31) // 32, dtype=torch.int32, device=dev),
+         "visible_count": torch.empty(D, dtype=torch.int32, device=dev),
+         "max_ts": torch.empty(D, dtype=torch.int64, device=dev),
+         "status": torch.empty(D, dtype=torch.int32, device=dev),
+         "yarn_perm": torch.empty(N, dtype=torch.int32, device=dev)}
+    s = torch.cuda.Stream(dev)
+    with abi.Weaver(0) as w:
+        w.set_stream(s.cuda_stream)
+        w.set_async(True)
+        w.weave_lists_device(off, g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(), lay,
+                             {k: v.data_ptr() for k, v in o.items()})
+        s.synchronize()
+    perm, vis, st, vcount, max_ts = oracle_batch(off, idk, ck, kd, lay)
+    h = {k: v.cpu().numpy() for k, v in o.items()}
+    assert np.array_equal(h["status"].view(np.uint32), st)
+    assert np.array_equal(h["weave_perm"].view(np.uint32), perm)
+    gvis = np.unpackbits(h["visible_bits"].view(np.uint8), bitorder="little")[:N]
+    assert np.array_equal(gvis, vis)
+    assert np.array_equal(h["visible_count"].view(np.uint32), vcount)
+    assert np.array_equal(h["max_ts"].view(np.uint64), max_ts)
+    mask = (1 << lay.site_bits) - 1
+    for d in range(D):
+        a, b = int(off[d]), int(off[d + 1])
+        assert np.array_equal(h["yarn_perm"][a:b].view(np.uint32),
+                              oracle.list_yarns(idk[a:b], lay.site_shift, mask))
+
+
+@pytest.mark.parametrize("case", ["orphan", "non_lamport", "no_root_first"])
+def test_weave_ranked_exact(case):
+    """cw_weave_ranked (the distributed giant list's last step) on a flagged
+    list: the literal fold of the ranks."""
+    import torch
+
+    from cause_amd import giant
+    from tests.test_gpu_giant import ranked_case
+
+    par, kd, val = ranked_case(30_000, 17)
+    par = par.view(np.uint32).copy()
+    kd = kd.copy()
+    rng = np.random.default_rng(1)
+    if case == "orphan":
+        par[rng.choice(np.arange(1, len(par)), 40, replace=False)] = 0xFFFFFFFF
+    elif case == "non_lamport":
+        js = rng.choice(np.arange(1, len(par) - 100), 40, replace=False)
+        par[js] = js + rng.integers(1, 100, len(js))
+    else:
+        kd[0] &= ~np.uint8(4)  # rank 0 not flagged root
+        par[5] = 0xFFFFFFFE    # and a nil cause (CW_NIL_RANK)
+    n = len(par)
+    # the same list as packed ids = ranks for the oracle
+    ids = np.arange(n, dtype=np.uint64)
+    causes = np.where(par == 0xFFFFFFFF, np.uint64(n + 5),
+                      np.where(par == 0xFFFFFFFE, np.uint64(2**64 - 1), par.astype(np.uint64)))
+    if kd[0] & 4:
+        causes[0] = np.uint64(2**64 - 1)
+    want, vis, st = oracle.batch_lists(np.array([0, n], np.uint64), ids, causes, kd,
+                                       method=oracle.METHOD_LITERAL)
+    with abi.Weaver(0) as w:
+        ops = giant.HipOps(w, "cuda:0")
+        dev = torch.device("cuda", 0)
+        got = ops.weave_ranked(torch.from_numpy(par.view(np.int32)).to(dev),
+                               torch.from_numpy(kd).to(dev), torch.from_numpy(val).to(dev))
+        torch.cuda.synchronize()
+    assert int(got["status"][0]) == int(st[0]) != 0
+    assert np.array_equal(got["weave_perm"].cpu().numpy().view(np.uint32), val.view(np.uint32)[want])
+    gvis = np.unpackbits(got["visible_bits"].cpu().numpy().view(np.uint8), bitorder="little")[:n]
+    assert np.array_equal(gvis, vis)
+    assert int(got["visible_count"][0]) == int(vis.sum())

@@ -79,9 +79,26 @@ def test_lookup(ops, n, m, base):
     if len(s):
         hit = rng.integers(0, len(s), m // 2)
         q[: m // 2] = s[hit]
-    got = ops.lookup(_t(_i64(s)), _t(_i64(q)), base).cpu().numpy()
-    ref = CpuOps().lookup(torch.from_numpy(_i64(s)), torch.from_numpy(_i64(q)), base).numpy()
-    assert np.array_equal(got, ref)
+    got, gdup = ops.lookup(_t(_i64(s)), _t(_i64(q)), base)
+    ref, rdup = CpuOps().lookup(torch.from_numpy(_i64(s)), torch.from_numpy(_i64(q)), base)
+    assert np.array_equal(got.cpu().numpy(), ref.numpy())
+    assert gdup == rdup == 0
+
+
+@pytest.mark.parametrize("m", [0, 1000])
+def test_lookup_reports_repeated_ids(ops, m):
+    """An id held by two ranks meets itself at its owner after the sample sort:
+    the owner's sorted run repeats it and cw_lookup_keys flags CW_STATUS_DUP
+    (even with no queries to answer)."""
+    import torch
+
+    s = np.sort(np.random.default_rng(3).integers(0, 1 << 30, 5000, dtype=np.uint64))
+    s[2500] = s[2499]
+    q = s[:m].copy()
+    got, dup = ops.lookup(_t(_i64(s)), _t(_i64(q)), 0)
+    ref, rdup = CpuOps().lookup(torch.from_numpy(_i64(s)), torch.from_numpy(_i64(q)), 0)
+    assert dup == rdup == abi.STATUS_DUP
+    assert np.array_equal(got.cpu().numpy(), ref.numpy())
 
 
 def test_gather_scatter(ops):

@@ -211,10 +211,12 @@ def _ref_ct(nodes, rng):
 
 
 def test_weft_matches_reference_restatement():
-    """shared.cljc:268-293: cut every site's yarn at a random node (or drop the
-    site), keep causally closed cuts, weave; compare with the restatement."""
+    """shared.cljc:268-293: cut every site's yarn at a random node, at an id
+    that is no node, or drop the site; name sites with no node at all; weave;
+    compare with the restatement -- causally closed cuts and the reference's
+    "gibberish trees" alike (the library's exact path weaves those)."""
     rng = random.Random(21)
-    checked = 0
+    checked = gibberish = bogus = 0
     for steps in (5, 20, 60, 150):
         for _ in range(25):
             nodes, _ = G.random_history(rng, steps)
@@ -223,26 +225,34 @@ def test_weft_matches_reference_restatement():
             ids = []
             T = rng.randint(1, max(n[0][0] for n in nodes))
             for s in sites:
-                if rng.random() < 0.25:
+                r = rng.random()
+                if r < 0.2:
                     ids.append(rng.choice(ref["yarns"][s])[0])  # arbitrary cut
-                elif rng.random() < 0.9:  # consistent cut: the site's state at time T
+                elif r < 0.3:
+                    ids.append((rng.randint(1, T + 3), s, 7))     # no such node
+                elif r < 0.9:  # consistent cut: the site's state at time T
                     older = [n for n in ref["yarns"][s] if n[0][0] <= T]
                     if older:
                         ids.append(older[-1][0])
+            if rng.random() < 0.2:
+                ids.append((T, R.new_site_id(rng), 0))            # a site with no node
             if not ids:
                 continue
             want = _weft_ref(ref, ids)
             kept = set(want["nodes"])
-            if any(b[0] is not None and b[0] not in kept for b in want["nodes"].values()):
-                continue  # not causally closed: the reference weaves gibberish
+            gibberish += any(len(b) > 1 and b[0] is not None and b[0] not in kept
+                             for b in want["nodes"].values())
+            bogus += any(len(b) == 0 for b in want["nodes"].values())
             ct = causal.new_list_ct(site_id=ref["site_id"], uuid=ref["uuid"])
             ct["nodes"] = dict(ref["nodes"])
             got = causal.weft(ct, ids)
             assert got["weave"] == want["weave"]
             assert causal.causal_list_to_edn(got) == R.causal_list_to_edn(want)
             assert got["lamport_ts"] == want["lamport_ts"]
+            assert got["nodes"] == want["nodes"]
+            assert got["yarns"] == want["yarns"]
             checked += 1
-    assert checked > 20
+    assert checked > 60 and gibberish > 5 and bogus > 5, (checked, gibberish, bogus)
 
 
 def test_weft_status_bits(weaver):
@@ -261,6 +271,8 @@ def test_weft_status_bits(weaver):
     cut[2 * S + rk[s2]] = lay.pack(2, rk[s2], 0)          # b2 without its cause
     res = weaver.weft_lists(b.offsets, b.id_key, b.cause_key, b.kind, lay, cut)
     st = res.weave.status
-    assert st[0] == 0 and list(np.diff(res.offsets)) == [2, 2, 2]
+    # doc 1: s1's whole yarn (take-while never stops) + the node [(5 s1 0)]
+    assert st[0] == 0 and list(np.diff(res.offsets)) == [2, 3, 2]
     assert st[1] & abi.STATUS_WEFT
+    assert list(res.src[2:5]) == [0, 1, 0xFFFFFFFF]
     assert st[2] & abi.STATUS_ORPHAN
