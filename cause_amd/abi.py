@@ -21,6 +21,7 @@ CW_MEM_HOST, CW_MEM_DEVICE = 0, 1
 STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1, 2, 4, 8, 32
 STATUS_MAP_KEY = 16
 STATUS_WEFT = 64
+STATUS_KEY_RANGE = 128
 
 
 class CwListBatch(C.Structure):
@@ -28,6 +29,11 @@ class CwListBatch(C.Structure):
                 ("id_key", C.c_void_p), ("cause_key", C.c_void_p), ("kind", C.c_void_p),
                 ("key_bits", C.c_uint32), ("ts_shift", C.c_uint32), ("site_shift", C.c_uint32),
                 ("site_bits", C.c_uint32)]
+
+
+class CwListBatchK128(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("doc_offsets", C.POINTER(C.c_uint64)),
+                ("id_key", C.c_void_p), ("cause_key", C.c_void_p), ("kind", C.c_void_p)]
 
 
 class CwListResult(C.Structure):
@@ -112,6 +118,9 @@ def lib():
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
                                      C.c_int]
         L.cw_weave_lists.restype = C.c_int
+        L.cw_weave_lists_k128.argtypes = [C.c_void_p, C.POINTER(CwListBatchK128),
+                                          C.POINTER(CwListResult), C.c_int]
+        L.cw_weave_lists_k128.restype = C.c_int
         L.cw_weave_maps.argtypes = [C.c_void_p, C.POINTER(CwMapBatch), C.POINTER(CwMapResult),
                                     C.c_int]
         L.cw_weave_maps.restype = C.c_int
@@ -281,6 +290,45 @@ class Weaver:
                          g("status"), g("yarn_perm"))
         self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
                     "cw_weave_lists")
+
+    @staticmethod
+    def _batch_k128(offsets, id_ptr, cause_ptr, kind_ptr):
+        off = np.ascontiguousarray(offsets, np.uint64)
+        b = CwListBatchK128()
+        b.n_docs = len(off) - 1
+        b.doc_offsets = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        b.id_key, b.cause_key, b.kind = id_ptr, cause_ptr, kind_ptr
+        return b, off
+
+    def weave_lists_k128(self, offsets, id_key, cause_key, kind, yarns=True) -> ListResult:
+        """Host-memory call of cw_weave_lists_k128: id_key / cause_key are
+        uint64[N, 2] (hi = ts, lo = site_rank << 32 | tx; nil = (NIL, NIL))."""
+        i = np.ascontiguousarray(id_key, np.uint64).reshape(-1, 2)
+        c = np.ascontiguousarray(cause_key, np.uint64).reshape(-1, 2)
+        k = np.ascontiguousarray(kind, np.uint8)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        D, N = len(off) - 1, len(k)
+        if int(off[-1]) != N or len(i) != N or len(c) != N:
+            raise ValueError("offsets[-1] / id_key / cause_key / kind sizes differ")
+        b, off = self._batch_k128(off, _ptr(i), _ptr(c), _ptr(k))
+        out = ListResult(np.zeros(N, np.uint32), np.zeros((N + 31) // 32, np.uint32),
+                         np.zeros(D, np.uint32), np.zeros(D, np.uint64), np.zeros(D, np.uint32),
+                         np.zeros(N, np.uint32) if yarns else None)
+        r = CwListResult(_ptr(out.weave_perm), _ptr(out.visible_bits), _ptr(out.visible_count),
+                         _ptr(out.max_ts), _ptr(out.status), _ptr(out.yarn_perm))
+        self._check(self._L.cw_weave_lists_k128(self._h, C.byref(b), C.byref(r), CW_MEM_HOST),
+                    "cw_weave_lists_k128")
+        return out
+
+    def weave_lists_k128_device(self, offsets, id_ptr, cause_ptr, kind_ptr, out_ptrs):
+        """Device-memory call of cw_weave_lists_k128 (out_ptrs as weave_lists_device)."""
+        b, off = self._batch_k128(offsets, C.c_void_p(id_ptr), C.c_void_p(cause_ptr),
+                                  C.c_void_p(kind_ptr))
+        g = lambda n: C.c_void_p(out_ptrs[n]) if out_ptrs.get(n) else None
+        r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), g("max_ts"),
+                         g("status"), g("yarn_perm"))
+        self._check(self._L.cw_weave_lists_k128(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
+                    "cw_weave_lists_k128")
 
     # --- building blocks of the distributed giant list (device pointers) ---------
     def sort_keys_device(self, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr):

@@ -101,8 +101,12 @@ def weave_lists(cts):
     """Full reweave of many list cts in ONE GPU call (the batch entry point).
     Returns new cts with ::weave, ::yarns, ::lamport-ts and rendered flags."""
     docs = [[(i, b[0], b[1]) for i, b in ct["nodes"].items()] for ct in cts]
-    b = pack.pack_lists(docs)
-    res = weaver().weave_lists(b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    try:
+        b = pack.pack_lists(docs)
+        res = weaver().weave_lists(b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+    except pack.KeyRangeError:  # ids over 63 bits: the K128 layout
+        b = pack.pack_lists_k128(docs)
+        res = weaver().weave_lists_k128(b.offsets, b.id_key, b.cause_key, b.kind)
     vis = res.visible()
     out = []
     for d, (ct, nodes) in enumerate(zip(cts, docs)):

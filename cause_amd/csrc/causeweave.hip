@@ -2176,6 +2176,20 @@ __global__ void k_or_reduce(const uint64_t *__restrict__ keys, uint32_t N,
   if ((threadIdx.x & 63) == 0 && acc) atomicOr(out, (unsigned long long)acc);
 }
 
+// K64 keys are < 2^63 (include/causeweave.h): flag the documents of a batch
+// whose ids use the top bit (run only when the batch's keys reach 64 bits).
+__global__ __launch_bounds__(256) void k_key_range(const uint64_t *__restrict__ id,
+                                                   const uint32_t *__restrict__ tile_start,
+                                                   const uint32_t *__restrict__ tile_doc,
+                                                   uint32_t *__restrict__ status) {
+  const uint32_t t = blockIdx.x;
+  bool hi = false;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x)
+    hi |= (id[i] >> 63) != 0;
+  if (__syncthreads_or(hi) && threadIdx.x == 0)
+    atomicOr(&status[tile_doc[t]], (uint32_t)CW_STATUS_KEY_RANGE);
+}
+
 // ============================================================================
 // Maps (c.map/weave 1-arity, map.cljc:26-45): every (collection, key) pair is
 // an independent list weave rooted at a virtual [[0 "0" 0] nil nil].  The map
@@ -3623,6 +3637,12 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       HIPCHK(c, hipMemcpyAsync(out->yarn_perm, yv, (size_t)N * 4, hipMemcpyDeviceToDevice,
                                c->stream));
     }
+    // ids of 64 significant bits: the documents with an id >= 2^63 (KEY_RANGE)
+    if (key_bits >= 64) {
+      hipLaunchKernelGGL(k_key_range, GT, B256, 0, c->stream, id_key, tile_start, tile_doc,
+                         out->status);
+      if (check_launch(c, "key_range")) return -1;
+    }
   }
   // empty documents (no root) are flagged by the host wrapper
   return 0;
@@ -3634,60 +3654,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
 
 namespace {
 
-int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace) {
-  if (!bt || !res) return fail(c, "null batch/result");
+// The list weave of a batch already in device memory (dres: device arrays):
+// the fast path, then the exact path for its flagged documents.
+int weave_lists_dev_all(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id,
+                        const uint64_t *cause, const uint8_t *kind, cw_list_result *dres_p) {
+  cw_list_result &dres = *dres_p;
   const uint64_t D = bt->n_docs;
-  if (!bt->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
-  const uint64_t N64 = bt->doc_offsets[D];
-  if (bt->doc_offsets[0] != 0) return fail(c, "doc_offsets[0] must be 0");
-  if (N64 >= 0xFFFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^32-1)",
-                                        (unsigned long long)N64);
-  // a one-document batch takes the giant path (wide links) up to 2^31 - 2
-  // nodes; in a batch of several documents each stays below 2^29 - 1
-  for (uint64_t d = 0; d < D; d++) {
-    if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
-    const uint64_t nd = bt->doc_offsets[d + 1] - bt->doc_offsets[d];
-    if (D == 1 ? nd >= SUCCW_END : nd >= LINK_IDX)
-      return fail(c, "document %llu too large (limit %s nodes)", (unsigned long long)d,
-                  D == 1 ? "2^31-2" : "2^29-2 in a batch of several documents");
-  }
-  if (!res->weave_perm || !res->visible_count || !res->status)
-    return fail(c, "weave_perm, visible_count and status are required");
-  const uint32_t N = (uint32_t)N64;
-  HIPCHK(c, hipSetDevice(c->device));
-
-  // host tables (cached while the document layout repeats)
-  if (ensure_tables(c, D, bt->doc_offsets)) return -1;
-
-  const uint64_t *id = bt->id_key, *cause = bt->cause_key;
-  const uint8_t *kind = bt->kind;
-  cw_list_result dres = *res;
-  if (memspace == CW_MEM_HOST) {
-    if (N && (!id || !cause || !kind)) return fail(c, "null input arrays");
-    uint64_t *did = scratch_t<uint64_t>(c, "h_id", N), *dca = scratch_t<uint64_t>(c, "h_cause", N);
-    uint8_t *dk = scratch_t<uint8_t>(c, "h_kind", N);
-    dres.weave_perm = scratch_t<uint32_t>(c, "h_perm", N);
-    dres.visible_bits = res->visible_bits ? scratch_t<uint32_t>(c, "h_bits", ((size_t)N + 31) / 32) : nullptr;
-    dres.visible_count = scratch_t<uint32_t>(c, "h_vcount", D);
-    dres.max_ts = res->max_ts ? scratch_t<uint64_t>(c, "h_maxts", D) : nullptr;
-    dres.status = scratch_t<uint32_t>(c, "h_status", D);
-    dres.yarn_perm = res->yarn_perm ? scratch_t<uint32_t>(c, "h_yarn", N) : nullptr;
-    if (!did || !dca || !dk || !dres.weave_perm || !dres.visible_count || !dres.status ||
-        (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
-        (res->yarn_perm && !dres.yarn_perm))
-      return fail(c, "out of device memory (host-mode staging)");
-    // Pageable host memory: blocking copies (hipMemcpyAsync from/to pageable
-    // memory is not reliably ordered by a later stream synchronize).
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (N) {
-      HIPCHK(c, hipMemcpy(did, id, (size_t)N * 8, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMemcpy(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
-    }
-    id = did;
-    cause = dca;
-    kind = dk;
-  }
+  const uint32_t N = (uint32_t)bt->doc_offsets[D];
   // A few large documents would leave the per-document tree with a handful of
   // workgroups on a 256-CU GPU: weave them one by one on the all-parallel
   // giant-document path instead (render bits merged at each document's offset).
@@ -3749,6 +3722,65 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   }
   // documents outside the fast path's domain: the literal fold (exact.hip)
   if (exact_fixup(c, bt, id, cause, kind, &dres, x_hint)) return -1;
+  return 0;
+
+}
+
+int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace) {
+  if (!bt || !res) return fail(c, "null batch/result");
+  const uint64_t D = bt->n_docs;
+  if (!bt->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
+  const uint64_t N64 = bt->doc_offsets[D];
+  if (bt->doc_offsets[0] != 0) return fail(c, "doc_offsets[0] must be 0");
+  if (N64 >= 0xFFFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^32-1)",
+                                        (unsigned long long)N64);
+  // a one-document batch takes the giant path (wide links) up to 2^31 - 2
+  // nodes; in a batch of several documents each stays below 2^29 - 1
+  for (uint64_t d = 0; d < D; d++) {
+    if (bt->doc_offsets[d + 1] < bt->doc_offsets[d]) return fail(c, "doc_offsets not monotone");
+    const uint64_t nd = bt->doc_offsets[d + 1] - bt->doc_offsets[d];
+    if (D == 1 ? nd >= SUCCW_END : nd >= LINK_IDX)
+      return fail(c, "document %llu too large (limit %s nodes)", (unsigned long long)d,
+                  D == 1 ? "2^31-2" : "2^29-2 in a batch of several documents");
+  }
+  if (!res->weave_perm || !res->visible_count || !res->status)
+    return fail(c, "weave_perm, visible_count and status are required");
+  const uint32_t N = (uint32_t)N64;
+  HIPCHK(c, hipSetDevice(c->device));
+
+  // host tables (cached while the document layout repeats)
+  if (ensure_tables(c, D, bt->doc_offsets)) return -1;
+
+  const uint64_t *id = bt->id_key, *cause = bt->cause_key;
+  const uint8_t *kind = bt->kind;
+  cw_list_result dres = *res;
+  if (memspace == CW_MEM_HOST) {
+    if (N && (!id || !cause || !kind)) return fail(c, "null input arrays");
+    uint64_t *did = scratch_t<uint64_t>(c, "h_id", N), *dca = scratch_t<uint64_t>(c, "h_cause", N);
+    uint8_t *dk = scratch_t<uint8_t>(c, "h_kind", N);
+    dres.weave_perm = scratch_t<uint32_t>(c, "h_perm", N);
+    dres.visible_bits = res->visible_bits ? scratch_t<uint32_t>(c, "h_bits", ((size_t)N + 31) / 32) : nullptr;
+    dres.visible_count = scratch_t<uint32_t>(c, "h_vcount", D);
+    dres.max_ts = res->max_ts ? scratch_t<uint64_t>(c, "h_maxts", D) : nullptr;
+    dres.status = scratch_t<uint32_t>(c, "h_status", D);
+    dres.yarn_perm = res->yarn_perm ? scratch_t<uint32_t>(c, "h_yarn", N) : nullptr;
+    if (!did || !dca || !dk || !dres.weave_perm || !dres.visible_count || !dres.status ||
+        (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
+        (res->yarn_perm && !dres.yarn_perm))
+      return fail(c, "out of device memory (host-mode staging)");
+    // Pageable host memory: blocking copies (hipMemcpyAsync from/to pageable
+    // memory is not reliably ordered by a later stream synchronize).
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (N) {
+      HIPCHK(c, hipMemcpy(did, id, (size_t)N * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
+    }
+    id = did;
+    cause = dca;
+    kind = dk;
+  }
+  if (weave_lists_dev_all(c, bt, id, cause, kind, &dres)) return -1;
 
   if (memspace == CW_MEM_HOST) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4512,6 +4544,8 @@ int weft_lists_impl(cw_ctx *c, const cw_weft_batch *bt, cw_weft_result *res, int
 
 }  // namespace
 
+#include "k128.hip"
+
 // ============================================================================
 // C ABI
 // ============================================================================
@@ -4621,6 +4655,12 @@ int cw_weave_lists(cw_ctx *c, const cw_list_batch *b, cw_list_result *r, int mem
   c->err.clear();
   if (memspace != CW_MEM_HOST && memspace != CW_MEM_DEVICE) return fail(c, "bad memspace");
   return weave_lists_impl(c, b, r, memspace);
+}
+
+int cw_weave_lists_k128(cw_ctx *c, const cw_list_batch_k128 *b, cw_list_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  return weave_lists_k128_impl(c, b, r, memspace);
 }
 
 int cw_weave_maps(cw_ctx *c, const cw_map_batch *b, cw_map_result *r, int memspace) {

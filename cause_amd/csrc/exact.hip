@@ -29,6 +29,8 @@ constexpr uint32_t X_NIL = 0xFFFFFFFEu;  // cause is nil (the root's, shared.clj
 constexpr uint32_t X_END = 0xFFFFFFFFu;  // no cause in the document / end of the list
 constexpr uint32_t X_HEAD = 0xFFFFFFFDu; // the split before the first node
 constexpr uint32_t X_MASK = CW_STATUS_ROOT | CW_STATUS_ORPHAN | CW_STATUS_NON_LAMPORT;
+// not a ::nodes map of the reference (a repeated id) or not a K64 key
+constexpr uint32_t X_SKIP = CW_STATUS_DUP | CW_STATUS_KEY_RANGE;
 
 // Documents the exact path takes: non-empty, flagged by the domain checks, no
 // repeated id.
@@ -39,7 +41,7 @@ __global__ __launch_bounds__(256) void k_xcount(const uint32_t *__restrict__ sta
   bool take = false;
   if (d < D) {
     const uint32_t s = status[d];
-    take = (s & X_MASK) && !(s & CW_STATUS_DUP) && doc_off[d + 1] > doc_off[d];
+    take = (s & X_MASK) && !(s & X_SKIP) && doc_off[d + 1] > doc_off[d];
   }
   const uint64_t b = __ballot(take);
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (uint32_t)__popcll(b));
@@ -268,7 +270,7 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
   std::vector<uint64_t> xoff(1, 0), src;
   std::vector<uint32_t> odoc;
   for (uint64_t d = 0; d < D; d++) {
-    if (!(st[d] & X_MASK) || (st[d] & CW_STATUS_DUP) || off[d + 1] == off[d]) continue;
+    if (!(st[d] & X_MASK) || (st[d] & X_SKIP) || off[d + 1] == off[d]) continue;
     src.push_back(off[d]);
     odoc.push_back((uint32_t)d);
     xoff.push_back(xoff.back() + (off[d + 1] - off[d]));

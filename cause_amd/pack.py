@@ -83,7 +83,8 @@ class KeyLayout:
 
 
 class KeyRangeError(ValueError):
-    """Ids do not fit a 64-bit key (CW_STATUS_KEY_RANGE)."""
+    """Ids do not fit a K64 key (< 2^63; CW_STATUS_KEY_RANGE): use the K128
+    layout (pack_lists_k128 / cw_weave_lists_k128), or they fit neither."""
 
 
 def _bits(v: int) -> int:
@@ -243,3 +244,61 @@ def pack_maps(docs) -> PackedMaps:
         off[d + 1] = j
     token_bits = max(1, _bits(max(len(tok) - 1, 0)))
     return PackedMaps(off, idk, ck, ci, kd, lay, token_bits, list(tok), docs, ranks)
+
+
+# ---------------------------------------------------------------- K128 ids ----
+# K128 = ts:64 | site_rank:32 | tx:32, as two u64 words per id
+# (include/causeweave.h, cw_list_batch_k128): hi = ts, lo = site_rank << 32 | tx.
+# (hi, lo) compared as one unsigned 128-bit number is (compare a b), util.cljc:4-10.
+NIL2 = (NIL, NIL)               # a nil cause
+NON_ID_CAUSE2 = (NIL, NIL - 1)  # a cause that is not an id (never matches one)
+
+
+def pack_k128(ts: int, site_rank: int, tx: int):
+    if not (0 <= ts < 1 << 64 and 0 <= site_rank < 1 << 32 and 0 <= tx < 1 << 32):
+        raise KeyRangeError(f"id ({ts}, site rank {site_rank}, {tx}) does not fit K128")
+    return ts, (site_rank << 32) | tx
+
+
+@dataclass
+class PackedBatchK128:
+    offsets: np.ndarray    # uint64 [D+1]
+    id_key: np.ndarray     # uint64 [N, 2] (hi, lo)
+    cause_key: np.ndarray  # uint64 [N, 2]
+    kind: np.ndarray       # uint8  [N]
+    docs: list             # PackedDoc per document (id_key / cause_key [n, 2])
+
+
+def pack_lists_k128(docs) -> PackedBatchK128:
+    """Pack a batch of list documents (nodes incl. root, any order) as K128 ids;
+    site-ids ranked per document in String.compareTo order like pack_lists."""
+    docs = [list(d) for d in docs]
+    packed = []
+    for nodes in docs:
+        ids = [n[0] for n in nodes] + [n[1] for n in nodes if len(n) > 1 and is_id(n[1])]
+        rank = intern_sites(ids)
+        n = len(nodes)
+        idk = np.empty((n, 2), np.uint64)
+        ck = np.empty((n, 2), np.uint64)
+        kd = np.empty(n, np.uint8)
+        for i, nd in enumerate(nodes):
+            nid = nd[0]
+            cause, value = (nd[1], nd[-1]) if len(nd) > 1 else (None, nid)
+            idk[i] = pack_k128(nid[0], rank[nid[1]], nid[2])
+            if cause is None:
+                ck[i] = NIL2
+            elif is_id(cause):
+                ck[i] = pack_k128(cause[0], rank[cause[1]], cause[2])
+            else:
+                ck[i] = NON_ID_CAUSE2
+            k = kind_of(value)
+            if nid == ROOT_ID and cause is None and value is None:
+                k |= KIND_ROOT
+            kd[i] = k
+        packed.append(PackedDoc(idk, ck, kd, nodes, rank))
+    off = np.zeros(len(docs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(d) for d in docs], dtype=np.uint64)
+    cat = lambda f, shape, dt: (np.concatenate([getattr(p, f) for p in packed]) if packed
+                                else np.zeros(shape, dt))
+    return PackedBatchK128(off, cat("id_key", (0, 2), np.uint64), cat("cause_key", (0, 2), np.uint64),
+                           cat("kind", (0,), np.uint8), packed)

@@ -20,15 +20,19 @@
  *    device scratch inside the context.
  *  - Ids are order-preserving packed 64-bit keys (cause_amd/pack.py):
  *      key(a) < key(b)  <=>  (compare a b) < 0   (util.cljc:4-10)
- *    CW_NIL (all ones) is nil and is reserved (root's cause).
+ *    below 2^63 (K64); CW_NIL (all ones) is nil and is reserved (root's cause).
+ *    Ids that need more bits take the K128 layout (cw_weave_lists_k128).
  *  - A document's nodes may come in any order (the ::nodes hash map,
  *    shared.cljc:62).  The root [[0 "0" 0] nil nil] (shared.cljc:22-23) is one
  *    of them, flagged CW_KIND_ROOT.
  *  - Return value: 0 ok, < 0 error (cw_last_error has the text).  Per-document
- *    problems are reported in status[] instead (CW_STATUS_*).  A document with
- *    a non-zero status is outside the fast path's domain (it would throw in the
- *    reference's s/insert, shared.cljc:163-178); its outputs are well-formed
- *    but unspecified.
+ *    problems are reported in status[] instead (CW_STATUS_*).  ROOT, ORPHAN,
+ *    NON_LAMPORT and WEFT mark documents the reference's s/insert would refuse
+ *    (shared.cljc:163-178) but its full reweave accepts (list.cljc:26-28): the
+ *    library reweaves them by the literal fold (exact path) and their outputs
+ *    are the reference's.  DUP, MAP_KEY, KEY_RANGE and INTERNAL documents
+ *    cannot be a ::nodes map of the reference or a K64 key; their outputs are
+ *    well-formed but unspecified.
  *  - A context is not thread-safe; use one context per host thread.  Calls are
  *    re-entrant with respect to each other's inputs (pure functions; swap!
  *    retries may repeat them).
@@ -65,7 +69,10 @@ enum {
   CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits, or a node caused by
                                       the root id (its key weave mixes children and orphans) */
   CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
-  CW_STATUS_WEFT = 1u << 6         /* weft: a cut id is not a node of the document         */
+  CW_STATUS_WEFT = 1u << 6,        /* weft: a cut id is not a node of the document         */
+  CW_STATUS_KEY_RANGE = 1u << 7    /* an id key >= 2^63: it does not fit the K64 layout
+                                      (CW_NIL and its neighbours are reserved); weave the
+                                      document with cw_weave_lists_k128                     */
 };
 
 /* Where the arrays of a batch/result live. */
@@ -132,6 +139,27 @@ typedef struct {
  * cause_key / kind and every result array live (doc_offsets is always host). */
 int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
                    int memspace);
+
+/* K128: ids that need more than 63 bits (ts:64 | site_rank:32 |
+ * tx:32).  Every id is two u64 words, hi then lo:
+ *     hi = lamport-ts (a nat-int Long, shared.cljc:31)
+ *     lo = site_rank << 32 | tx-index   (site ranks in String.compareTo order)
+ * so (hi, lo) compared as an unsigned 128-bit number is (compare a b)
+ * (util.cljc:4-10).  A nil cause is (CW_NIL, CW_NIL).  Same documents, same
+ * results as cw_weave_lists (weave order, rendered bits and counts, status,
+ * the exact path for out-of-domain documents); max_ts is the largest id's hi
+ * word and yarn_perm groups by the site rank in lo's high half.  The limits on
+ * document and batch sizes are cw_weave_lists'. */
+typedef struct {
+  uint64_t n_docs;
+  const uint64_t *doc_offsets; /* HOST memory, [n_docs+1]                                */
+  const uint64_t *id_key;      /* [2N]: (hi, lo) of node i at [2i], [2i+1]                */
+  const uint64_t *cause_key;   /* [2N]: (hi, lo) of its cause; (CW_NIL, CW_NIL) = nil      */
+  const uint8_t *kind;         /* [N] CW_KIND_*                                           */
+} cw_list_batch_k128;
+
+int cw_weave_lists_k128(cw_ctx *ctx, const cw_list_batch_k128 *batch, cw_list_result *result,
+                        int memspace);
 
 /* ----------------------------------------------------------------- maps ---- */
 /* Full reweave of a batch of CausalMaps (c.map/weave 1-arity, map.cljc:26-45)

@@ -35,6 +35,18 @@ def test_struct_layout_matches_header():
     assert ctypes.sizeof(abi.CwListBatch) == 8 * 5 + 4 * 4
     assert ctypes.sizeof(abi.CwListResult) == 8 * 6
     assert ctypes.sizeof(abi.CwKernelStat) == 48 + 8 * 3
+    assert ctypes.sizeof(abi.CwListBatchK128) == 8 * 5
+
+
+def test_status_bits_match_header():
+    import re
+
+    src = open(abi.HEADER).read()
+    bits = {m.group(1): 1 << int(m.group(2))
+            for m in re.finditer(r"CW_STATUS_(\w+)\s*=\s*1u\s*<<\s*(\d+)", src)}
+    for name, v in bits.items():
+        assert getattr(abi, "STATUS_" + name) == v, name
+    assert "KEY_RANGE" in bits
 
 
 def test_no_gpu_means_a_loud_error():
