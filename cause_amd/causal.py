@@ -59,17 +59,25 @@ class CauseError(Exception):
         self.causes = causes
 
 
-_weaver = None
-_lock = threading.Lock()
+_local = threading.local()
 
 
 def weaver() -> abi.Weaver:
-    """The process-wide GPU context (device 0)."""
-    global _weaver
-    with _lock:
-        if _weaver is None:
-            _weaver = abi.Weaver(0)
-        return _weaver
+    """This thread's GPU context (device 0).  A cw_ctx is not thread-safe
+    (include/causeweave.h), and swap! may run a weave-fn on several threads at
+    once: each host thread gets its own context, so calls never share one."""
+    w = getattr(_local, "weaver", None)
+    if w is None:
+        w = _local.weaver = abi.Weaver(0)
+    return w
+
+
+def causal_to_edn(v):
+    """s/causal->edn (shared.cljc:320-328): a causal collection (a list or map
+    ct held as a value) materialises recursively, anything else is itself."""
+    if isinstance(v, dict) and v.get("type") in ("list", "map") and "weave" in v:
+        return causal_list_to_edn(v) if v["type"] == "list" else causal_map_to_edn(v)
+    return v
 
 
 def new_node(ts, site, *rest):
@@ -340,8 +348,9 @@ def causal_list_to_list(ct):
 
 
 def causal_list_to_edn(ct):
-    """list.cljc:57-66: (peek node) of every rendered node"""
-    return [n[-1] for n in causal_list_to_list(ct)]
+    """list.cljc:57-66: (peek node) of every rendered node, nested causal
+    values materialised (s/causal->edn, list.cljc:64-66)"""
+    return [causal_to_edn(n[-1]) for n in causal_list_to_list(ct)]
 
 
 def count(ct):
@@ -363,6 +372,8 @@ def new_map_ct(site_id=None, uuid=None, rng=random):
 
 
 def _unpack_id(key, layout, rank):
+    if key == 0:
+        return ROOT_ID  # the virtual root packs to 0 (pack.pack_maps)
     inv = {r: s for s, r in rank.items()}
     ts = key >> layout.ts_shift
     site = (key >> layout.site_shift) & ((1 << layout.site_bits) - 1)
@@ -446,8 +457,9 @@ def map_dissoc(ct, k):
 
 
 def causal_map_to_edn(ct):
-    """map.cljc:94-103 (nested collections are opaque values here)."""
-    return {n[1]: n[2] for n in ct["_active"].values() if n is not BLANK}
+    """map.cljc:94-103: the active value of every key, nested causal values
+    materialised (s/causal->edn, map.cljc:101)."""
+    return {n[1]: causal_to_edn(n[2]) for n in ct["_active"].values() if n is not BLANK}
 
 
 def causal_map_to_list(ct):

@@ -213,8 +213,11 @@ class PackedMaps:
 def pack_maps(docs) -> PackedMaps:
     """Pack a batch of map collections (each an iterable of ``(id, cause, value)``
     nodes; maps have no root node of their own).  Keys get batch-wide tokens in
-    first-appearance order; the virtual root [[0 "0" 0] nil nil] packs to 0, so
-    "0" must be the smallest site-id (true of every u/new-uid, util.cljc:12-23)."""
+    first-appearance order.  The virtual root [[0 "0" 0] nil nil] packs to 0 and
+    so does a cause naming it; every other id packs by its site's rank in
+    String.compareTo order, which may put site-ids such as " a " before "0"
+    (list_test.cljc:85-96): an id with ts >= 1 still packs above 0, and only an
+    id that itself sorts before the root id (ts 0) is refused."""
     docs = [list(d) for d in docs]
     lay = layout_for([[(n[0], n[1] if valid_id(n[1]) else None, n[2]) for n in d]
                       + [((0, "0", 0), None, None)] for d in docs])
@@ -228,13 +231,14 @@ def pack_maps(docs) -> PackedMaps:
     for d, nodes in enumerate(docs):
         ids = [n[0] for n in nodes] + [n[1] for n in nodes if valid_id(n[1])] + [ROOT_ID]
         rank = intern_sites(ids)
-        if rank["0"] != 0:
-            raise KeyRangeError('a site-id sorts before "0": the virtual root must pack to 0')
         ranks.append(rank)
+        pk = lambda i: 0 if i == ROOT_ID else lay.pack(i[0], rank[i[1]], i[2])
         for nid, cause, value in nodes:
-            idk[j] = lay.pack(nid[0], rank[nid[1]], nid[2])
+            if nid[0] == 0 and java_str_key(nid[1]) < java_str_key("0"):
+                raise KeyRangeError(f"map node id {nid} sorts before the root id")
+            idk[j] = pk(nid)
             if valid_id(cause):
-                ck[j] = lay.pack(cause[0], rank[cause[1]], cause[2])
+                ck[j] = pk(cause)
                 ci[j] = 1
             else:
                 ck[j] = tok.setdefault(cause, len(tok))

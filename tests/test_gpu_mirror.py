@@ -128,13 +128,30 @@ def _cmap(*kvs):
 
 
 def test_map_basic():
-    """map_test.cljc:5-15 (a nested list value stays opaque here)."""
+    """map_test.cljc:5-15, the nested causal list included: (assoc :list
+    (swap! (atom (c/list)) conj "a" "b" "c")) materialises as ("a" "b" "c")."""
     ct = _cmap(MKW("foo"), "bar")
     ct = C.map_assoc(ct, MKW("fizz"), "buzz")
     ct = C.map_assoc(ct, MKW("fizz"), "bang")
     ct = C.map_dissoc(ct, MKW("foo"))
-    ct = C.map_assoc(ct, MKW("list"), "abc")
-    assert C.causal_map_to_edn(ct) == {MKW("fizz"): "bang", MKW("list"): "abc"}
+    lst = C.new_list_ct(rng=random.Random(6))
+    for v in ("a", "b", "c"):
+        lst = C.list_conj(lst, v)
+    ct = C.map_assoc(ct, MKW("list"), lst)
+    assert C.causal_map_to_edn(ct) == {MKW("fizz"): "bang", MKW("list"): ["a", "b", "c"]}
+
+
+def test_nested_causal_values_in_lists_and_maps():
+    """s/causal->edn recursion (shared.cljc:320-328) through lists and maps:
+    a list holding a map holding a list."""
+    inner = C.new_list_ct(rng=random.Random(7))
+    for v in ("x", "y"):
+        inner = C.list_conj(inner, v)
+    m = _cmap(MKW("k"), inner, MKW("n"), 1)
+    outer = C.new_list_ct(rng=random.Random(8))
+    outer = C.list_conj(outer, "head")
+    outer = C.list_conj(outer, m)
+    assert C.causal_list_to_edn(outer) == ["head", {MKW("k"): ["x", "y"], MKW("n"): 1}]
 
 
 def test_map_hide_and_show():
@@ -218,3 +235,48 @@ def test_map_batch_matches_python_restatement():
         assert have == want
         assert {k: str(v) for k, v in C.causal_map_to_edn(g).items()} == \
             {k: str(v) for k, v in R.causal_map_to_edn(p).items()}
+
+
+def test_map_exotic_site_ids_sort_before_zero():
+    """Map nodes from site-ids that sort before "0" in String.compareTo order
+    (" a ", " f ", " z ", as list_test.cljc:85-96 uses): the GPU map weave
+    equals the literal restatement (map.cljc:21-59) key by key."""
+    sites = [" a ", " f ", " z ", "A~aaaaaaaaaaa", "zzzzzzzzzzzzz"]
+    keys = [MKW("a"), MKW("b"), "s"]
+    for seed in range(6):
+        rng = random.Random(100 + seed)
+        nodes = {}
+        for ts in range(1, 80):
+            site = rng.choice(sites)
+            r = rng.random()
+            if r < 0.55 or not nodes:
+                body = (rng.choice(keys), rng.choice(["x", "y", 1, 2]))
+            elif r < 0.7:
+                body = (rng.choice(keys), R.HIDE)
+            else:  # undo / redo of an earlier node: an id cause (F8c keys too)
+                body = (rng.choice(list(nodes)), rng.choice([R.H_HIDE, R.H_SHOW, R.HIDE]))
+            nodes[(ts, site, rng.randrange(3))] = body
+        ct, ref = C.new_map_ct(), R.new_map_ct()
+        ct["nodes"], ref["nodes"] = dict(nodes), dict(nodes)
+        got, want = C.map_weave(ct), R.map_weave(ref)
+        assert got["weave"] == want["weave"], seed
+        assert C.causal_map_to_edn(got) == R.causal_map_to_edn(want), seed
+
+
+def test_mirror_threads_use_their_own_contexts():
+    """Concurrent weaves from several host threads (swap! retries, SURVEY
+    §8(b) threading): each thread gets its own context, results match."""
+    import concurrent.futures as cf
+
+    rng = random.Random(11)
+    cts = []
+    for _ in range(24):
+        nodes, _ = G.random_history(rng, 40)
+        ct = C.new_list_ct()
+        ct["nodes"] = {nd[0]: (nd[1], nd[2]) for nd in [R.ROOT_NODE] + nodes}
+        cts.append(ct)
+    want = [C.causal_list_to_edn(C.list_weave(ct)) for ct in cts]
+    with cf.ThreadPoolExecutor(6) as ex:
+        for _ in range(3):
+            got = list(ex.map(lambda ct: C.causal_list_to_edn(C.list_weave(ct)), cts))
+            assert got == want

@@ -50,3 +50,18 @@ def test_k128_limits_and_non_id_causes():
     assert tuple(b.cause_key[1]) == pack.NON_ID_CAUSE2
     assert list(b.offsets) == [0, 2, 2]
     assert b.id_key.dtype == np.uint64
+
+
+def test_map_packing_takes_sites_before_zero():
+    """Site-ids that sort before "0" (list_test.cljc:85-96) pack in maps: the
+    virtual root and causes naming it pack to 0, every other id above it."""
+    nodes = [((1, " a ", 0), "k", "x"), ((2, " f ", 0), (1, " a ", 0), R.HIDE),
+             ((3, "0", 1), R.ROOT_ID, "y")]
+    pm = pack.pack_maps([nodes])
+    assert pm.ranks[0][" a "] == 0 and pm.ranks[0]["0"] > 0
+    assert (pm.id_key > 0).all()
+    assert pm.cause[2] == 0 and pm.cause_is_id[2] == 1
+    order = np.argsort(pm.id_key)
+    assert [nodes[j][0] for j in order] == sorted((n[0] for n in nodes), key=R.id_key)
+    with pytest.raises(pack.KeyRangeError):
+        pack.pack_maps([[((0, " a ", 0), "k", "x")]])
