@@ -14,7 +14,8 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcauseweave.so")
+# (CW_LIB: another build of the same library, for A/B timing runs on one box)
+LIB_PATH = os.environ.get("CW_LIB") or os.path.join(_HERE, "libcauseweave.so")
 HEADER = os.path.join(os.path.dirname(_HERE), "include", "causeweave.h")
 
 CW_MEM_HOST, CW_MEM_DEVICE = 0, 1
