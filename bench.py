@@ -497,7 +497,10 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                            "d2h_ms_per_batch": float(np.mean(st.d2h_ms)),
                            "host_fill_s_per_batch": st.fill_s / nb,
                            "note": "host generation (16 threads), H2D, weave and D2H "
-                                   "overlapped over the slots; rank-0 figures"},
+                                   "pipelined over the slots; measured with per-kernel "
+                                   "profiling on, which synchronises after every weave, so "
+                                   "the next batch's H2D does not overlap a weave here (a "
+                                   "conservative end-to-end figure); rank-0 figures"},
             "visible_nodes": vis_total[0],
         }
         if cpu:

@@ -2167,6 +2167,24 @@ __global__ void k_max_ts1(const uint64_t *__restrict__ skey, uint32_t n, uint32_
   if (threadIdx.x == 0) max_ts[0] = n ? skey[n - 1] >> ts_shift : 0ull;
 }
 
+// OR of two key arrays at once (map ids and causes: one readback)
+__global__ void k_or_reduce2(const uint64_t *__restrict__ a, const uint64_t *__restrict__ b,
+                             uint32_t N, unsigned long long *__restrict__ out) {
+  uint64_t x = 0, y = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x) {
+    x |= a[i];
+    y |= b[i];
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    x |= __shfl_xor(x, o, 64);
+    y |= __shfl_xor(y, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (x) atomicOr(&out[0], (unsigned long long)x);
+    if (y) atomicOr(&out[1], (unsigned long long)y);
+  }
+}
+
 __global__ void k_or_reduce(const uint64_t *__restrict__ keys, uint32_t N,
                             unsigned long long *__restrict__ out) {
   uint64_t acc = 0;
@@ -2822,6 +2840,15 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
+  uint32_t map_fused = 1;          // CW_MAP_FUSED: one-kernel map weave of small collections
+  struct MapPacks {                // k_map_pack's pack table, cached by collection layout
+    std::vector<uint64_t> off;
+    std::vector<uint32_t> doc0;
+    uint32_t dbits = 0, pk = 0;
+    bool ok = false;
+  } mpack;
+  uint32_t map_pack = 0;           // CW_MAP_PACK: 0 = 2048 nodes / 512 threads, 1 = 1024 / 256,
+                                   // 2 = 2048 / 1024
 };
 
 namespace {
@@ -3651,6 +3678,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
 }  // namespace
 
 #include "exact.hip"
+#include "mappack.hip"
 
 namespace {
 
@@ -4103,14 +4131,47 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   if (!bt->id_key || !bt->cause || !bt->cause_is_id || !bt->kind)
     return fail(c, "null input arrays");
 
-  // collection tables: id sort, key resolution and key grouping run per collection
-  if (ensure_tables(c, D, bt->coll_offsets)) return -1;
-  auto &t = c->tab;
-  const uint32_t T = t.T;
   const uint64_t *id = dev ? bt->id_key : scratch_t<uint64_t>(c, "m_id", N);
   const uint64_t *cause = dev ? bt->cause : scratch_t<uint64_t>(c, "m_cause", N);
   const uint8_t *cis = dev ? bt->cause_is_id : scratch_t<uint8_t>(c, "m_cis", N);
   const uint8_t *kind = dev ? bt->kind : scratch_t<uint8_t>(c, "m_kind", N);
+  if (!id || !cause || !cis || !kind) return fail(c, "out of device memory (maps, N=%u)", N);
+  if (!dev) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy((void *)id, bt->id_key, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)cause, bt->cause, (size_t)N * 8, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)cis, bt->cause_is_id, N, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy((void *)kind, bt->kind, N, hipMemcpyHostToDevice));
+  }
+  if (c->map_fused) {  // small collections: one kernel (mappack.hip)
+    const int rc = weave_maps_packed(c, bt, res, dev, id, cause, cis, kind);
+    if (rc <= 0) return rc;
+  }
+  // significant bits of the ids and of the causes (id keys, SURVEY F8c, are
+  // cause ids, which may lie outside the collection): one reduction, one readback
+  uint32_t key_bits = bt->key_bits, cause_bits = 0;
+  {
+    unsigned long long *red = scratch_t<unsigned long long>(c, "red2", 2);
+    if (!red) return fail(c, "out of device memory (red)");
+    HIPCHK(c, hipMemsetAsync(red, 0, 16, c->stream));
+    hipLaunchKernelGGL(k_or_reduce2, dim3(1024), dim3(256), 0, c->stream, id, cause, N, red);
+    if (check_launch(c, "or_reduce2")) return -1;
+    if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, red, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t *v = reinterpret_cast<const uint64_t *>(c->pin_small);
+    const uint32_t ib = v[0] ? 64 - __builtin_clzll(v[0]) : 1, cb = v[1] ? 64 - __builtin_clzll(v[1]) : 1;
+    if (key_bits == 0) key_bits = ib;
+    cause_bits = cb;
+  }
+  if (key_bits > 62 || cause_bits > 62)
+    return fail(c, "map ids need %u bits (limit 62)", std::max(key_bits, cause_bits));
+
+  // the general path: collection tables (id sort, key resolution and key
+  // grouping run per collection), then every key weave through a list weave
+  if (ensure_tables(c, D, bt->coll_offsets)) return -1;
+  auto &t = c->tab;
+  const uint32_t T = t.T;
   uint32_t *status = scratch_t<uint32_t>(c, "m_status", D);
   uint64_t *skA = scratch_t<uint64_t>(c, "skA", N), *skB = scratch_t<uint64_t>(c, "skB", N);
   uint32_t *svA = scratch_t<uint32_t>(c, "svA", N), *svB = scratch_t<uint32_t>(c, "svB", N);
@@ -4121,26 +4182,11 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   uint32_t *vA = scratch_t<uint32_t>(c, "m_vA", N), *vB = scratch_t<uint32_t>(c, "m_vB", N);
   uint32_t *tcnt = scratch_t<uint32_t>(c, "m_tcnt", T), *tsb = scratch_t<uint32_t>(c, "m_tsb", T);
   uint32_t *seg_of = scratch_t<uint32_t>(c, "m_segof", N);
-  if (!id || !cause || !cis || !kind || !status || !skA || !skB || !svA || !svB || !segk ||
+  if (!status || !skA || !skB || !svA || !svB || !segk ||
       !mpar || !mkind || !kA || !kB || !vA || !vB || !tcnt || !tsb || !seg_of)
     return fail(c, "out of device memory (maps, N=%u)", N);
   if (!grid_ok(T, SORT_THREADS) || !grid_ok(D, 1024)) return fail(c, "batch too large for one dispatch");
-
-  if (!dev) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy((void *)id, bt->id_key, (size_t)N * 8, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy((void *)cause, bt->cause, (size_t)N * 8, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy((void *)cis, bt->cause_is_id, N, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy((void *)kind, bt->kind, N, hipMemcpyHostToDevice));
-  }
   HIPCHK(c, hipMemsetAsync(status, 0, D * 4, c->stream));
-  uint32_t key_bits = bt->key_bits;
-  if (key_bits == 0 && find_key_bits(c, id, N, &key_bits)) return -1;
-  // id keys are cause ids, which may lie outside the collection
-  uint32_t cause_bits = 0;
-  if (find_key_bits(c, cause, N, &cause_bits)) return -1;
-  if (key_bits > 62 || cause_bits > 62)
-    return fail(c, "map ids need %u bits (limit 62)", std::max(key_bits, cause_bits));
   const uint32_t W = std::max(std::max(bt->token_bits, key_bits), cause_bits);
 
   // 1. (sort (::s/nodes ct)) per collection -- map.cljc:28
@@ -4585,6 +4631,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->tree_pad = knob("CW_TREE_PAD", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
+  c->map_fused = knob("CW_MAP_FUSED", 1);
+  c->map_pack = knob("CW_MAP_PACK", 0);
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 16);
   c->tour = knob("CW_TOUR", 1);

@@ -1,0 +1,543 @@
+// mappack.hip -- the map weave of small collections in ONE kernel (config 4).
+// Included by causeweave.hip after the sort helpers (rank_subdigit, wb_elem,
+// block_exscan) it uses.
+//
+// c.map/weave 1-arity (map.cljc:21-45) + active-node (:47-59) for a batch of
+// CausalMaps whose collections have <= MPK nodes each.  One workgroup takes a
+// pack of whole consecutive collections (<= MPK nodes) and does, in LDS:
+//   1. (sort ::nodes) per collection: a stable LDS radix sort by (collection, id);
+//      repeated ids -> CW_STATUS_DUP;
+//   2. each node's key and cause-in-weave (map.cljc:31-37): a cause id is
+//      looked up among the collection's sorted ids; the key is the cause node's
+//      cause when that is a key token, the cause node's cause id otherwise
+//      (an id key), nil when the cause node is absent; a key cause
+//      weaves under the key's virtual root [[0 "0" 0] nil nil];
+//   3. a stable sort by (collection, key): every key weave is a run, id order kept;
+//   4. per key weave, the list weave of the root + its nodes (SURVEY F4/F5:
+//      effective parents, subtree sizes, siblings specials first by descending
+//      id, preorder positions) -- as k_small_weave does, for key weaves of any
+//      length up to the pack;
+//   5. active-node per key weave (first rendered value, ::blank behind a hide).
+// Key weaves are numbered across the batch with a decoupled look-back over the
+// packs (a pack publishes its count, then sums its predecessors'), so every
+// output goes straight to its final place: one pass over the inputs, one over
+// the outputs, instead of the eleven kernels and three host readbacks of the
+// general map path (kept for collections of more than MPK nodes).
+//
+// In the key weave a node caused by an id whose node is itself id-caused (an id
+// key) or absent (the nil key) is never next to its cause, so weave-node
+// appends it (shared.cljc:236-238): it chains after the previous node of the
+// key weave, as k_seg_build does.
+
+constexpr uint32_t MPK = 2048;                 // largest pack (nodes); CW_MAP_PACK picks the geometry
+constexpr uint16_t MP_ROOT = 0xFFFFu;          // cause-in-weave = the key weave's root
+constexpr uint16_t MP_CHAIN = 0xFFFEu;         // appended after the previous node
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
+
+// Stable LDS radix sort of the pack's wave-blocked items by the low `bits` of
+// ck (carrying val), 6 bits per sub-pass.  On return item u holds the element
+// of sorted position wb_elem(u), and ks[] the sorted keys.
+template <int NT, int IT>
+__device__ __forceinline__ void mp_sort(uint64_t (&ck)[IT], uint32_t (&val)[IT], uint32_t len,
+                                        uint32_t bits, uint64_t *ks, uint16_t *vs,
+                                        uint32_t (*wcnt)[SUB_BINS], uint32_t *run) {
+  uint32_t sd[IT], pos[IT];
+  for (uint32_t sh = 0; sh < bits; sh += SUB_BITS) {
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) sd[u] = (uint32_t)(ck[u] >> sh) & (SUB_BINS - 1);
+    rank_subdigit<NT, IT>(sd, len, min(SUB_BITS, bits - sh), pos, wcnt, run);
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++)
+      if (wb_elem<IT>(u) < len) {
+        ks[pos[u]] = ck[u];
+        vs[pos[u]] = (uint16_t)val[u];
+      }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t j = wb_elem<IT>(u);
+      if (j < len) {
+        ck[u] = ks[j];
+        val[u] = vs[j];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int PK, int NT>
+__global__ __launch_bounds__(NT) void k_map_pack(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause,
+    const uint8_t *__restrict__ cause_is_id, const uint8_t *__restrict__ kind,
+    const uint64_t *__restrict__ coll_off, const uint32_t *__restrict__ pack_doc0, uint32_t P,
+    uint32_t token_bits, unsigned long long *lb, uint64_t cap_segs, uint64_t n_total,
+    uint64_t *__restrict__ seg_offsets, uint32_t *__restrict__ seg_coll,
+    uint64_t *__restrict__ seg_key, int64_t *__restrict__ seg_active,
+    uint32_t *__restrict__ seg_perm, uint32_t *__restrict__ status, uint32_t *ctl,
+    unsigned long long *__restrict__ tprof) {
+  constexpr uint32_t IT = PK / NT;
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
+    if (tprof) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tacc[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  stamp(-1);
+  // LDS by phase: A = sorted (collection, id) keys, then sorted (collection,
+  // key) keys, then the key weaves' numbering (SEG, SS), siblings-before and
+  // weave order (BEF, WV); B = causes by input index, then each member's parent,
+  // effective parent and subtree size (PAR, EFF, SZ).  By position: I2J (id
+  // order -> input), P16 (id order: cause position or MP_*), Q (id order -> key
+  // order), LQ / KQ (key order: collection-local input index, kind).
+  __shared__ uint64_t A[PK], B[PK];
+  __shared__ uint16_t VS[PK], I2J[PK], P16[PK], Q[PK], LQ[PK];
+  __shared__ uint8_t K8[PK], KQ[PK];
+  __shared__ uint32_t dstart[PK + 1], dstat[PK];
+  __shared__ uint32_t wcnt[NT / 64][SUB_BINS], run[64], wtot[NT / 64];
+  __shared__ uint32_t s_base;
+  __shared__ unsigned long long s_or[2];
+  uint16_t *SEG = reinterpret_cast<uint16_t *>(A), *SS = SEG + PK, *BEF = SS + PK, *WV = BEF + PK;
+  uint16_t *PAR = reinterpret_cast<uint16_t *>(B), *EFF = PAR + PK;
+  uint32_t *SZ = reinterpret_cast<uint32_t *>(EFF + PK);
+
+  const uint32_t pk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t d0 = pack_doc0[pk], nd = pack_doc0[pk + 1] - d0;
+  const uint64_t s0 = coll_off[d0];
+  const uint32_t len = (uint32_t)(coll_off[d0 + nd] - s0);
+  for (uint32_t i = tid; i <= nd; i += NT) dstart[i] = (uint32_t)(coll_off[d0 + i] - s0);
+  for (uint32_t i = tid; i < nd; i += NT) dstat[i] = 0;
+  if (tid < 2) s_or[tid] = 0;
+  __syncthreads();
+  const uint64_t tmask = (1ull << token_bits) - 1;
+
+  // 1. load; stable sort by (collection, id) -- (sort ::nodes), map.cljc:28
+  // (the pack's own key widths: ids, id causes, collections in the pack)
+  uint64_t ck[IT];
+  uint32_t val[IT], dl0[IT];
+  unsigned long long oid = 0, oca = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t j = wb_elem<IT>(u);
+    ck[u] = 0;
+    val[u] = 0;
+    dl0[u] = 0;
+    if (j < len) {
+      uint32_t lo = 0, hi = nd;  // the collection of element j
+      while (hi - lo > 1) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (dstart[m] <= j) lo = m; else hi = m;
+      }
+      const uint64_t c = cause[s0 + j];
+      const bool cid = cause_is_id[s0 + j] != 0;
+      B[j] = c;
+      K8[j] = (uint8_t)((cid ? 0x80u : 0u) | (kind[s0 + j] & KIND_CLASS));
+      ck[u] = id_key[s0 + j];
+      oid |= ck[u];
+      oca |= cid ? c : 0ull;
+      val[u] = j;
+      dl0[u] = lo;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    oid |= __shfl_xor(oid, o, 64);
+    oca |= __shfl_xor(oca, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    if (oid) atomicOr(&s_or[0], oid);
+    if (oca) atomicOr(&s_or[1], oca);
+  }
+  __syncthreads();
+  const uint32_t kbits = s_or[0] ? 64 - __builtin_clzll(s_or[0]) : 1;
+  const uint32_t cbits = s_or[1] ? 64 - __builtin_clzll(s_or[1]) : 1;
+  const uint32_t dbits = nd > 1 ? 32 - __builtin_clz(nd - 1) : 0;
+  const uint32_t W = max(max(token_bits, kbits), cbits);
+  // composite sort keys must fit 63 bits: otherwise the general path (host)
+  const bool fits = kbits + dbits <= 63 && W + 2 + dbits <= 63;
+  if (!fits && tid == 0) atomicOr(&ctl[2], 1u);
+  const uint64_t imask = (1ull << min(kbits, 63u)) - 1;
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) ck[u] = fits ? (((uint64_t)dl0[u] << kbits) | ck[u]) : 0ull;
+  mp_sort<NT, IT>(ck, val, len, fits ? kbits + dbits : 1, A, VS, wcnt, run);
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t i = wb_elem<IT>(u);
+    if (i >= len) continue;
+    I2J[i] = (uint16_t)val[u];
+    // a repeated id (::nodes is a map); an id of 0 repeats the virtual root's
+    if ((i > 0 && A[i - 1] == ck[u]) || (ck[u] & imask) == 0)
+      atomicOr(&dstat[ck[u] >> kbits], (uint32_t)CW_STATUS_DUP);
+  }
+  __syncthreads();
+
+  stamp(0);
+  // 2. key and cause-in-weave of every node, in id order (map.cljc:31-37)
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t i = wb_elem<IT>(u);
+    if (i >= len) continue;
+    const uint32_t dl = (uint32_t)(ck[u] >> kbits), j = val[u];
+    const uint64_t c = B[j];
+    uint64_t key;
+    uint16_t p;
+    uint32_t st = 0;
+    if (K8[j] & 0x80u) {  // (spec/valid? ::s/id cause): the cause node by binary search
+      const uint32_t a1 = dstart[dl + 1];
+      const uint64_t want = ((uint64_t)dl << kbits) | c;
+      const bool inrange = (c & ~imask) == 0;
+      uint32_t lo = dstart[dl], hi = a1;
+      while (inrange && lo < hi) {
+        const uint32_t m = (lo + hi) >> 1;
+        if (A[m] < want) lo = m + 1; else hi = m;
+      }
+      if (inrange && lo < a1 && A[lo] == want) {
+        const uint32_t jc = I2J[lo];
+        const uint64_t gc = B[jc];
+        if (K8[jc] & 0x80u) {  // the cause node is id-caused: the key is that id (F8c)
+          key = (1ull << W) | gc;
+          p = MP_CHAIN;
+        } else {
+          key = gc & tmask;
+          if (gc > tmask) st |= CW_STATUS_MAP_KEY;
+          p = (uint16_t)lo;
+        }
+      } else {  // the cause node is absent: the nil key
+        key = 2ull << W;
+        p = MP_CHAIN;
+        if (c == 0) st |= CW_STATUS_MAP_KEY;  // caused by the root id itself
+      }
+    } else {  // a key: woven under that key's root
+      key = c & tmask;
+      if (c > tmask) st |= CW_STATUS_MAP_KEY;
+      p = MP_ROOT;
+    }
+    P16[i] = p;
+    if (st) atomicOr(&dstat[dl], st);
+    ck[u] = fits ? (((uint64_t)dl << (W + 2)) | key) : 0ull;
+    val[u] = i;
+  }
+  __syncthreads();
+
+  stamp(1);
+  // 3. stable sort by (collection, key): every key weave a run, id order kept
+  mp_sort<NT, IT>(ck, val, len, fits ? W + 2 + dbits : 1, A, VS, wcnt, run);
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    if (q >= len) continue;
+    const uint32_t i = val[u], j = I2J[i], dl = (uint32_t)(ck[u] >> (W + 2));
+    Q[i] = (uint16_t)q;
+    LQ[q] = (uint16_t)(j - dstart[dl]);
+    KQ[q] = K8[j] & KIND_CLASS;
+  }
+  // key weave heads over contiguous runs of IT positions (A: the sorted keys)
+  uint32_t heads = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t q = tid * IT + k;
+    if (q < len && (q == 0 || A[q] != A[q - 1])) heads |= 1u << k;
+  }
+  uint32_t nseg;
+  const uint32_t sfirst = block_exscan<NT>(__popc(heads), wtot, &nseg);  // (its barriers free A)
+  {
+    uint32_t sg = sfirst;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t q = tid * IT + k;
+      if (q >= len) continue;
+      if ((heads >> k) & 1u) SS[sg++] = (uint16_t)q;
+      SEG[q] = (uint16_t)(sg - 1);
+    }
+  }
+  __syncthreads();  // SEG / SS are read across threads below
+  stamp(2);
+  // 4. publish this pack's number of key weaves (its prefix comes after the
+  // weave below, so the wait for earlier packs overlaps this pack's work)
+  if (tid == 0)
+    __hip_atomic_store(lb + pk, (pk == 0 ? LB_INC : LB_AGG) | nseg, __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
+
+  // 5. each key weave's list weave: member 0 the root, members 1..m in id order
+  uint32_t mst[IT], mm[IT], mr[IT], me[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    mst[u] = mm[u] = mr[u] = me[u] = 0;
+    if (q >= len) continue;
+    const uint32_t sg = SEG[q], st0 = SS[sg], en = sg + 1 < nseg ? SS[sg + 1] : len;
+    const uint32_t r = q - st0 + 1;
+    mst[u] = st0;
+    mm[u] = en - st0;
+    mr[u] = r;
+    const uint16_t p = P16[val[u]];
+    uint32_t par = 0;
+    if (p == MP_CHAIN) {
+      par = r - 1;
+    } else if (p != MP_ROOT) {  // the cause node: same key, so same key weave
+      const uint32_t qc = Q[p], dl = (uint32_t)(ck[u] >> (W + 2));
+      if (qc < st0 || qc >= en) atomicOr(&dstat[dl], (uint32_t)CW_STATUS_INTERNAL);
+      else if (qc >= q) atomicOr(&dstat[dl], (uint32_t)CW_STATUS_NON_LAMPORT);
+      else par = qc - st0 + 1;
+    }
+    PAR[q] = (uint16_t)par;
+    SZ[q] = 1;
+  }
+  __syncthreads();
+  // effective parent: a non-special climbs through special causes
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    if (q >= len) continue;
+    uint32_t e = PAR[q];
+    if (!is_special(KQ[q]))
+      for (uint32_t it = 0; e != 0 && is_special(KQ[mst[u] + e - 1]) && it < mm[u]; it++)
+        e = PAR[mst[u] + e - 1];
+    EFF[q] = (uint16_t)e;
+    me[u] = e;
+  }
+  __syncthreads();
+  // subtree sizes: every member counts itself into each effective ancestor
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    uint32_t a = me[u];
+    for (uint32_t it = 0; a != 0 && it < mm[u]; it++) {
+      atomicAdd(&SZ[mst[u] + a - 1], 1u);
+      a = EFF[mst[u] + a - 1];
+    }
+  }
+  __syncthreads();
+  // siblings before me: specials first, each class by descending id
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    if (q >= len) continue;
+    const bool sp = is_special(KQ[q]);
+    uint32_t bf = 0;
+    for (uint32_t x = mst[u]; x < mst[u] + mm[u]; x++) {
+      if (x == q || EFF[x] != me[u]) continue;
+      const bool sx = is_special(KQ[x]);
+      if ((sx && !sp) || (sx == sp && x > q)) bf += SZ[x];
+    }
+    BEF[q] = (uint16_t)bf;
+  }
+  __syncthreads();
+  // preorder position = sum over the effective ancestors of (1 + siblings before)
+  uint32_t mpos[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    mpos[u] = 0;
+    if (q >= len) continue;
+    uint32_t pos = 0, x = mr[u];
+    for (uint32_t it = 0; x != 0 && it < mm[u]; it++) {
+      pos += 1 + BEF[mst[u] + x - 1];
+      x = EFF[mst[u] + x - 1];
+    }
+    if (pos < 1 || pos > mm[u]) {
+      atomicOr(&dstat[(uint32_t)(ck[u] >> (W + 2))], (uint32_t)CW_STATUS_INTERNAL);
+      continue;
+    }
+    WV[mst[u] + pos - 1] = (uint16_t)q;
+    mpos[u] = pos;
+  }
+  __syncthreads();
+  // 6. active-node per key weave (map.cljc:47-59): blank when the first node
+  // after the root is a hide; else the first non-special not followed by a hide
+  int32_t *ACT = reinterpret_cast<int32_t *>(SZ);  // (sizes are done)
+  for (uint32_t sg = tid; sg < nseg; sg += NT) {
+    const uint32_t st0 = SS[sg], m = (sg + 1 < nseg ? SS[sg + 1] : len) - st0;
+    int32_t act = -1;
+    uint32_t k = KQ[WV[st0]];
+    if (!is_hide((uint8_t)k)) {
+      for (uint32_t p = 1; p <= m; p++) {
+        const uint32_t nk = p < m ? KQ[WV[st0 + p]] : 0u;
+        if (!is_special((uint8_t)k) && !(p < m && is_hide((uint8_t)nk))) {
+          act = (int32_t)LQ[WV[st0 + p - 1]];
+          break;
+        }
+        k = nk;
+      }
+    }
+    ACT[sg] = act;
+  }
+  stamp(4);
+  // 7. this pack's first key weave number: decoupled look-back over the packs,
+  // one wave reading 64 predecessors at a time (earlier packs are dispatched
+  // first and publish their counts before weaving, so the wait always ends)
+  if (tid < 64) {
+    const uint32_t lane = tid;
+    uint32_t base = 0;
+    if (pk > 0) {
+      for (int64_t q0 = (int64_t)pk - 1; q0 >= 0;) {
+        const int64_t q = q0 - lane;  // lane 0 = the nearest predecessor
+        const unsigned long long v =
+            q >= 0 ? __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
+        const uint64_t inc = __ballot((v >> 62) == 2), none = __ballot((v >> 62) == 0);
+        const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive
+        const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+        if (none & need) {  // a pack in the window has not counted its key weaves yet
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint32_t x = lane <= first ? (uint32_t)v : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        base += x;
+        if (first < 64) break;
+        q0 -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_base = base;
+      if ((uint64_t)base + nseg > cap_segs) atomicOr(&ctl[1], 1u);
+      if (pk == P - 1) {  // the batch's number of key weaves, and the end offset
+        ctl[0] = base + nseg;
+        if ((uint64_t)base + nseg <= cap_segs) seg_offsets[base + nseg] = n_total + base + nseg;
+      }
+    }
+  }
+  __syncthreads();
+  stamp(3);
+  const uint32_t sbase = s_base;
+  // 8. outputs: key weave sg = its root, then its members in weave order
+  if ((uint64_t)sbase + nseg <= cap_segs) {
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t q = wb_elem<IT>(u);
+      if (q >= len || mpos[u] == 0) continue;
+      const uint32_t sg = SEG[q];
+      const uint64_t goff = s0 + mst[u] + sbase + sg;
+      seg_perm[goff + mpos[u]] = LQ[q];
+      if (mr[u] == 1) {
+        const uint64_t g = ck[u] & ((1ull << (W + 2)) - 1), cls = g >> W;  // (W + 2 < 64)
+        seg_perm[goff] = 0xFFFFFFFFu;
+        seg_offsets[sbase + sg] = goff;
+        seg_coll[sbase + sg] = d0 + (uint32_t)(ck[u] >> (W + 2));
+        seg_key[sbase + sg] = cls == 0 ? g : cls == 1 ? (CW_MAP_ID_KEY | (g & ((1ull << W) - 1))) : CW_NIL;
+      }
+    }
+    for (uint32_t sg = tid; sg < nseg; sg += NT) seg_active[sbase + sg] = ACT[sg];
+  }
+  for (uint32_t dl = tid; dl < nd; dl += NT) status[d0 + dl] = dstat[dl];
+  stamp(5);
+  if (tprof && tid == 0)
+    for (int ph = 0; ph < 8; ph++) tprof[(size_t)pk * 8 + ph] = tacc[ph];
+}
+
+namespace {
+
+// cw_weave_maps through k_map_pack: every collection <= MPK nodes and every
+// pack's sort keys fit 63 bits (each pack finds its own key widths: no
+// reduction over the batch and no readback before the kernel).  Returns 1 when it does not apply (the caller takes
+// the general path), 0 on success, -1 on error.
+int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, bool dev,
+                      const uint64_t *id, const uint64_t *cause, const uint8_t *cis,
+                      const uint8_t *kind) {
+  const uint64_t D = bt->n_colls, *off = bt->coll_offsets;
+  const uint32_t N = (uint32_t)off[D];
+  // pack table, cached while the collection layout repeats
+  auto &pc = c->mpack;
+  const uint32_t PKN = c->map_pack == 1 ? 1024u : MPK;  // CW_MAP_PACK=1: packs of 1024 nodes
+  if (!(pc.pk == PKN && pc.off.size() == D + 1 && memcmp(pc.off.data(), off, (D + 1) * 8) == 0)) {
+    pc.off.assign(off, off + D + 1);
+    pc.pk = PKN;
+    pc.doc0.clear();
+    pc.ok = true;
+    uint32_t dmax = 1;
+    for (uint64_t d = 0; d < D;) {
+      const uint64_t a = d;
+      while (d < D && off[d + 1] - off[a] <= PKN) d++;
+      if (d == a) {  // a collection of more than MPK nodes
+        pc.ok = false;
+        break;
+      }
+      pc.doc0.push_back((uint32_t)a);
+      dmax = std::max<uint32_t>(dmax, (uint32_t)(d - a));
+    }
+    pc.doc0.push_back((uint32_t)D);
+    pc.dbits = ceil_log2(dmax);
+    if (pc.ok) {
+      uint32_t *dp = scratch_t<uint32_t>(c, "mp_doc0", pc.doc0.size());
+      uint64_t *dof = scratch_t<uint64_t>(c, "mp_off", D + 1);
+      if (!dp || !dof) return fail(c, "out of device memory (map packs)");
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(dp, pc.doc0.data(), pc.doc0.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(c, hipMemcpy(dof, off, (D + 1) * 8, hipMemcpyHostToDevice));
+    }
+  }
+  if (!pc.ok) return 1;
+  const uint32_t P = (uint32_t)pc.doc0.size() - 1;
+  const uint64_t cap = res->cap_segs;
+  unsigned long long *lb = scratch_t<unsigned long long>(c, "mp_lb", P);
+  uint32_t *ctl = scratch_t<uint32_t>(c, "mp_ctl", 4);
+  if (!lb || !ctl) return fail(c, "out of device memory (map packs)");
+  // outputs: the caller's arrays (device memory) or staging (host memory)
+  uint64_t *so = res->seg_offsets, *sk = res->seg_key;
+  uint32_t *sc = res->seg_coll, *sp = res->seg_perm, *st = res->status;
+  int64_t *sa = res->seg_active;
+  if (!dev) {
+    so = scratch_t<uint64_t>(c, "mp_so", cap + 1);
+    sk = scratch_t<uint64_t>(c, "mp_sk", cap);
+    sc = scratch_t<uint32_t>(c, "mp_sc", cap);
+    sp = scratch_t<uint32_t>(c, "mp_sp", N + cap);
+    st = scratch_t<uint32_t>(c, "mp_st", D);
+    sa = scratch_t<int64_t>(c, "mp_sa", cap);
+    if (!so || !sk || !sc || !sp || !st || !sa) return fail(c, "out of device memory (map outputs)");
+  }
+  unsigned long long *tprof = nullptr;
+  if (c->tree_prof) {
+    tprof = scratch_t<unsigned long long>(c, "mp_tprof", (size_t)P * 8);
+    if (!tprof) return fail(c, "out of device memory (tprof)");
+    HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)P * 64, c->stream));
+  }
+  HIPCHK(c, hipMemsetAsync(lb, 0, (size_t)P * 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(ctl, 0, 16, c->stream));
+  {
+    // ids, causes, flags and kinds in; per node seg_perm, per key weave
+    // offsets, collection, key, active node out
+    Launch L(c, "m_pack", (double)N * (8 + 8 + 1 + 1 + 4) + (double)N * 0.42 * (4 + 8 + 4 + 8 + 8));
+#define CW_MAP_PACK_LAUNCH(PK_, NT_)                                                              \
+  hipLaunchKernelGGL((k_map_pack<PK_, NT_>), dim3(P), dim3(NT_), 0, c->stream, id, cause, cis, kind, \
+                     (const uint64_t *)c->bufs["mp_off"].p, (const uint32_t *)c->bufs["mp_doc0"].p, \
+                     P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
+                     sp, st, ctl, tprof)
+    if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
+    else if (c->map_pack == 2) CW_MAP_PACK_LAUNCH(2048, 1024);
+    else CW_MAP_PACK_LAUNCH(2048, 512);
+#undef CW_MAP_PACK_LAUNCH
+  }
+  if (check_launch(c, "map_pack")) return -1;
+  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+  HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 12, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->pin_small[2]) return 1;  // a pack's keys need more than 63 bits: the general path
+  const uint64_t S = c->pin_small[0];
+  if (c->pin_small[1]) return fail(c, "cap_segs too small: %llu key weaves", (unsigned long long)S);
+  if (tprof) {
+    std::vector<unsigned long long> h((size_t)P * 8);
+    HIPCHK(c, hipMemcpy(h.data(), tprof, (size_t)P * 64, hipMemcpyDeviceToHost));
+    double a[8] = {0};
+    for (uint32_t q = 0; q < P; q++)
+      for (int ph = 0; ph < 8; ph++) a[ph] += (double)h[(size_t)q * 8 + ph];
+    fprintf(stderr, "map pack phases (memtime ticks per pack): sort1 %.0f keys %.0f sort2 %.0f "
+            "weave+active %.0f lookback %.0f outputs %.0f\n", a[0] / P, a[1] / P, a[2] / P, a[4] / P,
+            a[3] / P, a[5] / P);
+  }
+  if (!dev) {
+    HIPCHK(c, hipMemcpy(res->seg_perm, sp, ((size_t)N + S) * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->seg_offsets, so, (S + 1) * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->seg_coll, sc, S * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->seg_key, sk, S * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->seg_active, sa, S * 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(res->status, st, D * 4, hipMemcpyDeviceToHost));
+  }
+  res->n_segs = S;
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
+}  // namespace

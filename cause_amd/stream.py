@@ -98,7 +98,12 @@ class BatchStreamer:
     fill(i, (id, cause, kind) pinned numpy views) -> offsets (u64[D+1]) fills
     batch i into the slot and returns its document offsets; it runs on a
     producer thread (`depth` - 1 batches ahead of the GPU).  consume(BatchOut)
-    runs on the calling thread once the batch's results are in host memory."""
+    runs on the calling thread once the batch's results are in host memory.
+
+    The streamer borrows the Weaver: while it is open the Weaver launches on
+    the streamer's compute stream and returns right after enqueueing.  close()
+    (or leaving a ``with`` block) gives the Weaver back on its own stream, in
+    synchronous mode."""
 
     def __init__(self, weaver: abi.Weaver, device, max_nodes, max_docs, layout, depth=2):
         if depth < 2:
@@ -113,7 +118,23 @@ class BatchStreamer:
         self.slots = [_Slot(self.dev, self.max_nodes, self.max_docs) for _ in range(depth)]
         weaver.set_stream(self.s_w.cuda_stream)
         weaver.set_async(True)
+        self._open = True
         torch.cuda.synchronize(self.dev)
+
+    def close(self):
+        """Finish the streamer's work and hand the Weaver back (its own stream,
+        synchronous calls)."""
+        if getattr(self, "_open", False):
+            torch.cuda.synchronize(self.dev)
+            self.w.set_async(False)
+            self.w.set_stream(None)
+            self._open = False
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def _fill(self, fill, i, slot):
         # the slot's pinned inputs are free once the previous H2D from them ran

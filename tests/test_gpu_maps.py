@@ -23,16 +23,18 @@ ID_KEY = 1 << 63
 NIL = (1 << 64) - 1
 
 
-@pytest.fixture(scope="module", params=["small", "pipeline"])
+@pytest.fixture(scope="module", params=["fused", "small", "pipeline"])
 def weaver(request):
-    """Both ways of weaving key weaves: one wave per tiny key weave
-    (k_small_weave, LDS pack sorts) and the full list pipeline (CW_MAP_SMALL=0,
-    global radix passes)."""
+    """Every way of weaving key weaves: the one-kernel pack path (k_map_pack,
+    collections of <= 2048 nodes), one wave per tiny key weave after the
+    general sorts (k_small_weave, LDS pack sorts; CW_MAP_FUSED=0) and the full
+    list pipeline (CW_MAP_SMALL=0, global radix passes)."""
     import os
 
     # "pipeline" also sorts with the global radix passes instead of the LDS packs
-    knobs = ({"CW_MAP_SMALL": "1", "CW_PACK_SORT": "1"} if request.param == "small"
-             else {"CW_MAP_SMALL": "0", "CW_PACK_SORT": "0"})
+    knobs = {"fused": {"CW_MAP_FUSED": "1"},
+             "small": {"CW_MAP_FUSED": "0", "CW_MAP_SMALL": "1", "CW_PACK_SORT": "1"},
+             "pipeline": {"CW_MAP_FUSED": "0", "CW_MAP_SMALL": "0", "CW_PACK_SORT": "0"}}[request.param]
     old = {k: os.environ.get(k) for k in knobs}
     os.environ.update(knobs)
     try:
@@ -125,6 +127,21 @@ def test_large_collections_few_keys(weaver):
     _, tb = spec.layout()
     off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 6, nthreads=6)
     check(weaver, off, idk, ck, ci, kd, tb)
+
+
+def test_pack_limit_collections_long_key_weaves(weaver):
+    """Collections at the fused path's pack limit (2048 nodes) with 3 keys:
+    key weaves of hundreds of nodes woven inside one pack, next to a pack of
+    many tiny collections."""
+    spec = gen.MapSpec(nodes_per_coll=2048, n_keys=3, zipf_s=0.5, seed=12)
+    _, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 5, nthreads=5)
+    small = gen.MapSpec(nodes_per_coll=3, seed=13)
+    _, tb2 = small.layout()
+    o2, i2, c2, ci2, k2 = gen.generate_maps(small, 0, 700, nthreads=4)
+    cat = lambda a, b: np.concatenate([a, b])
+    off2 = np.concatenate([off, off[-1] + o2[1:]])
+    check(weaver, off2, cat(idk, i2), cat(ck, c2), cat(ci, ci2), cat(kd, k2), max(tb, tb2))
 
 
 def test_many_keys(weaver):

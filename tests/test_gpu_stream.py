@@ -80,3 +80,24 @@ def test_stream_rejects_oversized_batch():
         s = stream.BatchStreamer(w, "cuda:0", len(idk), 8, spec.layout())
         with pytest.raises(ValueError):
             s.run(1, fill)
+
+
+def test_stream_close_returns_the_weaver():
+    """After close() the Weaver is synchronous on its own stream again: a host
+    call right after sees finished results (the streamer used to
+    keep the Weaver on its private stream in async mode)."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=2000)
+    off, idk, ck, kd = gen.generate(spec, 0, 6, nthreads=2)
+
+    def fill(i, views):
+        n = len(idk)
+        views[0][:n], views[1][:n], views[2][:n] = idk, ck, kd
+        return off
+
+    with abi.Weaver(0) as w:
+        with stream.BatchStreamer(w, "cuda:0", len(idk), 6, spec.layout()) as s:
+            s.run(2, fill)
+        r = w.weave_lists(off, idk, ck, kd, spec.layout(), yarns=False)
+    perm, vis, st = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF)
+    np.testing.assert_array_equal(r.weave_perm, perm)
+    assert not r.status.any()
