@@ -3341,6 +3341,16 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
                          (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
                          kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
                          dev_tab(c, "t_tile_first"));
+    else if (c->tree_cfg == 4)
+      hipLaunchKernelGGL((k_tree<512, 1024>), dim3((uint32_t)D), dim3(512),
+                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
+    else if (c->tree_cfg == 5)
+      hipLaunchKernelGGL((k_tree<1024, 2048>), dim3((uint32_t)D), dim3(1024),
+                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
+                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
+                         dev_tab(c, "t_tile_first"));
     else if (c->tree_cfg == 1)
       hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
                          (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
