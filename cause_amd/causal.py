@@ -394,7 +394,10 @@ def weave_maps(cts):
         segs_of.setdefault(d, []).append(s)
     for d, (ct, nodes) in enumerate(zip(cts, docs)):
         st = int(res.status[d])
-        if st:
+        # non-Lamport causes and causes that are not nodes are the literal
+        # fold's (the library's fused map path); a repeated id, a key token
+        # out of range or an internal check are not a ::nodes map it weaves
+        if st & (abi.STATUS_DUP | abi.STATUS_MAP_KEY | abi.STATUS_INTERNAL):
             raise CauseError(f"map outside the weave's domain (status {st})", {"weave-domain"})
         weave, active = {}, {}
         for s in segs_of.get(d, []):

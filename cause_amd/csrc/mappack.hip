@@ -32,6 +32,8 @@
 constexpr uint32_t MPK = 2048;                 // largest pack (nodes); CW_MAP_PACK picks the geometry
 constexpr uint16_t MP_ROOT = 0xFFFFu;          // cause-in-weave = the key weave's root
 constexpr uint16_t MP_CHAIN = 0xFFFEu;         // appended after the previous node
+constexpr uint16_t MP_ROOT_ID = 0xFFFDu;       // caused by the root id [0 "0" 0] (not a node)
+constexpr uint16_t ML_ABSENT = 0xFFFFu;        // literal fold: the cause is not in the key weave
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 
 // Stable LDS radix sort of the pack's wave-blocked items by the low `bits` of
@@ -98,6 +100,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS], run[64], wtot[NT / 64];
   __shared__ uint32_t s_base;
   __shared__ unsigned long long s_or[2];
+  __shared__ uint8_t SLIT[PK];  // key weave woven by the literal fold (root-id / non-Lamport causes)
   uint16_t *SEG = reinterpret_cast<uint16_t *>(A), *SS = SEG + PK, *BEF = SS + PK, *WV = BEF + PK;
   uint16_t *PAR = reinterpret_cast<uint16_t *>(B), *EFF = PAR + PK;
   uint32_t *SZ = reinterpret_cast<uint32_t *>(EFF + PK);
@@ -205,8 +208,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         }
       } else {  // the cause node is absent: the nil key
         key = 2ull << W;
-        p = MP_CHAIN;
-        if (c == 0) st |= CW_STATUS_MAP_KEY;  // caused by the root id itself
+        // (caused by the root id: woven right after the nil key weave's root,
+        // which the literal fold below handles; other absent causes append)
+        p = c == 0 ? MP_ROOT_ID : MP_CHAIN;
       }
     } else {  // a key: woven under that key's root
       key = c & tmask;
@@ -251,6 +255,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       SEG[q] = (uint16_t)(sg - 1);
     }
   }
+  for (uint32_t sg = tid; sg < nseg; sg += NT) SLIT[sg] = 0;
   __syncthreads();  // SEG / SS are read across threads below
   stamp(2);
   // 4. publish this pack's number of key weaves (its prefix comes after the
@@ -275,14 +280,34 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     uint32_t par = 0;
     if (p == MP_CHAIN) {
       par = r - 1;
+    } else if (p == MP_ROOT_ID) {  // a child of the key weave's root, next to appended nodes
+      SLIT[sg] = 1;
     } else if (p != MP_ROOT) {  // the cause node: same key, so same key weave
       const uint32_t qc = Q[p], dl = (uint32_t)(ck[u] >> (W + 2));
-      if (qc < st0 || qc >= en) atomicOr(&dstat[dl], (uint32_t)CW_STATUS_INTERNAL);
-      else if (qc >= q) atomicOr(&dstat[dl], (uint32_t)CW_STATUS_NON_LAMPORT);
-      else par = qc - st0 + 1;
+      if (qc < st0 || qc >= en) {
+        atomicOr(&dstat[dl], (uint32_t)CW_STATUS_INTERNAL);
+      } else if (qc >= q) {  // the cause has a larger id: the literal fold
+        atomicOr(&dstat[dl], (uint32_t)CW_STATUS_NON_LAMPORT);
+        SLIT[sg] = 1;
+        par = qc - st0 + 1;
+      } else {
+        par = qc - st0 + 1;
+      }
     }
     PAR[q] = (uint16_t)par;
     SZ[q] = 1;
+  }
+  __syncthreads();
+  // a key weave the literal fold takes: each member's cause-in-weave as the
+  // fold sees it (0 = the root, a member, or ML_ABSENT: appended)
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    if (q >= len || !SLIT[SEG[q]]) continue;
+    const uint16_t p = P16[val[u]];
+    if (p == MP_CHAIN) PAR[q] = ML_ABSENT;
+    else if (p == MP_ROOT_ID || p == MP_ROOT) PAR[q] = 0;
+    me[u] = 0;
   }
   __syncthreads();
   // effective parent: a non-special climbs through special causes
@@ -290,6 +315,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t q = wb_elem<IT>(u);
     if (q >= len) continue;
+    if (SLIT[SEG[q]]) continue;  // (the literal fold below)
     uint32_t e = PAR[q];
     if (!is_special(KQ[q]))
       for (uint32_t it = 0; e != 0 && is_special(KQ[mst[u] + e - 1]) && it < mm[u]; it++)
@@ -312,7 +338,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t q = wb_elem<IT>(u);
-    if (q >= len) continue;
+    if (q >= len || SLIT[SEG[q]]) continue;
     const bool sp = is_special(KQ[q]);
     uint32_t bf = 0;
     for (uint32_t x = mst[u]; x < mst[u] + mm[u]; x++) {
@@ -329,7 +355,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t q = wb_elem<IT>(u);
     mpos[u] = 0;
-    if (q >= len) continue;
+    if (q >= len || SLIT[SEG[q]]) continue;
     uint32_t pos = 0, x = mr[u];
     for (uint32_t it = 0; x != 0 && it < mm[u]; it++) {
       pos += 1 + BEF[mst[u] + x - 1];
@@ -343,6 +369,70 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     mpos[u] = pos;
   }
   __syncthreads();
+  // the literal fold (shared.cljc:225-241, as exact.hip's k_xfold) for key
+  // weaves whose nodes are not all children of their causes in id order: one
+  // thread per such key weave, a linked list over its members (EFF = next,
+  // SZ = "a member with a smaller id is caused by me"); then each member's
+  // weave position into BEF
+  for (uint32_t sg = tid; sg < nseg; sg += NT) {
+    if (!SLIT[sg]) continue;
+    const uint32_t st0 = SS[sg], m = (sg + 1 < nseg ? SS[sg + 1] : len) - st0;
+    constexpr uint32_t END = 0xFFFFu, HEAD = 0xFFFEu;
+    for (uint32_t x = 1; x <= m; x++) SZ[st0 + x - 1] = 0;
+    for (uint32_t x = 1; x <= m; x++) {
+      const uint32_t c = PAR[st0 + x - 1];
+      if (c != ML_ABSENT && c > x && c <= m) SZ[st0 + c - 1] = 1;
+    }
+    uint32_t head = END, tail = END;
+    auto nxt = [&](uint32_t v) -> uint32_t { return v == HEAD ? head : EFF[st0 + v - 1]; };
+    for (uint32_t x = 1; x <= m; x++) {
+      const uint32_t c = PAR[st0 + x - 1];
+      const bool sp = is_special(KQ[st0 + x - 1]);
+      uint32_t at = END;  // the node x goes after (HEAD: right after the root)
+      if (c == 0) {
+        at = HEAD;
+      } else if (SZ[st0 + x - 1]) {  // first of: after the cause, before a child
+        uint32_t prev = HEAD;
+        for (uint32_t v = head; v != END; prev = v, v = EFF[st0 + v - 1]) {
+          if (PAR[st0 + v - 1] == x) {
+            at = prev;
+            break;
+          }
+          if (v == c) {
+            at = v;
+            break;
+          }
+        }
+      } else if (c != ML_ABSENT && c < x) {
+        at = c;
+      }
+      if (at == END) {
+        at = tail == END ? HEAD : tail;  // weave-asap? never held: the end
+      } else if (!sp) {                   // clause A: skip specials not caused by x
+        for (;;) {
+          const uint32_t q2 = nxt(at);
+          if (q2 == END || !is_special(KQ[st0 + q2 - 1]) || PAR[st0 + q2 - 1] == x) break;
+          at = q2;
+        }
+      }
+      const uint32_t q2 = nxt(at);
+      EFF[st0 + x - 1] = (uint16_t)q2;
+      if (at == HEAD) head = x;
+      else EFF[st0 + at - 1] = (uint16_t)x;
+      if (q2 == END) tail = x;
+    }
+    uint32_t pos = 1;
+    for (uint32_t v = head; v != END && pos <= m; v = EFF[st0 + v - 1], pos++) {
+      WV[st0 + pos - 1] = (uint16_t)(st0 + v - 1);
+      BEF[st0 + v - 1] = (uint16_t)pos;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t q = wb_elem<IT>(u);
+    if (q < len && SLIT[SEG[q]]) mpos[u] = BEF[q];
+  }
   // 6. active-node per key weave (map.cljc:47-59): blank when the first node
   // after the root is a hide; else the first non-special not followed by a hide
   int32_t *ACT = reinterpret_cast<int32_t *>(SZ);  // (sizes are done)

@@ -66,8 +66,9 @@ enum {
   CW_STATUS_DUP = 1u << 1,         /* two nodes share an id (shared.cljc:166-171)          */
   CW_STATUS_ORPHAN = 1u << 2,      /* a cause is not in the document (shared.cljc:175-178) */
   CW_STATUS_NON_LAMPORT = 1u << 3, /* a cause id is not older than its node                */
-  CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits, or a node caused by
-                                      the root id (its key weave mixes children and orphans) */
+  CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits; on the general map
+                                      path (a collection of > 2048 nodes) also a node caused by
+                                      the root id, which the fused path weaves exactly    */
   CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
   CW_STATUS_WEFT = 1u << 6,        /* weft: a cut id is not a node of the document         */
   CW_STATUS_KEY_RANGE = 1u << 7    /* an id key >= 2^63: it does not fit the K64 layout
@@ -176,7 +177,12 @@ int cw_weave_lists_k128(cw_ctx *ctx, const cw_list_batch_k128 *batch, cw_list_re
  * CW_NIL).  Every key weave is a list weave; the active node is its first
  * rendered node, blank when the root's first child is a hide.  Key weaves are
  * returned per collection in ascending seg_key order.  Ids and tokens must fit
- * 62 bits. */
+ * 62 bits.  Collections of <= 2048 nodes are woven by one kernel per pack of
+ * collections (mappack.hip), which also folds key weaves with nodes caused by
+ * the root id or by a node with a larger id literally (shared.cljc:225-241;
+ * CW_STATUS_NON_LAMPORT stays as information); on the general path those
+ * collections are flagged (MAP_KEY / NON_LAMPORT) and their output is
+ * unspecified. */
 typedef struct {
   uint64_t n_colls;
   const uint64_t *coll_offsets; /* HOST memory, [n_colls+1]                                */

@@ -45,6 +45,7 @@ def weaver(request):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+    w.fused = request.param == "fused"
     yield w
     w.close()
 
@@ -83,29 +84,36 @@ def gpu_maps(res, D):
     return out
 
 
-def expected_flags(off, idk, ck, ci):
-    """Host reading of the map domain: duplicate ids, root-id causes."""
+def expected_flags(off, idk, ck, ci, fused=False):
+    """Host reading of the map domain: duplicate ids; root-id causes, which
+    the general path flags and the fused path weaves by the literal fold."""
     flags = np.zeros(len(off) - 1, np.uint32)
     for d in range(len(off) - 1):
         a, b = int(off[d]), int(off[d + 1])
         if len(set(idk[a:b].tolist())) != b - a:
             flags[d] |= abi.STATUS_DUP
-        if ((ci[a:b] == 1) & (ck[a:b] == 0)).any():
+        if not fused and ((ci[a:b] == 1) & (ck[a:b] == 0)).any():
             flags[d] |= abi.STATUS_MAP_KEY
     return flags
 
 
 def check(weaver, off, idk, ck, ci, kd, token_bits, key_bits=0, flags=None):
+    """Every collection without a flag is compared with the literal map fold;
+    the fused path also weaves key weaves with non-Lamport causes exactly
+    (CW_STATUS_NON_LAMPORT stays as information), the general paths do not."""
     res = weaver.weave_maps(off, idk, ck, ci, kd, token_bits, key_bits)
     D = len(off) - 1
+    fused = getattr(weaver, "fused", False)
     if flags is None:
-        flags = expected_flags(off, idk, ck, ci)
+        flags = expected_flags(off, idk, ck, ci, fused)
     np.testing.assert_array_equal(res.status & (abi.STATUS_MAP_KEY | abi.STATUS_DUP), flags)
     got, want = gpu_maps(res, D), oracle_maps(off, idk, ck, ci, kd)
     for d in range(D):
         if flags[d]:
             continue
-        assert res.status[d] == 0, (d, res.status[d])
+        if res.status[d] & abi.STATUS_NON_LAMPORT and not fused:
+            continue
+        assert int(res.status[d]) & ~abi.STATUS_NON_LAMPORT == 0, (d, res.status[d])
         assert got[d] == want[d], f"collection {d}"
     # key weaves come per collection in ascending key order
     sc, sk = res.seg_coll.astype(np.uint64), res.seg_key
@@ -197,7 +205,8 @@ def test_absent_causes_nil_key_and_flags(weaver):
     j = 150 + int(np.flatnonzero(ci[150:200] == 0)[0])
     ci[j], ck[j] = 1, 0
     res = check(weaver, off, idk, ck, ci, kd, tb)
-    assert res.status[2] & abi.STATUS_DUP and res.status[3] & abi.STATUS_MAP_KEY
+    assert res.status[2] & abi.STATUS_DUP
+    assert bool(res.status[3] & abi.STATUS_MAP_KEY) != weaver.fused  # fused: the literal fold
     assert res.status[0] == 0 and res.status[1] == 0 and res.status[4] == 0
     nil = np.flatnonzero((res.seg_coll == 1) & (res.seg_key == np.uint64(NIL)))
     assert len(nil) == 1 and len(res.key_weave(int(nil[0]))) == 4
@@ -242,6 +251,44 @@ def test_random_small_maps_match_oracle(weaver):
         offs.append(len(I))
     check(weaver, np.array(offs, np.uint64), np.array(I, np.uint64), np.array(Cs, np.uint64),
           np.array(CI, np.uint8), np.array(K, np.uint8), 3)
+
+
+def test_literal_key_weaves_root_id_and_non_lamport_causes(weaver):
+    """Key weaves the reference folds with nodes that are not children of
+    their causes in id order: nodes caused by the root id [0 "0" 0] (the nil
+    key, next to nodes whose cause is absent) and undo/redo nodes whose cause
+    has a larger id.  The fused path weaves them by the literal fold and must
+    match the oracle's literal map fold exactly."""
+    rng = random.Random(23)
+    offs, I, Cs, CI, K = [0], [], [], [], []
+    for d in range(400):
+        n = rng.randint(2, 30)
+        nodes = []
+        ids = rng.sample(range(1, 200), n)
+        for m, t in enumerate(ids):
+            idv = (t << 2) | rng.randint(1, 3)
+            r = rng.random()
+            if r < 0.45:                   # a value or hide under a key
+                nodes.append([idv, rng.randint(0, 3), 0, rng.choice([0, 0, 0, 1])])
+            elif r < 0.6:                  # caused by the root id
+                nodes.append([idv, 0, 1, rng.choice([0, 1, 2, 3])])
+            elif r < 0.7:                  # an absent cause
+                nodes.append([idv, (rng.randint(200, 300) << 2) | 1, 1, rng.choice([0, 2, 3])])
+            else:                          # undo / redo of any node (older or newer)
+                nodes.append([idv, None, 1, rng.choice([1, 2, 3, 0])])
+        for x in nodes:
+            if x[1] is None:
+                x[1] = rng.choice(nodes)[0] if len(nodes) > 1 else 0
+                if x[1] == x[0]:
+                    x[1] = 0
+        rng.shuffle(nodes)
+        for x in nodes:
+            I.append(x[0]); Cs.append(x[1]); CI.append(x[2]); K.append(x[3])
+        offs.append(len(I))
+    res = check(weaver, np.array(offs, np.uint64), np.array(I, np.uint64), np.array(Cs, np.uint64),
+                np.array(CI, np.uint8), np.array(K, np.uint8), 2)
+    if weaver.fused:
+        assert (res.status & abi.STATUS_NON_LAMPORT).any()
 
 
 def test_repeat_calls_identical(weaver):
