@@ -2933,8 +2933,12 @@ int check_launch(cw_ctx *c, const char *what) {
   return 0;
 }
 
-int collect_prof(cw_ctx *c) {
+// Event pairs are read back when the stats are asked for (or a call is
+// synchronous, or many are pending): an asynchronous call under profiling
+// does not wait for its kernels.
+int collect_prof(cw_ctx *c, bool now = false) {
   if (c->pending.empty()) return 0;
+  if (!now && c->async && c->pending.size() < 8192) return 0;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (auto &p : c->pending) {
     float ms = 0;
@@ -4676,24 +4680,28 @@ const char *cw_last_error(const cw_ctx *c) { return c ? c->err.c_str() : "null c
 
 int cw_ctx_set_stream(cw_ctx *c, void *s) {
   if (!c) return -1;
+  if (collect_prof(c, true)) return -1;
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return 0;
 }
 
 int cw_ctx_set_async(cw_ctx *c, int a) {
   if (!c) return -1;
+  if (collect_prof(c, true)) return -1;
   c->async = a != 0;
   return 0;
 }
 
 int cw_ctx_set_profiling(cw_ctx *c, int on) {
   if (!c) return -1;
+  if (collect_prof(c, true)) return -1;
   c->prof = on != 0;
   return 0;
 }
 
 int cw_get_kernel_stats(const cw_ctx *c, cw_kernel_stat *out, int cap) {
   if (!c) return -1;
+  if (collect_prof(const_cast<cw_ctx *>(c), true)) return -1;
   int i = 0;
   for (auto &kv : c->stats) {
     if (i < cap && out) {
@@ -4790,6 +4798,7 @@ int cw_weave_ranked(cw_ctx *c, const cw_ranked_list *l, cw_list_result *r) {
 
 int cw_reset_kernel_stats(cw_ctx *c) {
   if (!c) return -1;
+  if (collect_prof(c, true)) return -1;
   c->stats.clear();
   return 0;
 }

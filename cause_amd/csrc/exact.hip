@@ -246,7 +246,16 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
   const uint64_t D = bt->n_docs;
   const uint64_t *off = bt->doc_offsets;
   if (!hint || D == 0 || off[D] == 0) return 0;
-  // the fast path's tables (uploaded for this layout) give the document offsets
+  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+  if (D <= 16) {
+    // a few documents (one giant list): their status words in one readback
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, out->status, D * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    bool any = false;
+    for (uint64_t d = 0; d < D; d++)
+      any |= (c->pin_small[d] & X_MASK) && !(c->pin_small[d] & X_SKIP) && off[d + 1] > off[d];
+    if (!any) return 0;
+  }
   uint32_t *cnt = scratch_t<uint32_t>(c, "x_cnt", 1);
   uint32_t *doff = scratch_t<uint32_t>(c, "x_doff", D + 1);
   if (!cnt || !doff) return fail(c, "out of device memory (exact path)");
@@ -260,7 +269,6 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
   hipLaunchKernelGGL(k_xcount, dim3((uint32_t)((D + 255) / 256)), dim3(256), 0, c->stream,
                      out->status, doff, (uint32_t)D, cnt);
   if (check_launch(c, "xcount")) return -1;
-  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
   HIPCHK(c, hipMemcpyAsync(c->pin_small, cnt, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->pin_small[0] == 0) return 0;
