@@ -23,6 +23,23 @@ STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1,
 STATUS_MAP_KEY = 16
 STATUS_WEFT = 64
 STATUS_KEY_RANGE = 128
+NIL32 = 0xFFFFFFFF
+K32_RESERVED = 0xFFFFFFF0     # K32 words from here up = the top 16 K64 values (CW_NIL, ...)
+
+
+def narrow_k32(id_key, cause_key):
+    """K64 packed keys -> the K32 words of cw_weave_lists_k32.  The top 16 K64
+    values (nil, the non-id cause) map to the top 16 K32 words; every other key
+    must be below K32_RESERVED (ValueError otherwise)."""
+    out = []
+    for a in (id_key, cause_key):
+        a = np.ascontiguousarray(a, np.uint64)
+        top = a >= np.uint64((1 << 64) - 16)
+        rest = np.where(top, np.uint64(0), a)
+        if rest.size and int(rest.max()) >= K32_RESERVED:
+            raise ValueError("keys do not fit K32 (every id and cause below 2^32 - 16)")
+        out.append(a.astype(np.uint32))     # the top 16 keep their low 32 bits
+    return out[0], out[1]
 
 
 class CwListBatch(C.Structure):
@@ -119,6 +136,9 @@ def lib():
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
                                      C.c_int]
         L.cw_weave_lists.restype = C.c_int
+        L.cw_weave_lists_k32.argtypes = [C.c_void_p, C.POINTER(CwListBatch),
+                                         C.POINTER(CwListResult), C.c_int]
+        L.cw_weave_lists_k32.restype = C.c_int
         L.cw_weave_lists_k128.argtypes = [C.c_void_p, C.POINTER(CwListBatchK128),
                                           C.POINTER(CwListResult), C.c_int]
         L.cw_weave_lists_k128.restype = C.c_int
@@ -291,6 +311,39 @@ class Weaver:
                          g("status"), g("yarn_perm"))
         self._check(self._L.cw_weave_lists(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
                     "cw_weave_lists")
+
+    def weave_lists_k32(self, offsets, id_key, cause_key, kind, layout, yarns=True,
+                        key_bits=None) -> ListResult:
+        """Host-memory call of cw_weave_lists_k32: id_key / cause_key are uint32
+        (nil = NIL32, see narrow_k32)."""
+        i = np.ascontiguousarray(id_key, np.uint32)
+        c = np.ascontiguousarray(cause_key, np.uint32)
+        k = np.ascontiguousarray(kind, np.uint8)
+        off = np.ascontiguousarray(offsets, np.uint64)
+        D, N = len(off) - 1, len(i)
+        if int(off[-1]) != N or len(c) != N or len(k) != N:
+            raise ValueError("offsets[-1] / id_key / cause_key / kind sizes differ")
+        b, off = self._batch(off, _ptr(i), _ptr(c), _ptr(k), layout, key_bits)
+        out = ListResult(np.zeros(N, np.uint32), np.zeros((N + 31) // 32, np.uint32),
+                         np.zeros(D, np.uint32), np.zeros(D, np.uint64), np.zeros(D, np.uint32),
+                         np.zeros(N, np.uint32) if (yarns and layout.site_bits) else None)
+        r = CwListResult(_ptr(out.weave_perm), _ptr(out.visible_bits), _ptr(out.visible_count),
+                         _ptr(out.max_ts), _ptr(out.status), _ptr(out.yarn_perm))
+        self._check(self._L.cw_weave_lists_k32(self._h, C.byref(b), C.byref(r), CW_MEM_HOST),
+                    "cw_weave_lists_k32")
+        return out
+
+    def weave_lists_k32_device(self, offsets, id_ptr, cause_ptr, kind_ptr, layout, out_ptrs,
+                               key_bits=None):
+        """Device-memory call of cw_weave_lists_k32 (u32 keys; out_ptrs as
+        weave_lists_device)."""
+        b, off = self._batch(offsets, C.c_void_p(id_ptr), C.c_void_p(cause_ptr),
+                             C.c_void_p(kind_ptr), layout, key_bits)
+        g = lambda n: C.c_void_p(out_ptrs[n]) if out_ptrs.get(n) else None
+        r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), g("max_ts"),
+                         g("status"), g("yarn_perm"))
+        self._check(self._L.cw_weave_lists_k32(self._h, C.byref(b), C.byref(r), CW_MEM_DEVICE),
+                    "cw_weave_lists_k32")
 
     @staticmethod
     def _batch_k128(offsets, id_ptr, cause_ptr, kind_ptr):

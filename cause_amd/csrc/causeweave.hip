@@ -3768,7 +3768,10 @@ int weave_lists_dev_all(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id,
 
 }
 
-int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace) {
+// dev_inputs: id_key / cause_key / kind are device arrays even when the results
+// are host memory (cw_weave_lists_k32 widens its keys on the device first).
+int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, int memspace,
+                     bool dev_inputs = false) {
   if (!bt || !res) return fail(c, "null batch/result");
   const uint64_t D = bt->n_docs;
   if (!bt->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
@@ -3798,29 +3801,32 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
   cw_list_result dres = *res;
   if (memspace == CW_MEM_HOST) {
     if (N && (!id || !cause || !kind)) return fail(c, "null input arrays");
-    uint64_t *did = scratch_t<uint64_t>(c, "h_id", N), *dca = scratch_t<uint64_t>(c, "h_cause", N);
-    uint8_t *dk = scratch_t<uint8_t>(c, "h_kind", N);
+    uint64_t *did = dev_inputs ? nullptr : scratch_t<uint64_t>(c, "h_id", N);
+    uint64_t *dca = dev_inputs ? nullptr : scratch_t<uint64_t>(c, "h_cause", N);
+    uint8_t *dk = dev_inputs ? nullptr : scratch_t<uint8_t>(c, "h_kind", N);
     dres.weave_perm = scratch_t<uint32_t>(c, "h_perm", N);
     dres.visible_bits = res->visible_bits ? scratch_t<uint32_t>(c, "h_bits", ((size_t)N + 31) / 32) : nullptr;
     dres.visible_count = scratch_t<uint32_t>(c, "h_vcount", D);
     dres.max_ts = res->max_ts ? scratch_t<uint64_t>(c, "h_maxts", D) : nullptr;
     dres.status = scratch_t<uint32_t>(c, "h_status", D);
     dres.yarn_perm = res->yarn_perm ? scratch_t<uint32_t>(c, "h_yarn", N) : nullptr;
-    if (!did || !dca || !dk || !dres.weave_perm || !dres.visible_count || !dres.status ||
-        (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
+    if ((!dev_inputs && (!did || !dca || !dk)) || !dres.weave_perm || !dres.visible_count ||
+        !dres.status || (res->visible_bits && !dres.visible_bits) || (res->max_ts && !dres.max_ts) ||
         (res->yarn_perm && !dres.yarn_perm))
       return fail(c, "out of device memory (host-mode staging)");
-    // Pageable host memory: blocking copies (hipMemcpyAsync from/to pageable
-    // memory is not reliably ordered by a later stream synchronize).
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (N) {
-      HIPCHK(c, hipMemcpy(did, id, (size_t)N * 8, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMemcpy(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice));
-      HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
+    if (!dev_inputs) {
+      // Pageable host memory: blocking copies (hipMemcpyAsync from/to pageable
+      // memory is not reliably ordered by a later stream synchronize).
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (N) {
+        HIPCHK(c, hipMemcpy(did, id, (size_t)N * 8, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(dca, cause, (size_t)N * 8, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
+      }
+      id = did;
+      cause = dca;
+      kind = dk;
     }
-    id = did;
-    cause = dca;
-    kind = dk;
   }
   if (weave_lists_dev_all(c, bt, id, cause, kind, &dres)) return -1;
 
@@ -3846,10 +3852,73 @@ int weave_lists_impl(cw_ctx *c, const cw_list_batch *bt, cw_list_result *res, in
       if (bt->doc_offsets[d + 1] == bt->doc_offsets[d])
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)(res->status + d), CW_STATUS_ROOT, 1,
                                     c->stream));
-    if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   if (c->prof) return collect_prof(c);
   return 0;
+}
+
+// --- K32: narrow keys (cw_weave_lists_k32) ---------------------------------------
+// Ids and causes arrive as u32 (half the bytes over PCIe and in HBM for a batch
+// whose packed ids fit 32 bits: config 2 needs 20) and are widened on the device
+// into the K64 pipeline's scratch.  The top 16 K32 values are the reserved top
+// of the K64 range (CW_NIL32 -> CW_NIL, CW_NIL32 - 1 -> the non-id cause, ...):
+// they widen by sign extension, everything else by zero extension.
+__global__ __launch_bounds__(256) void k_widen32(const uint32_t *__restrict__ id32,
+                                                 const uint32_t *__restrict__ ca32, uint32_t n,
+                                                 uint64_t *__restrict__ id,
+                                                 uint64_t *__restrict__ ca) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = id32[i], c = ca32[i];
+  id[i] = x >= CW_K32_RESERVED ? (uint64_t)(int64_t)(int32_t)x : (uint64_t)x;
+  ca[i] = c >= CW_K32_RESERVED ? (uint64_t)(int64_t)(int32_t)c : (uint64_t)c;
+}
+
+int weave_lists_k32_impl(cw_ctx *c, const cw_list_batch_k32 *b, cw_list_result *res, int memspace) {
+  if (!b || !res) return fail(c, "null batch/result");
+  if (!b->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
+  if (memspace != CW_MEM_HOST && memspace != CW_MEM_DEVICE) return fail(c, "bad memspace");
+  const uint64_t D = b->n_docs, N64 = b->doc_offsets[D];
+  if (N64 >= 0xFFFFFFFFull) return fail(c, "batch too large: N=%llu (limit 2^32-1)",
+                                        (unsigned long long)N64);
+  const uint32_t N = (uint32_t)N64;
+  const size_t Ns = std::max<uint32_t>(N, 1);
+  const uint32_t *id32 = b->id_key, *ca32 = b->cause_key;
+  const uint8_t *kind = b->kind;
+  if (N && (!id32 || !ca32 || !kind)) return fail(c, "null input arrays");
+  HIPCHK(c, hipSetDevice(c->device));
+  uint64_t *wid = scratch_t<uint64_t>(c, "k32_id", Ns), *wca = scratch_t<uint64_t>(c, "k32_cause", Ns);
+  if (!wid || !wca) return fail(c, "out of device memory (k32)");
+  if (memspace == CW_MEM_HOST && N) {
+    uint32_t *d32 = scratch_t<uint32_t>(c, "k32_h", 2 * Ns);
+    uint8_t *dk = scratch_t<uint8_t>(c, "h_kind", Ns);
+    if (!d32 || !dk) return fail(c, "out of device memory (k32 staging)");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(d32, id32, (size_t)N * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(d32 + Ns, ca32, (size_t)N * 4, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(dk, kind, N, hipMemcpyHostToDevice));
+    id32 = d32;
+    ca32 = d32 + Ns;
+    kind = dk;
+  }
+  if (N) {
+    Launch L(c, "widen32", (double)N * (4 + 4 + 8 + 8));
+    hipLaunchKernelGGL(k_widen32, dim3((N + 255) / 256), dim3(256), 0, c->stream, id32, ca32, N, wid,
+                       wca);
+  }
+  if (check_launch(c, "widen32")) return -1;
+  cw_list_batch wb{};
+  wb.n_docs = D;
+  wb.doc_offsets = b->doc_offsets;
+  wb.id_key = wid;
+  wb.cause_key = wca;
+  wb.kind = kind;
+  wb.key_bits = b->key_bits;
+  wb.ts_shift = b->ts_shift;
+  wb.site_shift = b->site_shift;
+  wb.site_bits = b->site_bits;
+  return weave_lists_impl(c, &wb, res, memspace, true);
 }
 
 // --- building blocks of the distributed giant list (cause_amd/giant.py) ---------
@@ -4099,7 +4168,7 @@ int weave_ranked_impl(cw_ctx *c, const cw_ranked_list *in, cw_list_result *out) 
     if ((c->pin_small[0] & X_MASK) && !(c->pin_small[0] & CW_STATUS_DUP) && exact_ranked(c, in, out))
       return -1;
   }
-  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->prof) return collect_prof(c);
   return 0;
 }
@@ -4723,6 +4792,12 @@ int cw_weave_lists(cw_ctx *c, const cw_list_batch *b, cw_list_result *r, int mem
   return weave_lists_impl(c, b, r, memspace);
 }
 
+int cw_weave_lists_k32(cw_ctx *c, const cw_list_batch_k32 *b, cw_list_result *r, int memspace) {
+  if (!c) return -1;
+  c->err.clear();
+  return weave_lists_k32_impl(c, b, r, memspace);
+}
+
 int cw_weave_lists_k128(cw_ctx *c, const cw_list_batch_k128 *b, cw_list_result *r, int memspace) {
   if (!c) return -1;
   c->err.clear();
@@ -4752,7 +4827,7 @@ int cw_sort_keys(cw_ctx *c, const uint64_t *keys, uint64_t n, uint32_t key_bits,
   if (!c) return -1;
   c->err.clear();
   if (sort_keys_impl(c, keys, n, key_bits, keys_out, idx_out)) return -1;
-  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }
 
@@ -4761,7 +4836,7 @@ int cw_lookup_keys(cw_ctx *c, const uint64_t *sorted, uint64_t n, const uint64_t
   if (!c) return -1;
   c->err.clear();
   if (lookup_keys_impl(c, sorted, n, queries, m, base, out, status)) return -1;
-  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }
 
@@ -4770,7 +4845,7 @@ int cw_gather(cw_ctx *c, const void *src, const uint32_t *idx, uint64_t m, uint3
   if (!c) return -1;
   c->err.clear();
   if (gather_impl(c, src, idx, m, elem_size, dst)) return -1;
-  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }
 
@@ -4786,7 +4861,7 @@ int cw_scatter32(cw_ctx *c, const uint32_t *src, const uint32_t *idx, uint64_t m
   if (!c) return -1;
   c->err.clear();
   if (scatter_impl(c, src, idx, m, dst)) return -1;
-  if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }
 

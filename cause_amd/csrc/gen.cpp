@@ -60,8 +60,9 @@ struct DocGen {
   std::vector<uint32_t> nonspecial;  // every non-special node (root included)
   Pool visible, hidden;
 
-  void run(const cwg_params &p, uint64_t d, uint32_t site_bits, uint64_t *idk, uint64_t *ck,
-           uint8_t *kd) {
+  // K = uint64_t (K64 keys, nil = all ones) or uint32_t (K32 keys, nil = CW_NIL32)
+  template <typename K>
+  void run(const cwg_params &p, uint64_t d, uint32_t site_bits, K *idk, K *ck, uint8_t *kd) {
     const uint32_t n = p.nodes_per_doc + 1;
     ts.assign(n, 0);
     site.assign(n, 0);
@@ -129,8 +130,8 @@ struct DocGen {
       for (uint32_t i = n - 1; i > 0; i--) std::swap(order[i], order[rng.below(i + 1)]);
     for (uint32_t j = 0; j < n; j++) {
       const uint32_t i = order[j];
-      idk[j] = ((uint64_t)ts[i] << site_bits) | site[i];
-      ck[j] = i == 0 ? UINT64_MAX : (((uint64_t)ts[cause[i]] << site_bits) | site[cause[i]]);
+      idk[j] = (K)(((uint64_t)ts[i] << site_bits) | site[i]);
+      ck[j] = i == 0 ? (K)~(K)0 : (K)(((uint64_t)ts[cause[i]] << site_bits) | site[cause[i]]);
       kd[j] = kind[i];
     }
   }
@@ -253,11 +254,15 @@ void cwg_layout(const cwg_params *p, uint32_t *ts_bits, uint32_t *site_bits) {
   *site_bits = bits_for(p->n_sites);
 }
 
-int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint64_t *id_key,
-                 uint64_t *cause_key, uint8_t *kind, int nthreads) {
+}  // extern "C"
+
+template <typename K>
+static int gen_docs(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, K *id_key,
+                    K *cause_key, uint8_t *kind, int nthreads) {
   if (!p || doc_end < doc_begin || p->n_sites == 0) return -1;
   uint32_t tsb, sb;
   cwg_layout(p, &tsb, &sb);
+  if (sizeof(K) == 4 && tsb + sb > 31) return -1;  // K32: every key below CW_K32_RESERVED
   const uint64_t n = (uint64_t)p->nodes_per_doc + 1;
   std::atomic<uint64_t> next{doc_begin};
   auto work = [&]() {
@@ -266,7 +271,7 @@ int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint
       const uint64_t d = next.fetch_add(1);
       if (d >= doc_end) break;
       const uint64_t o = (d - doc_begin) * n;
-      g.run(*p, d, sb, id_key + o, cause_key + o, kind + o);
+      g.run<K>(*p, d, sb, id_key + o, cause_key + o, kind + o);
     }
   };
   if (nthreads < 1) nthreads = 1;
@@ -275,6 +280,18 @@ int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint
   work();
   for (auto &t : th) t.join();
   return 0;
+}
+
+extern "C" {
+
+int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint64_t *id_key,
+                 uint64_t *cause_key, uint8_t *kind, int nthreads) {
+  return gen_docs<uint64_t>(p, doc_begin, doc_end, id_key, cause_key, kind, nthreads);
+}
+
+int cwg_generate32(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint32_t *id_key,
+                   uint32_t *cause_key, uint8_t *kind, int nthreads) {
+  return gen_docs<uint32_t>(p, doc_begin, doc_end, id_key, cause_key, kind, nthreads);
 }
 
 }  // extern "C"

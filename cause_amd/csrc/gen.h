@@ -40,6 +40,9 @@ void cwg_layout(const cwg_params *p, uint32_t *ts_bits, uint32_t *site_bits);
  * (doc_end-doc_begin)*(nodes_per_doc+1) entries.  Returns 0 on success. */
 int cwg_generate(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint64_t *id_key,
                  uint64_t *cause_key, uint8_t *kind, int nthreads);
+/* The same documents with K32 keys (cw_weave_lists_k32; nil = 0xFFFFFFFF). */
+int cwg_generate32(const cwg_params *p, uint64_t doc_begin, uint64_t doc_end, uint32_t *id_key,
+                   uint32_t *cause_key, uint8_t *kind, int nthreads);
 
 /* Maps: each collection holds `nodes_per_coll` nodes
  * typed by `n_sites` sites over `n_keys` key tokens drawn Zipf(zipf_s):

@@ -260,7 +260,7 @@ int weave_lists_k128_impl(cw_ctx *c, const cw_list_batch_k128 *bt, cw_list_resul
     for (uint64_t d = 0; d < D; d++)
       if (off[d + 1] == off[d])
         HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)(res->status + d), CW_STATUS_ROOT, 1, c->stream));
-    if (!c->async || c->prof) HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   if (c->prof) return collect_prof(c);
   return 0;

@@ -49,6 +49,8 @@ def lib():
         L.cwg_generate.argtypes = [C.POINTER(CwgParams), C.c_uint64, C.c_uint64, C.c_void_p,
                                    C.c_void_p, C.c_void_p, C.c_int]
         L.cwg_generate.restype = C.c_int
+        L.cwg_generate32.argtypes = L.cwg_generate.argtypes
+        L.cwg_generate32.restype = C.c_int
         L.cwg_map_layout.argtypes = [C.POINTER(CwgMapParams)] + [C.POINTER(C.c_uint32)] * 3
         L.cwg_map_layout.restype = None
         L.cwg_map_generate.argtypes = [C.POINTER(CwgMapParams), C.c_uint64, C.c_uint64] + \
@@ -89,18 +91,24 @@ CONFIG2 = GenSpec(nodes_per_doc=50_000, n_sites=8, p_hide=0.10, p_show=0.02, p_c
                   seed=0xC0FFEE ^ 2)
 
 
-def generate(spec: GenSpec, doc_begin: int, doc_end: int, nthreads: int | None = None, out=None):
+def generate(spec: GenSpec, doc_begin: int, doc_end: int, nthreads: int | None = None, out=None,
+             k32: bool = False):
     """-> (offsets u64[D+1], id_key u64[N], cause_key u64[N], kind u8[N]) for
     documents [doc_begin, doc_end) of ``spec``.  ``out`` may pass preallocated
-    (id, cause, kind) arrays (e.g. pinned host memory)."""
+    (id, cause, kind) arrays (e.g. pinned host memory).  k32: the same documents
+    with u32 keys for cw_weave_lists_k32 (nil = 0xFFFFFFFF)."""
     D = doc_end - doc_begin
     n = spec.doc_size
     N = D * n
+    kt = np.uint32 if k32 else np.uint64
     if out is None:
-        idk, ck, kd = np.empty(N, np.uint64), np.empty(N, np.uint64), np.empty(N, np.uint8)
+        idk, ck, kd = np.empty(N, kt), np.empty(N, kt), np.empty(N, np.uint8)
     else:
         idk, ck, kd = out
-    rc = lib().cwg_generate(C.byref(spec.params()), doc_begin, doc_end,
+        if idk.dtype != kt or ck.dtype != kt:
+            raise ValueError(f"out arrays must be {np.dtype(kt).name}")
+    fn = lib().cwg_generate32 if k32 else lib().cwg_generate
+    rc = fn(C.byref(spec.params()), doc_begin, doc_end,
                             idk.ctypes.data_as(C.c_void_p), ck.ctypes.data_as(C.c_void_p),
                             kd.ctypes.data_as(C.c_void_p), nthreads or min(os.cpu_count() or 1, 32))
     if rc != 0:

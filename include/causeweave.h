@@ -95,7 +95,8 @@ int cw_ctx_set_stream(cw_ctx *ctx, void *hip_stream);
 /* 0: synchronous calls (default).  1: device-memory calls return right after
  * enqueueing (the caller synchronises the stream). */
 int cw_ctx_set_async(cw_ctx *ctx, int async);
-/* Per-kernel timing with HIP events on the launch stream (adds a sync per call). */
+/* Per-kernel timing with HIP events on the launch stream (event pairs are read
+ * back when the stats are asked for; asynchronous calls stay asynchronous). */
 int cw_ctx_set_profiling(cw_ctx *ctx, int on);
 
 typedef struct {
@@ -140,6 +141,30 @@ typedef struct {
  * cause_key / kind and every result array live (doc_offsets is always host). */
 int cw_weave_lists(cw_ctx *ctx, const cw_list_batch *batch, cw_list_result *result,
                    int memspace);
+
+/* K32: narrow keys.  The same batch as cw_list_batch with 4-byte id and cause
+ * words, for batches whose packed ids fit 32 bits (config 2 needs 20): half the
+ * input bytes over PCIe and in HBM.  The keys are widened on the device and
+ * woven by cw_weave_lists' pipeline, so results and limits are cw_weave_lists'.
+ * Keys are below CW_K32_RESERVED; the 16 values from there up stand for the
+ * top 16 K64 values (CW_NIL32 = CW_NIL is a nil cause, CW_NIL32 - 1 a cause
+ * that is no id). */
+#define CW_NIL32 0xFFFFFFFFu
+#define CW_K32_RESERVED 0xFFFFFFF0u
+typedef struct {
+  uint64_t n_docs;
+  const uint64_t *doc_offsets; /* HOST memory, [n_docs+1]                                */
+  const uint32_t *id_key;      /* [N] packed id of each node                             */
+  const uint32_t *cause_key;   /* [N] packed cause id (CW_NIL32 for the root)            */
+  const uint8_t *kind;         /* [N] CW_KIND_*                                          */
+  uint32_t key_bits;           /* as cw_list_batch                                        */
+  uint32_t ts_shift;
+  uint32_t site_shift;
+  uint32_t site_bits;
+} cw_list_batch_k32;
+
+int cw_weave_lists_k32(cw_ctx *ctx, const cw_list_batch_k32 *batch, cw_list_result *result,
+                       int memspace);
 
 /* K128: ids that need more than 63 bits (ts:64 | site_rank:32 |
  * tx:32).  Every id is two u64 words, hi then lo:

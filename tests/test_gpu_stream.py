@@ -19,8 +19,8 @@ def _batch(spec, i, docs):
     return gen.generate(spec, d0, d0 + docs[i], nthreads=4)
 
 
-@pytest.mark.parametrize("depth", [2, 3])
-def test_stream_matches_direct_and_oracle(depth):
+@pytest.mark.parametrize("depth,k32", [(2, False), (3, False), (2, True)])
+def test_stream_matches_direct_and_oracle(depth, k32):
     import torch
 
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=700)
@@ -31,6 +31,8 @@ def test_stream_matches_direct_and_oracle(depth):
     def fill(i, views):
         off, idk, ck, kd = batches[i]
         n = len(idk)
+        if k32:
+            idk, ck = abi.narrow_k32(idk, ck)
         views[0][:n], views[1][:n], views[2][:n] = idk, ck, kd
         return off
 
@@ -41,7 +43,8 @@ def test_stream_matches_direct_and_oracle(depth):
                         o.max_ts.copy(), o.status.copy())
 
     with abi.Weaver(0) as w:
-        s = stream.BatchStreamer(w, "cuda:0", max_nodes, max(docs), spec.layout(), depth=depth)
+        s = stream.BatchStreamer(w, "cuda:0", max_nodes, max(docs), spec.layout(), depth=depth,
+                                 k32=k32)
         st = s.run(len(docs), fill, consume)
         del s
         torch.cuda.synchronize()
