@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--stream-docs", type=int, default=1_000_000,
                     help="--config 3: documents in the whole job (all GPUs)")
     ap.add_argument("--depth", type=int, default=2, help="--config 3: pipeline slots")
+    ap.add_argument("--keys", type=int, default=64, choices=[32, 64],
+                    help="configs 1/2/5: key words of the resident inputs (32 = cw_weave_lists_k32)")
     ap.add_argument("--k64", action="store_true",
                     help="--config 3: stream 8-byte keys (cw_weave_lists) instead of K32")
     ap.add_argument("--no-prestaged", action="store_true",
@@ -80,6 +82,18 @@ def launch_ranks(a) -> int:
            str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.call(cmd, env=env)
+
+
+def _k64(*keys):
+    """K32 words -> the K64 keys they stand for (reserved top words sign-extend);
+    K64 keys pass through."""
+    out = []
+    for x in keys:
+        if x.dtype == np.uint32:
+            x = np.where(x >= 0xFFFFFFF0, x.view(np.int32).astype(np.int64).view(np.uint64),
+                         x.astype(np.uint64))
+        out.append(x)
+    return out
 
 
 def check_lists(off, idk, ck, kd, perm, bits, vcount, status):
@@ -607,12 +621,14 @@ def main():
         workload = "config2: independent CausalLists, full reweave"
     layout = spec.layout()
     t0 = time.time()
+    k32 = a.keys == 32
     with heartbeat("generating the input"):
-        off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16)
+        off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16, k32=k32)
     N = len(idk)
     t_gen = time.time() - t0
-    g_id = torch.from_numpy(idk.view(np.int64)).to(dev)
-    g_ca = torch.from_numpy(ck.view(np.int64)).to(dev)
+    kv = np.int32 if k32 else np.int64
+    g_id = torch.from_numpy(idk.view(kv)).to(dev)
+    g_ca = torch.from_numpy(ck.view(kv)).to(dev)
     g_kd = torch.from_numpy(kd).to(dev)
     perm = torch.empty(N, dtype=torch.int32, device=dev)
     bits = torch.empty((N + 31) // 32, dtype=torch.int32, device=dev)
@@ -628,8 +644,10 @@ def main():
     w.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     w.set_async(True)
 
+    call = w.weave_lists_k32_device if k32 else w.weave_lists_device
+
     def step():
-        w.weave_lists_device(off, g_id.data_ptr(), g_ca.data_ptr(), g_kd.data_ptr(), layout, outs)
+        call(off, g_id.data_ptr(), g_ca.data_ptr(), g_kd.data_ptr(), layout, outs)
 
     for _ in range(a.warmup):
         step()
@@ -658,7 +676,7 @@ def main():
     value = total_nodes / dt_max
     check = None
     if a.check:
-        bad = check_lists(off, idk, ck, kd, perm, bits, vcount, status)
+        bad = check_lists(off, *_k64(idk, ck), kd, perm, bits, vcount, status)
         tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
         check = {"documents_checked": tot[1], "mismatches": tot[0],
                  "against": "effective-tree preorder + visibility (oracle, C)"}
@@ -706,7 +724,7 @@ def main():
     if rank == 0:
         cpu = None
         if world == 1 and not a.no_cpu:
-            cpu = (cpu_baseline_prefix(idk, ck, kd, 100_000) if a.config == 5 else
+            cpu = (cpu_baseline_prefix(*_k64(idk, ck), kd, 100_000) if a.config == 5 else
                    cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64))
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
@@ -718,6 +736,7 @@ def main():
                        "nodes_per_gpu": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
                        "p_show": spec.p_show, "p_conj": spec.p_conj,
                        "key_bits": layout.key_bits,
+                       "key_words": "u32 (cw_weave_lists_k32)" if k32 else "u64 (cw_weave_lists)",
                        "parallelism": (f"replicas x{world}" if a.config in (1, 5)
                                        else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
