@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--stream-docs", type=int, default=1_000_000,
                     help="--config 3: documents in the whole job (all GPUs)")
     ap.add_argument("--depth", type=int, default=2, help="--config 3: pipeline slots")
+    ap.add_argument("--tree", default="auto", choices=["auto", "dist", "root"],
+                    help="--config 5 --dist: the tree rank by rank (dist) or on rank 0 (root); "
+                         "auto = dist for N > 1")
     ap.add_argument("--keys", type=int, default=64, choices=[32, 64],
                     help="configs 1/2/5: key words of the resident inputs (32 = cw_weave_lists_k32)")
     ap.add_argument("--k64", action="store_true",
@@ -254,9 +257,11 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     """--config 5 on N GPUs: ONE list of --giant nodes whose nodes are spread
     over the ranks (rank r holds every N-th node of the generation order).
     One step = cause_amd.giant.weave_distributed: local sort, sample sort by
-    all_to_all (RCCL), cause join at the owners, gather of the rank-ordered
-    arrays on rank 0 and the tree + tour there.  Strong scaling: the list is
-    the same at every N."""
+    all_to_all (RCCL), cause join at the owners, then (--tree dist, the
+    default for N > 1) the tree rank by rank with all-to-all rounds and the
+    successors gathered on rank 0 for the list ranking, or (--tree root) the
+    rank-ordered arrays gathered on rank 0 and the whole tree + tour there.
+    Strong scaling: the list is the same at every N."""
     import dataclasses
 
     from cause_amd import abi, gen, giant
@@ -290,7 +295,7 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
 
     def step():
         return giant.weave_distributed(ops, g_id, g_ca, g_kd, lay.key_bits, ts_shift=lay.ts_shift,
-                                       group=group)
+                                       group=group, tree=a.tree)
 
     res = None
     for _ in range(a.warmup):
@@ -326,7 +331,9 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
             "warmup": a.warmup, "ms_per_step": dt_max / a.steps * 1e3, "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": (f"config5: one CausalList of {N:,} nodes spread over "
-                                    f"{world} rank(s), distributed sample sort + gather"),
+                                    f"{world} rank(s), distributed sample sort + "
+                                    f"{'tree by rank' if a.tree == 'dist' or (a.tree == 'auto' and world > 1) else 'tree on rank 0'}"),
+                       "tree": a.tree,
                        "nodes_total": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
                        "key_bits": lay.key_bits,
                        "parallelism": f"sample sort x{world} ({dist.get_backend()})"},

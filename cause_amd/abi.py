@@ -95,6 +95,20 @@ class CwRankedList(C.Structure):
     _fields_ = [("n", C.c_uint64), ("par", C.c_void_p), ("kind", C.c_void_p), ("val", C.c_void_p)]
 
 
+class CwLinkedList(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("succ", C.c_void_p), ("val", C.c_void_p)]
+
+
+# the distributed tree's building blocks (include/causeweave.h, dist.hip):
+# argument types after the context
+_DIST_ARGS = {
+    "check": "U64 U32 P P P", "eff": "U64 U32 P P P", "climb": "U64 U32 P P P U64 P",
+    "pending": "P U64 U32 P", "gkey": "P P U64 P", "runs": "P P U64 U32 P P P P",
+    "rkey": "P U64 P", "link": "P P U64 P U32 U64 P P P", "put": "P P U64 U32 U64 P",
+    "thr": "P U64 U32 P", "fetch": "P U32 U64 P U64 P", "succ": "P P P P U64 U32 P",
+}
+
+
 class CwKernelStat(C.Structure):
     _fields_ = [("name", C.c_char * 48), ("launches", C.c_uint64), ("total_ms", C.c_double),
                 ("bytes_alg", C.c_double)]
@@ -158,9 +172,14 @@ def lib():
         L.cw_gather.argtypes = [P, P, P, U64, U32, P]
         L.cw_scatter32.argtypes = [P, P, P, U64, P]
         L.cw_weave_ranked.argtypes = [P, C.POINTER(CwRankedList), C.POINTER(CwListResult)]
+        L.cw_weave_linked.argtypes = [P, C.POINTER(CwLinkedList), C.POINTER(CwListResult)]
         for f in ("cw_sort_keys", "cw_lookup_keys", "cw_partition_keys", "cw_gather", "cw_scatter32",
-                  "cw_weave_ranked"):
+                  "cw_weave_ranked", "cw_weave_linked"):
             getattr(L, f).restype = C.c_int
+        for f, a in _DIST_ARGS.items():
+            fn = getattr(L, "cw_dist_" + f)
+            fn.argtypes = [P] + [{"P": P, "U64": U64, "U32": U32}[x] for x in a.split()]
+            fn.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -429,6 +448,19 @@ class Weaver:
         r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), None, g("status"),
                          None)
         self._check(self._L.cw_weave_ranked(self._h, C.byref(lst), C.byref(r)), "cw_weave_ranked")
+
+    def dist(self, name, *args):
+        """cw_dist_<name>(ctx, *args): a building block of the distributed tree
+        (device pointers as ints, sizes, bases)."""
+        self._check(getattr(self._L, "cw_dist_" + name)(self._h, *args), "cw_dist_" + name)
+
+    def weave_linked_device(self, n, succ_ptr, val_ptr, out_ptrs):
+        """cw_weave_linked: out_ptrs as weave_ranked_device."""
+        lst = CwLinkedList(n, succ_ptr, val_ptr)
+        g = lambda k: C.c_void_p(out_ptrs[k]) if out_ptrs.get(k) else None
+        r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), None, g("status"),
+                         None)
+        self._check(self._L.cw_weave_linked(self._h, C.byref(lst), C.byref(r)), "cw_weave_linked")
 
     def merge_lists(self, a, b, layout, yarns=True) -> MergeResult:
         """Host-memory call of cw_merge_lists.  a, b: (offsets, id_key, cause_key,

@@ -3253,7 +3253,7 @@ int ensure_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool force_giant =
 int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *par,
                const uint8_t *skind, const uint32_t *sval, const uint32_t *kbm,
                const uint64_t *skey, uint32_t ts_shift, cw_list_result *out,
-               void *spareA = nullptr, void *spareB = nullptr) {
+               void *spareA = nullptr, void *spareB = nullptr, bool linked = false) {
   auto &t = c->tab;
   const dim3 B256(256);
   if (giant && out->max_ts && skey) {  // ::lamport-ts = largest id (k_fdir wrote it otherwise)
@@ -3283,8 +3283,9 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   }
   uint32_t *doc_off = dev_tab(c, "t_doc_off"), *doc_log2k = dev_tab(c, "t_doc_log2k");
   uint32_t *doc_W = dev_tab(c, "t_doc_W"), *walk_first = dev_tab(c, "t_walk_first");
-  // 3-5. effective parents, sibling order, links
-  if (giant) {
+  // 3-5. effective parents, sibling order, links (linked: the caller wrote
+  // link and thr, cw_weave_linked)
+  if (giant && !linked) {
     const uint32_t gbits = ceil_log2(2ull * N + 2);
     const uint32_t root_key = gbits >= 32 ? 0xFFFFFFFFu : (1u << gbits) - 1;
     // group keys: sort input in thr (written only after the sort), ping-pong
@@ -3693,6 +3694,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
 
 #include "exact.hip"
 #include "mappack.hip"
+#include "dist.hip"
 
 namespace {
 
@@ -4089,8 +4091,10 @@ int gather_impl(cw_ctx *c, const void *src, const uint32_t *idx, uint64_t m, uin
     hipLaunchKernelGGL(k_gather<uint32_t>, G, B, 0, c->stream, (const uint32_t *)src, idx, m, (uint32_t *)dst);
   else if (es == 1)
     hipLaunchKernelGGL(k_gather<uint8_t>, G, B, 0, c->stream, (const uint8_t *)src, idx, m, (uint8_t *)dst);
+  else if (es == 16)
+    hipLaunchKernelGGL(k_gather<uint4>, G, B, 0, c->stream, (const uint4 *)src, idx, m, (uint4 *)dst);
   else
-    return fail(c, "gather: element size %u (1, 4 or 8)", es);
+    return fail(c, "gather: element size %u (1, 4, 8 or 16)", es);
   return check_launch(c, "gather");
 }
 
@@ -4869,6 +4873,68 @@ int cw_weave_ranked(cw_ctx *c, const cw_ranked_list *l, cw_list_result *r) {
   if (!c) return -1;
   c->err.clear();
   return weave_ranked_impl(c, l, r);
+}
+
+// distributed tree (dist.hip): device memory, ordered on the context's stream
+#define CW_DIST_ENTRY(call)                                \
+  if (!c) return -1;                                       \
+  c->err.clear();                                          \
+  HIPCHK(c, hipSetDevice(c->device));                      \
+  if (call) return -1;                                     \
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream)); \
+  return c->prof ? collect_prof(c) : 0;
+
+int cw_dist_check(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                  uint32_t *status) {
+  CW_DIST_ENTRY(dist_check_impl(c, n, base, par, kind, status))
+}
+int cw_dist_eff(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                uint32_t *eff) {
+  CW_DIST_ENTRY(dist_eff_impl(c, n, base, par, kind, eff))
+}
+int cw_dist_climb(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                  const uint64_t *q, uint64_t m, uint32_t *out) {
+  CW_DIST_ENTRY(dist_climb_impl(c, n, base, par, kind, q, m, out))
+}
+int cw_dist_pending(cw_ctx *c, const uint32_t *w, uint64_t n, uint32_t mode, uint64_t *keys) {
+  CW_DIST_ENTRY(dist_pending_impl(c, w, n, mode, keys))
+}
+int cw_dist_gkey(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint64_t *key) {
+  CW_DIST_ENTRY(dist_gkey_impl(c, eff, kind, n, key))
+}
+int cw_dist_runs(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
+                 const uint8_t *kind, uint32_t *nsc, uint64_t *okey, uint32_t *rec) {
+  CW_DIST_ENTRY(dist_runs_impl(c, skey, sidx, n, base, kind, nsc, okey, rec))
+}
+int cw_dist_rkey(cw_ctx *c, const uint32_t *rec, uint64_t m, uint64_t *key) {
+  CW_DIST_ENTRY(dist_rkey_impl(c, rec, m, key))
+}
+int cw_dist_link(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t m,
+                 const uint32_t *rec, uint32_t base, uint64_t n, uint32_t *fcS, uint32_t *fcN,
+                 uint32_t *reply) {
+  CW_DIST_ENTRY(dist_link_impl(c, skey, sidx, m, rec, base, n, fcS, fcN, reply))
+}
+int cw_dist_put(cw_ctx *c, const uint32_t *rec, const uint32_t *reply, uint64_t m, uint32_t base,
+                uint64_t n, uint32_t *nsc) {
+  CW_DIST_ENTRY(dist_put_impl(c, rec, reply, m, base, n, nsc))
+}
+int cw_dist_thr(cw_ctx *c, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *T) {
+  CW_DIST_ENTRY(dist_thr_impl(c, nsc, n, base, T))
+}
+int cw_dist_fetch(cw_ctx *c, const uint32_t *src, uint32_t base, uint64_t n, const uint64_t *q,
+                  uint64_t m, uint32_t *out) {
+  CW_DIST_ENTRY(dist_fetch_impl(c, src, base, n, q, m, out))
+}
+int cw_dist_succ(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
+                 const uint32_t *T, uint64_t n, uint32_t base, uint32_t *out) {
+  CW_DIST_ENTRY(dist_succ_impl(c, kind, fcS, fcN, T, n, base, out))
+}
+#undef CW_DIST_ENTRY
+
+int cw_weave_linked(cw_ctx *c, const cw_linked_list *l, cw_list_result *r) {
+  if (!c) return -1;
+  c->err.clear();
+  return weave_linked_impl(c, l, r);
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

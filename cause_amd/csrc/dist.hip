@@ -1,0 +1,398 @@
+// dist.hip -- the tree of ONE list spread over several GPUs (BASELINE config
+// 5), rank by rank.  Included by causeweave.hip after weave_tail.
+//
+// After the sample sort and the cause join (cause_amd/giant.py) rank r holds
+// the nodes of global ranks [base, base + n) -- a contiguous run of the id
+// order -- with par (global rank of the cause) and kind.  The single-GPU tree
+// (k_geff / k_gsib / k_gthr: SURVEY F5 effective parents, sibling order, F6
+// visibility, preorder successors) needs nodes of other ranks in three places,
+// each resolved by all-to-all rounds between kernels of this file:
+//
+//   effective parent: a non-special node climbs through special causes
+//     (weave-later? clause A, shared.cljc:208-212).  cw_dist_eff climbs while
+//     the cause is local; a climb that leaves the run asks the owner of the
+//     next cause (cw_dist_climb answers with its own local climb).
+//   siblings: children of e, specials first, each class newest first
+//     (shared.cljc:194-223).  Every rank sorts its (e, class) group keys and
+//     links its local runs (cw_dist_runs); one record per run (its oldest and
+//     newest node) goes to the owner of e, which orders the runs of every
+//     group (cw_dist_link): the newest run's newest node is e's first child
+//     of that class, each older run's newest node the next sibling of the
+//     next run's oldest, and the oldest special's next sibling is e's newest
+//     non-special.  The answers go back (cw_dist_put).
+//   threads: thr(x) = next sibling of x, else thr(e(x)) -- the preorder
+//     successor of a node without children.  cw_dist_thr resolves the local
+//     chains by pointer jumping; pointers into earlier ranks are answered by
+//     their owners (cw_dist_fetch), at most W - 1 rounds since a thread
+//     pointer only moves to a smaller rank.
+//
+// cw_dist_succ then gives every node its successor (first child, else thread)
+// and render bit, and the list ranking runs on one GPU (cw_weave_linked).
+
+constexpr uint32_t DIST_PEND = 0x80000000u;  // eff: climb goes on at the rank in the low bits
+constexpr uint32_t DIST_NONE = 0xFFFFFFFFu;  // eff of the root
+constexpr uint32_t DIST_RES = 0x80000000u;   // thread word: resolved (low bits: the successor)
+constexpr uint32_t FCS_HIDE = 0x80000000u;   // fcS word: the newest special child is a hide
+constexpr uint64_t DIST_ROOT_KEY = (1ull << 33) - 1;  // group key of the root: sorts last (33 bits)
+
+__global__ __launch_bounds__(256) void k_dist_check(const uint32_t *__restrict__ par,
+                                                    const uint8_t *__restrict__ kind, uint32_t n,
+                                                    uint32_t base, uint32_t *__restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t st = 0;
+  if (i < n) {
+    const uint32_t g = base + i;
+    const bool root = (kind[i] & KIND_ROOT) != 0;
+    if ((g == 0) != root) st |= CW_STATUS_ROOT;
+    if (g > 0 && par[i] >= g) st |= par[i] >= CW_NIL_RANK ? CW_STATUS_ORPHAN : CW_STATUS_NON_LAMPORT;
+  }
+  if (__syncthreads_or(st != 0)) {
+    if (st) atomicOr(status, st);
+  }
+}
+
+// Climb from global rank c (local or not) through local special nodes: the
+// first local non-special, or DIST_PEND | the first rank outside the run.
+__device__ __forceinline__ uint32_t dist_climb(uint32_t c, const uint32_t *__restrict__ par,
+                                               const uint8_t *__restrict__ kind, uint32_t n,
+                                               uint32_t base) {
+  for (uint32_t hop = 0; hop <= n; hop++) {
+    if (c < base || c - base >= n) return DIST_PEND | c;
+    if (!is_special(kind[c - base])) return c;
+    const uint32_t p = par[c - base];
+    if (p >= c) return 0;  // (out of domain: checked before; keeps the climb bounded)
+    c = p;
+  }
+  return 0;
+}
+
+__global__ __launch_bounds__(256) void k_dist_eff(const uint32_t *__restrict__ par,
+                                                  const uint8_t *__restrict__ kind, uint32_t n,
+                                                  uint32_t base, uint32_t *__restrict__ eff) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (base + i == 0) {
+    eff[i] = DIST_NONE;
+    return;
+  }
+  eff[i] = is_special(kind[i]) ? par[i] : dist_climb(par[i], par, kind, n, base);
+}
+
+__global__ __launch_bounds__(256) void k_dist_climb(const uint32_t *__restrict__ par,
+                                                    const uint8_t *__restrict__ kind, uint32_t n,
+                                                    uint32_t base, const uint64_t *__restrict__ q,
+                                                    uint32_t m, uint32_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) out[i] = dist_climb((uint32_t)q[i], par, kind, n, base);
+}
+
+// Partition keys of the words still waiting on another rank (UINT64_MAX: none).
+// mode 0: eff words (DIST_PEND | rank); mode 1: thread words (a rank without DIST_RES).
+__global__ __launch_bounds__(256) void k_dist_pending(const uint32_t *__restrict__ w, uint32_t n,
+                                                      uint32_t mode, uint64_t *__restrict__ keys) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t x = w[i];
+  bool pend;
+  if (mode == 0) pend = (x & DIST_PEND) && x != DIST_NONE;
+  else pend = !(x & DIST_RES);
+  keys[i] = pend ? (uint64_t)(x & ~DIST_PEND) : ~0ull;
+}
+
+// Group keys (e << 1 | class; special = 0; 33 bits) for the local sort; the root last.
+__global__ __launch_bounds__(256) void k_dist_gkey(const uint32_t *__restrict__ eff,
+                                                   const uint8_t *__restrict__ kind, uint32_t n,
+                                                   uint64_t *__restrict__ key) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t e = eff[i];
+  key[i] = e == DIST_NONE ? DIST_ROOT_KEY : (((uint64_t)e << 1) | (is_special(kind[i]) ? 0u : 1u));
+}
+
+// Runs of equal group keys in the locally sorted order: inside a run each node's
+// next sibling is the next older node; a run's oldest node waits for the owner
+// of e (record: group, oldest, newest, kind of the newest; key = e for the
+// partition by owner, UINT64_MAX on the other positions).
+__global__ __launch_bounds__(256) void k_dist_runs(const uint64_t *__restrict__ skey,
+                                                   const uint32_t *__restrict__ sidx, uint32_t n,
+                                                   uint32_t base, const uint8_t *__restrict__ kind,
+                                                   uint32_t *__restrict__ nsc,
+                                                   uint64_t *__restrict__ okey,
+                                                   uint4 *__restrict__ rec) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = skey[i];
+  okey[i] = ~0ull;
+  const uint32_t x = sidx[i];
+  if (k == DIST_ROOT_KEY) {  // the root: no siblings
+    nsc[x] = 0;
+    return;
+  }
+  if (i > 0 && skey[i - 1] == k) {
+    nsc[x] = base + sidx[i - 1];
+    return;
+  }
+  uint32_t lo = i, hi = n;  // the run's end: first position with a larger key
+  while (lo < hi) {
+    const uint32_t mid = lo + ((hi - lo) >> 1);
+    if (skey[mid] <= k) lo = mid + 1; else hi = mid;
+  }
+  const uint32_t newest = sidx[lo - 1];
+  nsc[x] = NSC_UP | (uint32_t)(k >> 1);  // placeholder until the owner answers
+  okey[i] = k >> 1;
+  rec[i] = make_uint4((uint32_t)k, base + x, base + newest, kind[newest]);
+}
+
+// At the owner of e: the runs of every group sorted by (group, oldest).
+__global__ __launch_bounds__(256) void k_dist_rkey(const uint4 *__restrict__ rec, uint32_t m,
+                                                   uint64_t *__restrict__ key) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key[i] = ((uint64_t)rec[i].x << 32) | rec[i].y;
+}
+
+__global__ __launch_bounds__(256) void k_dist_link(const uint64_t *__restrict__ skey,
+                                                   const uint32_t *__restrict__ sidx, uint32_t m,
+                                                   const uint4 *__restrict__ rec, uint32_t base,
+                                                   uint32_t n, uint32_t *__restrict__ fcS,
+                                                   uint32_t *__restrict__ fcN,
+                                                   uint32_t *__restrict__ reply) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint32_t g = (uint32_t)(skey[j] >> 32), e = g >> 1;
+  const uint4 r = rec[sidx[j]];
+  const bool first = j == 0 || (uint32_t)(skey[j - 1] >> 32) != g;
+  const bool last = j + 1 == m || (uint32_t)(skey[j + 1] >> 32) != g;
+  uint32_t ns = NSC_UP | e;
+  if (!first) {
+    ns = rec[sidx[j - 1]].z;
+  } else if (!(g & 1)) {  // the oldest special: e's newest non-special follows the specials
+    const uint64_t want = (uint64_t)(g | 1u) + 1;  // first key of the next group
+    uint32_t lo = j, hi = m;
+    while (lo < hi) {
+      const uint32_t mid = lo + ((hi - lo) >> 1);
+      if ((skey[mid] >> 32) < want) lo = mid + 1; else hi = mid;
+    }
+    if (lo > 0 && (uint32_t)(skey[lo - 1] >> 32) == (g | 1u)) ns = rec[sidx[lo - 1]].z;
+  }
+  reply[sidx[j]] = ns;
+  if (last && e >= base && e - base < n) {
+    if (g & 1) fcN[e - base] = r.z;
+    else fcS[e - base] = r.z | (is_hide((uint8_t)r.w) ? FCS_HIDE : 0u);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dist_put(const uint4 *__restrict__ rec,
+                                                  const uint32_t *__restrict__ reply, uint32_t m,
+                                                  uint32_t base, uint32_t n,
+                                                  uint32_t *__restrict__ nsc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint32_t x = rec[i].y - base;
+  if (x < n) nsc[x] = reply[i];
+}
+
+__global__ __launch_bounds__(256) void k_dist_thr_init(const uint32_t *__restrict__ nsc, uint32_t n,
+                                                       uint32_t base, uint32_t *__restrict__ T) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = nsc[i];
+  T[i] = base + i == 0 ? (DIST_RES | SUCCW_END) : (s & NSC_UP) ? (s & ~NSC_UP) : (DIST_RES | s);
+}
+
+// One round of pointer jumping over the pointers into this rank's run.
+__global__ __launch_bounds__(256) void k_dist_jump(uint32_t *T, uint32_t n, uint32_t base,
+                                                   uint32_t *open) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool o = false;
+  if (i < n) {
+    const uint32_t a = T[i];
+    if (!(a & DIST_RES) && a >= base && a - base < n) {
+      const uint32_t b = T[a - base];
+      T[i] = b;
+      o = !(b & DIST_RES) && b >= base && b - base < n;
+    }
+  }
+  if (__syncthreads_or(o)) {
+    if (threadIdx.x == 0) atomicOr(open, 1u);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dist_fetch(const uint32_t *__restrict__ src, uint32_t base,
+                                                    uint32_t n, const uint64_t *__restrict__ q,
+                                                    uint32_t m, uint32_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t x = q[i] - base;
+  out[i] = x < n ? src[x] : (DIST_RES | SUCCW_END);
+}
+
+// Successor (first child -- the newest special, else the newest non-special --
+// else the thread) and render bit of every node of the run.
+__global__ __launch_bounds__(256) void k_dist_succ(const uint8_t *__restrict__ kind,
+                                                   const uint32_t *__restrict__ fcS,
+                                                   const uint32_t *__restrict__ fcN,
+                                                   const uint32_t *__restrict__ T, uint32_t n,
+                                                   uint32_t base, uint32_t *__restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t fs = fcS[i], fn = fcN[i];
+  const uint32_t t = T[i];
+  const uint32_t succ = (fs & ~FCS_HIDE) ? (fs & ~FCS_HIDE) : fn ? fn : (t & ~DIST_RES);
+  const bool vis = !is_special(kind[i]) && base + i != 0 && !(fs && (fs & FCS_HIDE));
+  out[i] = succ | (vis ? LINK_VIS : 0u);
+}
+
+// cw_weave_linked: link words for the giant walk from successor | render bit.
+__global__ __launch_bounds__(256) void k_linked_words(const uint32_t *__restrict__ sv, uint32_t n,
+                                                      uint32_t log2k, uint64_t *__restrict__ link,
+                                                      uint32_t *__restrict__ thr) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t w = sv[r], succ = w & ~LINK_VIS;
+  const bool split = r == split_node(0, r >> log2k, log2k, n);
+  const uint32_t f = (w & LINK_VIS) | (split ? LINK_SPLIT : 0u);
+  link[r] = (uint64_t)(succ < n ? succ : SUCCW_END) | ((uint64_t)f << 32);
+  thr[r] = succ < n ? succ : SUCCW_END;
+}
+
+int dist_launch_ok(cw_ctx *c, const char *nm) { return check_launch(c, nm); }
+
+#define DIST_GRID(m) dim3((uint32_t)(((m) + 255) / 256)), dim3(256), 0, c->stream
+
+int dist_check_impl(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                    uint32_t *status) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_dist_check, DIST_GRID(n), par, kind, (uint32_t)n, base, status);
+  return dist_launch_ok(c, "dist_check");
+}
+
+int dist_eff_impl(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                  uint32_t *eff) {
+  if (!n) return 0;
+  Launch L(c, "dist_eff", (double)n * (4 + 1 + 4));
+  hipLaunchKernelGGL(k_dist_eff, DIST_GRID(n), par, kind, (uint32_t)n, base, eff);
+  return dist_launch_ok(c, "dist_eff");
+}
+
+int dist_climb_impl(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
+                    const uint64_t *q, uint64_t m, uint32_t *out) {
+  if (!m) return 0;
+  hipLaunchKernelGGL(k_dist_climb, DIST_GRID(m), par, kind, (uint32_t)n, base, q, (uint32_t)m, out);
+  return dist_launch_ok(c, "dist_climb");
+}
+
+int dist_pending_impl(cw_ctx *c, const uint32_t *w, uint64_t n, uint32_t mode, uint64_t *keys) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_dist_pending, DIST_GRID(n), w, (uint32_t)n, mode, keys);
+  return dist_launch_ok(c, "dist_pending");
+}
+
+int dist_gkey_impl(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint64_t *key) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_dist_gkey, DIST_GRID(n), eff, kind, (uint32_t)n, key);
+  return dist_launch_ok(c, "dist_gkey");
+}
+
+int dist_runs_impl(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
+                   const uint8_t *kind, uint32_t *nsc, uint64_t *okey, uint32_t *rec) {
+  if (!n) return 0;
+  Launch L(c, "dist_runs", (double)n * (8 + 4 + 4 + 8) + (double)n * 0.4 * 16);
+  hipLaunchKernelGGL(k_dist_runs, DIST_GRID(n), skey, sidx, (uint32_t)n, base, kind, nsc, okey,
+                     reinterpret_cast<uint4 *>(rec));
+  return dist_launch_ok(c, "dist_runs");
+}
+
+int dist_rkey_impl(cw_ctx *c, const uint32_t *rec, uint64_t m, uint64_t *key) {
+  if (!m) return 0;
+  hipLaunchKernelGGL(k_dist_rkey, DIST_GRID(m), reinterpret_cast<const uint4 *>(rec), (uint32_t)m, key);
+  return dist_launch_ok(c, "dist_rkey");
+}
+
+int dist_link_impl(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t m,
+                   const uint32_t *rec, uint32_t base, uint64_t n, uint32_t *fcS, uint32_t *fcN,
+                   uint32_t *reply) {
+  if (!m) return 0;
+  Launch L(c, "dist_link", (double)m * (8 + 4 + 16 + 4 + 4));
+  hipLaunchKernelGGL(k_dist_link, DIST_GRID(m), skey, sidx, (uint32_t)m,
+                     reinterpret_cast<const uint4 *>(rec), base, (uint32_t)n, fcS, fcN, reply);
+  return dist_launch_ok(c, "dist_link");
+}
+
+int dist_put_impl(cw_ctx *c, const uint32_t *rec, const uint32_t *reply, uint64_t m, uint32_t base,
+                  uint64_t n, uint32_t *nsc) {
+  if (!m) return 0;
+  hipLaunchKernelGGL(k_dist_put, DIST_GRID(m), reinterpret_cast<const uint4 *>(rec), reply,
+                     (uint32_t)m, base, (uint32_t)n, nsc);
+  return dist_launch_ok(c, "dist_put");
+}
+
+// Thread words with every pointer into the local run resolved (pointer
+// jumping, one readback per round: O(log depth) rounds).
+int dist_thr_impl(cw_ctx *c, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *T) {
+  if (!n) return 0;
+  hipLaunchKernelGGL(k_dist_thr_init, DIST_GRID(n), nsc, (uint32_t)n, base, T);
+  if (dist_launch_ok(c, "dist_thr")) return -1;
+  uint32_t *open = scratch_t<uint32_t>(c, "dist_open", 1);
+  if (!open) return fail(c, "out of device memory (dist_thr)");
+  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+  Launch L(c, "dist_jump", (double)n * 12);
+  for (int round = 0; round < 64; round++) {
+    HIPCHK(c, hipMemsetAsync(open, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_dist_jump, DIST_GRID(n), T, (uint32_t)n, base, open);
+    if (dist_launch_ok(c, "dist_jump")) return -1;
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, open, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (!c->pin_small[0]) return 0;
+  }
+  return fail(c, "dist_thr: pointer jumping did not converge");
+}
+
+int dist_fetch_impl(cw_ctx *c, const uint32_t *src, uint32_t base, uint64_t n, const uint64_t *q,
+                    uint64_t m, uint32_t *out) {
+  if (!m) return 0;
+  hipLaunchKernelGGL(k_dist_fetch, DIST_GRID(m), src, base, (uint32_t)n, q, (uint32_t)m, out);
+  return dist_launch_ok(c, "dist_fetch");
+}
+
+int dist_succ_impl(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
+                   const uint32_t *T, uint64_t n, uint32_t base, uint32_t *out) {
+  if (!n) return 0;
+  Launch L(c, "dist_succ", (double)n * (1 + 4 + 4 + 4 + 4));
+  hipLaunchKernelGGL(k_dist_succ, DIST_GRID(n), kind, fcS, fcN, T, (uint32_t)n, base, out);
+  return dist_launch_ok(c, "dist_succ");
+}
+
+// The walk, ranking and emit of one list given every node's successor.
+int weave_linked_impl(cw_ctx *c, const cw_linked_list *in, cw_list_result *out) {
+  if (!in || !out) return fail(c, "null list/result");
+  if (!out->weave_perm || !out->visible_count || !out->status)
+    return fail(c, "weave_perm, visible_count and status are required");
+  if (out->yarn_perm || out->max_ts) return fail(c, "yarn_perm / max_ts: not produced from links");
+  const uint64_t n64 = in->n;
+  if (n64 == 0 || n64 >= SUCCW_END) return fail(c, "list size %llu (1 .. 2^31-2)", (unsigned long long)n64);
+  if (!in->succ) return fail(c, "null input arrays");
+  const uint32_t n = (uint32_t)n64;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t off[2] = {0, n64};
+  if (ensure_tables(c, 1, off, true)) return -1;
+  HIPCHK(c, hipMemsetAsync(out->status, 0, 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(out->visible_count, 0, 4, c->stream));
+  if (out->visible_bits)
+    HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)n + 31) / 32 * 4, c->stream));
+  uint64_t *link = scratch_t<uint64_t>(c, "link", n);
+  uint32_t *thr = scratch_t<uint32_t>(c, "thr", n);
+  if (!link || !thr) return fail(c, "out of device memory (linked, n=%u)", n);
+  {
+    Launch L(c, "linked", (double)n * (4 + 8 + 4));
+    hipLaunchKernelGGL(k_linked_words, DIST_GRID(n), in->succ, n, c->tab.doc_log2k[0], link, thr);
+  }
+  if (dist_launch_ok(c, "linked")) return -1;
+  if (weave_tail(c, 1, n, true, nullptr, nullptr, in->val, nullptr, nullptr, 0, out, nullptr, nullptr,
+                 true))
+    return -1;
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->prof) return collect_prof(c);
+  return 0;
+}
+
+#undef DIST_GRID

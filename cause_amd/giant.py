@@ -131,6 +131,116 @@ class HipOps:
                                    {k: t.data_ptr() for k, t in o.items()})
         return o
 
+    # --- the distributed tree (dist.hip) ----------------------------------------
+    @staticmethod
+    def _p(t):
+        return t.data_ptr() if t is not None and t.numel() else 0
+
+    @_on_stream
+    def dist_check(self, par, kind, base):
+        st = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.w.dist("check", par.numel(), base, self._p(par), self._p(kind), st.data_ptr())
+        return int(st.item())
+
+    @_on_stream
+    def dist_eff(self, par, kind, base):
+        eff = self._e(par.numel(), torch.int32)
+        self.w.dist("eff", par.numel(), base, self._p(par), self._p(kind), self._p(eff))
+        return eff
+
+    @_on_stream
+    def dist_climb(self, par, kind, base, q):
+        out = self._e(q.numel(), torch.int32)
+        self.w.dist("climb", par.numel(), base, self._p(par), self._p(kind), self._p(q), q.numel(),
+                    self._p(out))
+        return out
+
+    @_on_stream
+    def dist_pending(self, w, mode):
+        keys = self._e(w.numel(), torch.int64)
+        self.w.dist("pending", self._p(w), w.numel(), mode, self._p(keys))
+        return keys
+
+    @_on_stream
+    def dist_gkey(self, eff, kind):
+        key = self._e(eff.numel(), torch.int64)
+        self.w.dist("gkey", self._p(eff), self._p(kind), eff.numel(), self._p(key))
+        return key
+
+    @_on_stream
+    def dist_runs(self, skey, sidx, base, kind):
+        n = skey.numel()
+        nsc, okey = self._e(n, torch.int32), self._e(n, torch.int64)
+        rec = self._e(n * 4, torch.int32)
+        self.w.dist("runs", self._p(skey), self._p(sidx), n, base, self._p(kind), self._p(nsc),
+                    self._p(okey), self._p(rec))
+        return nsc, okey, rec.view(n, 4)
+
+    @_on_stream
+    def dist_rkey(self, rec):
+        key = self._e(rec.shape[0], torch.int64)
+        self.w.dist("rkey", self._p(rec), rec.shape[0], self._p(key))
+        return key
+
+    @_on_stream
+    def dist_link(self, skey, sidx, rec, base, n, fcS, fcN):
+        reply = self._e(rec.shape[0], torch.int32)
+        self.w.dist("link", self._p(skey), self._p(sidx), rec.shape[0], self._p(rec), base, n,
+                    self._p(fcS), self._p(fcN), self._p(reply))
+        return reply
+
+    @_on_stream
+    def dist_put(self, rec, reply, base, nsc):
+        self.w.dist("put", self._p(rec), self._p(reply), rec.shape[0], base, nsc.numel(), self._p(nsc))
+
+    @_on_stream
+    def dist_thr(self, nsc, base):
+        T = self._e(nsc.numel(), torch.int32)
+        self.w.dist("thr", self._p(nsc), nsc.numel(), base, self._p(T))
+        return T
+
+    @_on_stream
+    def dist_fetch(self, src, base, q):
+        out = self._e(q.numel(), torch.int32)
+        self.w.dist("fetch", self._p(src), base, src.numel(), self._p(q), q.numel(), self._p(out))
+        return out
+
+    @_on_stream
+    def dist_succ(self, kind, fcS, fcN, T, base):
+        out = self._e(T.numel(), torch.int32)
+        self.w.dist("succ", self._p(kind), self._p(fcS), self._p(fcN), self._p(T), T.numel(), base,
+                    self._p(out))
+        return out
+
+    @_on_stream
+    def gather_rows(self, rec, idx):
+        """rec[idx] for 16-byte rows (int32 [n, 4])."""
+        m = idx.numel()
+        out = self._e(m * 4, torch.int32).view(m, 4)
+        if m:
+            self.w.gather_device(rec.data_ptr(), idx.data_ptr(), m, 16, out.data_ptr())
+        return out
+
+    @_on_stream
+    def scatter_into(self, dst, src, idx):
+        """dst[idx[i]] = src[i] (4-byte elements, in place)."""
+        if idx.numel():
+            self.w.scatter32_device(src.data_ptr(), idx.data_ptr(), idx.numel(), dst.data_ptr())
+
+    @_on_stream
+    def zeros32(self, n):
+        return torch.zeros(n, dtype=torch.int32, device=self.dev)
+
+    @_on_stream
+    def weave_linked(self, succ, val):
+        n = succ.numel()
+        o = {"weave_perm": self._e(n, torch.int32),
+             "visible_bits": self._e((n + 31) // 32, torch.int32),
+             "visible_count": self._e(1, torch.int32), "status": self._e(1, torch.int32)}
+        self.w.weave_linked_device(n, succ.data_ptr(), val.data_ptr(),
+                                   {k: t.data_ptr() for k, t in o.items()})
+        return o
+
     def sync(self):
         torch.cuda.synchronize(self.dev)
 
@@ -196,20 +306,89 @@ def choose_splitters(samples, weights, W):
 
 
 def weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift=0, group=None,
-                      root=0, samples=256) -> GiantResult:
+                      root=0, samples=256, tree="auto") -> GiantResult:
     """Weave one list whose nodes are spread over the ranks of `group`.
 
     id_key / cause_key: int64 tensors holding the packed u64 keys (< 2^63);
-    kind: uint8.  Every rank calls this; rank `root` receives the weave."""
+    kind: uint8.  Every rank calls this; rank `root` receives the weave.
+    tree: "dist" builds the tree rank by rank (_tree_distributed), "root" on
+    the root alone (cw_weave_ranked), "auto" = dist for W > 1.  Lists outside
+    the fast path's domain always take "root" (its exact path)."""
     if key_bits > 63:
         raise ValueError("keys must be < 2^63 (int64 order)")
+    if tree not in ("auto", "dist", "root"):
+        raise ValueError("tree: auto, dist or root")
     ctx = getattr(ops, "stream_context", contextlib.nullcontext)
     with ctx():
         return _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root,
-                                  samples)
+                                  samples, tree)
 
 
-def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples):
+def _route(ops, keys, split_t, W, group, dev):
+    """Send every entry whose key (a global rank) is < N to the owner of that
+    rank: (positions of the sent entries, send counts, receive counts, the
+    keys received).  Keys of UINT64_MAX (-1 as int64) stay home."""
+    perm, counts = ops.partition(keys, split_t)   # W + 1 buckets: the last one stays
+    send = counts[:W]
+    idx = perm[:sum(send)]
+    q = ops.gather(keys, idx)
+    recv = _exchange_counts(send, group, dev)
+    return idx, send, recv, _a2a(q, send, recv, group)
+
+
+def _any(v, group, dev):
+    return sum(x[0] for x in _all_gather_ints([v], group, dev))
+
+
+def _tree_distributed(ops, par, kind, base, owns, group, dev):
+    """Preorder successor | render bit of this rank's nodes (global ranks
+    [base, base + n)) -- the giant path's tree with the
+    cross-rank steps as all-to-all rounds (dist.hip)."""
+    W = len(owns)
+    N = sum(owns)
+    n = par.numel()
+    starts = [sum(owns[:j]) for j in range(1, W)] + [N]
+    split_t = torch.as_tensor(np.array(starts, np.int64), device=dev)
+    # effective parents: climbs leave the run at most W - 1 times
+    eff = ops.dist_eff(par, kind, base)
+    for _ in range(W + 1):
+        idx, send, recv, rq = _route(ops, ops.dist_pending(eff, 0), split_t, W, group, dev)
+        if not _any(len(idx), group, dev):
+            break
+        ans = ops.dist_climb(par, kind, base, rq)
+        ops.scatter_into(eff, _a2a(ans, recv, send, group), idx)
+    else:
+        raise RuntimeError("distributed tree: effective parents did not converge")
+    # siblings: local runs of each (e, class), their records at the owner of e
+    sk, si = ops.sort_keys(ops.dist_gkey(eff, kind), 33)
+    nsc, okey, rec = ops.dist_runs(sk, si, base, kind)
+    del eff, sk, si
+    perm, counts = ops.partition(okey, split_t)
+    send = counts[:W]
+    idx = perm[:sum(send)]
+    rs = ops.gather_rows(rec, idx)
+    recv = _exchange_counts(send, group, dev)
+    rr = _a2a(rs.reshape(-1), [4 * x for x in send], [4 * x for x in recv], group).view(-1, 4)
+    fcS, fcN = ops.zeros32(n), ops.zeros32(n)
+    rk, ri = ops.sort_keys(ops.dist_rkey(rr), 64)
+    reply = ops.dist_link(rk, ri, rr, base, n, fcS, fcN)
+    ops.dist_put(rs, _a2a(reply, recv, send, group), base, nsc)
+    del rec, okey, perm, idx, rs, rr, rk, ri, reply
+    # threads: local chains by pointer jumping, pointers into earlier runs by
+    # their owners (one run nearer the root per round)
+    T = ops.dist_thr(nsc, base)
+    for _ in range(W + 1):
+        idx, send, recv, rq = _route(ops, ops.dist_pending(T, 1), split_t, W, group, dev)
+        if not _any(len(idx), group, dev):
+            break
+        ops.scatter_into(T, _a2a(ops.dist_fetch(T, base, rq), recv, send, group), idx)
+    else:
+        raise RuntimeError("distributed tree: threads did not converge")
+    return ops.dist_succ(kind, fcS, fcN, T, base)
+
+
+def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples,
+                       tree="auto"):
     W, r = dist.get_world_size(group), dist.get_rank(group)
     dev = id_key.device
     n = id_key.numel()
@@ -270,17 +449,36 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
     par = ops.scatter32(back, perm)
     del perm, rq, ans, back, oca
 
-    # 5. gather the rank-ordered arrays on the root and weave there
-    gsend = [n_own if j == root else 0 for j in range(W)]
-    grecv = [owns[j] if r == root else 0 for j in range(W)]
-    g_par = _a2a(par, gsend, grecv, group)
-    g_kd = _a2a(okd, gsend, grecv, group)
-    g_org = _a2a(oorg, gsend, grecv, group)
     mx = _all_gather_ints([local_max, dup], group, dev)
     max_ts = max(v[0] for v in mx)
     dups = 0
     for v in mx:  # an id held twice meets itself at its owner (shared.cljc:166-171)
         dups |= v[1]
+    if tree == "dist" or (tree == "auto" and W > 1):
+        # 5'. the tree rank by rank (dist.hip) when the list is in the fast
+        # path's domain; the rank-ordered successors gather on the root
+        st = 0
+        for v in _all_gather_ints([ops.dist_check(par, okd, own_base)], group, dev):
+            st |= v[0]
+        if not st and not dups:
+            succ = _tree_distributed(ops, par, okd, own_base, owns, group, dev)
+            gsend = [n_own if j == root else 0 for j in range(W)]
+            grecv = [owns[j] if r == root else 0 for j in range(W)]
+            g_succ = _a2a(succ, gsend, grecv, group)
+            g_org = _a2a(oorg, gsend, grecv, group)
+            if r != root:
+                return GiantResult(None, None, None, None, N, n_own, max_ts)
+            o = ops.weave_linked(g_succ, g_org)
+            return GiantResult(o["weave_perm"], o["visible_bits"], int(o["visible_count"][0]),
+                               int(o["status"][0]), N, n_own, max_ts)
+
+    # 5. gather the rank-ordered arrays on the root and weave there (the whole
+    # tree on one GPU; also the exact path for lists outside the domain)
+    gsend = [n_own if j == root else 0 for j in range(W)]
+    grecv = [owns[j] if r == root else 0 for j in range(W)]
+    g_par = _a2a(par, gsend, grecv, group)
+    g_kd = _a2a(okd, gsend, grecv, group)
+    g_org = _a2a(oorg, gsend, grecv, group)
     if r != root:
         return GiantResult(None, None, None, None, N, n_own, max_ts)
     o = ops.weave_ranked(g_par, g_kd, g_org)

@@ -61,3 +61,194 @@ class CpuOps:
                 "visible_bits": torch.from_numpy(bits.copy()),
                 "visible_count": torch.tensor([int(vis.sum())], dtype=torch.int32),
                 "status": torch.tensor([int(st[0])], dtype=torch.int32)}
+
+    # --- the distributed tree (numpy restatement of dist.hip) -------------------
+    PEND = RES = 0x80000000
+    NONE = 0xFFFFFFFF
+    NSC_UP = 0x80000000
+    END = 0x7FFFFFFF
+    ROOT_KEY = (1 << 33) - 1
+
+    @staticmethod
+    def _special(k):
+        return (np.asarray(k) & 3) != 0
+
+    @staticmethod
+    def _hide(k):
+        k = int(k) & 3
+        return k == 1 or k == 2   # hide, h.hide (pack.KIND_*)
+
+    @staticmethod
+    def _u32(t):
+        return t.numpy().view(np.uint32)
+
+    @staticmethod
+    def _t32(a):
+        return torch.from_numpy(np.ascontiguousarray(a, np.uint32).view(np.int32))
+
+    def dist_check(self, par, kind, base):
+        p, k = self._u32(par), kind.numpy()
+        st = 0
+        for i in range(len(p)):
+            g = base + i
+            if (g == 0) != bool(k[i] & 4):
+                st |= 1
+            if g > 0 and p[i] >= g:
+                st |= 4 if p[i] >= 0xFFFFFFFE else 8
+        return st
+
+    def _climb(self, c, p, k, base):
+        n = len(p)
+        while True:
+            if c < base or c - base >= n:
+                return self.PEND | c
+            if not self._special(k[c - base]):
+                return c
+            c = int(p[c - base])
+
+    def dist_eff(self, par, kind, base):
+        p, k = self._u32(par), kind.numpy()
+        out = np.empty(len(p), np.uint32)
+        for i in range(len(p)):
+            if base + i == 0:
+                out[i] = self.NONE
+            elif self._special(k[i]):
+                out[i] = p[i]
+            else:
+                out[i] = self._climb(int(p[i]), p, k, base)
+        return self._t32(out)
+
+    def dist_climb(self, par, kind, base, q):
+        p, k = self._u32(par), kind.numpy()
+        return self._t32([self._climb(int(x), p, k, base) for x in _u64(q)])
+
+    def dist_pending(self, w, mode):
+        x = self._u32(w).astype(np.uint64)
+        if mode == 0:
+            pend = ((x & self.PEND) != 0) & (x != self.NONE)
+        else:
+            pend = (x & self.RES) == 0
+        keys = np.where(pend, x & ~np.uint64(self.PEND), np.uint64(2**64 - 1))
+        return torch.from_numpy(keys.view(np.int64))
+
+    def dist_gkey(self, eff, kind):
+        e = self._u32(eff).astype(np.uint64)
+        cls = np.where(self._special(kind.numpy()), 0, 1).astype(np.uint64)
+        key = np.where(e == self.NONE, np.uint64(self.ROOT_KEY), (e << np.uint64(1)) | cls)
+        return torch.from_numpy(key.view(np.int64))
+
+    def dist_runs(self, skey, sidx, base, kind):
+        sk, si, k = _u64(skey), sidx.numpy().view(np.uint32), kind.numpy()
+        n = len(sk)
+        nsc = np.zeros(n, np.uint32)
+        okey = np.full(n, 2**64 - 1, np.uint64)
+        rec = np.zeros((n, 4), np.uint32)
+        for i in range(n):
+            kk = int(sk[i])
+            if kk == self.ROOT_KEY:
+                continue
+            x = int(si[i])
+            if i > 0 and sk[i - 1] == sk[i]:
+                nsc[x] = base + int(si[i - 1])
+                continue
+            j = i
+            while j + 1 < n and sk[j + 1] == sk[i]:
+                j += 1
+            newest = int(si[j])
+            nsc[x] = self.NSC_UP | (kk >> 1)
+            okey[i] = kk >> 1
+            rec[i] = (kk & 0xFFFFFFFF, base + x, base + newest, k[newest])
+        return (self._t32(nsc), torch.from_numpy(okey.view(np.int64)),
+                torch.from_numpy(rec.view(np.int32)))
+
+    def dist_rkey(self, rec):
+        r = rec.numpy().view(np.uint32).astype(np.uint64)
+        return torch.from_numpy(((r[:, 0] << np.uint64(32)) | r[:, 1]).view(np.int64))
+
+    def dist_link(self, skey, sidx, rec, base, n, fcS, fcN):
+        sk, si = _u64(skey), sidx.numpy().view(np.uint32)
+        r = rec.numpy().view(np.uint32)
+        fs, fn = fcS.numpy().view(np.uint32), fcN.numpy().view(np.uint32)
+        m = len(sk)
+        g = (sk >> np.uint64(32)).astype(np.uint64)
+        reply = np.zeros(m, np.uint32)
+        for j in range(m):
+            gj, e = int(g[j]), int(g[j]) >> 1
+            first = j == 0 or g[j - 1] != g[j]
+            last = j + 1 == m or g[j + 1] != g[j]
+            ns = self.NSC_UP | e
+            if not first:
+                ns = int(r[si[j - 1], 2])
+            elif not gj & 1:
+                hit = np.flatnonzero(g == (gj | 1))
+                if len(hit):
+                    ns = int(r[si[hit[-1]], 2])
+            reply[si[j]] = ns
+            if last and base <= e < base + n:
+                hi = int(r[si[j], 2])
+                if gj & 1:
+                    fn[e - base] = hi
+                else:
+                    fs[e - base] = hi | (0x80000000 if self._hide(r[si[j], 3]) else 0)
+        return self._t32(reply)
+
+    def dist_put(self, rec, reply, base, nsc):
+        r, rp, ns = rec.numpy().view(np.uint32), self._u32(reply), nsc.numpy().view(np.uint32)
+        for i in range(len(rp)):
+            ns[int(r[i, 1]) - base] = rp[i]
+
+    def dist_thr(self, nsc, base):
+        s = self._u32(nsc)
+        n = len(s)
+        T = np.where((s & self.NSC_UP) != 0, s & ~np.uint32(self.NSC_UP), s | np.uint32(self.RES))
+        if base == 0 and n:
+            T[0] = self.RES | self.END
+        while True:   # pointer jumping over the local pointers
+            loc = ((T & self.RES) == 0) & (T >= base) & (T < base + n)
+            if not loc.any():
+                return self._t32(T)
+            T = np.where(loc, T[np.where(loc, T - base, 0)], T)
+
+    def dist_fetch(self, src, base, q):
+        s = self._u32(src)
+        return self._t32([s[int(x) - base] for x in _u64(q)])
+
+    def dist_succ(self, kind, fcS, fcN, T, base):
+        k = kind.numpy()
+        fs, fn, t = self._u32(fcS), self._u32(fcN), self._u32(T)
+        out = np.zeros(len(t), np.uint32)
+        for i in range(len(t)):
+            f = int(fs[i]) & 0x7FFFFFFF
+            succ = f if f else (int(fn[i]) if fn[i] else int(t[i]) & 0x7FFFFFFF)
+            vis = not self._special(k[i]) and base + i != 0 and not (fs[i] and fs[i] & 0x80000000)
+            out[i] = succ | (0x80000000 if vis else 0)
+        return self._t32(out)
+
+    def gather_rows(self, rec, idx):
+        return rec[idx.long()]
+
+    def scatter_into(self, dst, src, idx):
+        dst[idx.long()] = src
+
+    def zeros32(self, n):
+        return torch.zeros(n, dtype=torch.int32)
+
+    def weave_linked(self, succ, val):
+        """The list ranking by walking the successors from the root (rank 0)."""
+        s = self._u32(succ)
+        n = len(s)
+        order, vis = np.empty(n, np.int64), np.zeros(n, np.uint8)
+        x, g = 0, 0
+        while x < n and g < n:
+            order[g] = x
+            vis[g] = 1 if s[x] & 0x80000000 else 0
+            x = int(s[x]) & 0x7FFFFFFF
+            g += 1
+        st = 0 if g == n else 32   # CW_STATUS_INTERNAL
+        wp = val.numpy()[order[:g]] if g == n else np.zeros(n, np.int32)
+        bits = np.packbits(vis, bitorder="little")
+        bits = np.pad(bits, (0, (-len(bits)) % 4)).view(np.int32)
+        return {"weave_perm": torch.from_numpy(np.ascontiguousarray(wp).astype(np.int32)),
+                "visible_bits": torch.from_numpy(bits.copy()),
+                "visible_count": torch.tensor([int(vis.sum())], dtype=torch.int32),
+                "status": torch.tensor([st], dtype=torch.int32)}

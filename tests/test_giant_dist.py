@@ -40,7 +40,7 @@ def shares(N, W, seed, empty_rank=None):
     return [rng.permutation(np.flatnonzero(owner == r)) for r in range(W)]
 
 
-def _worker(rank, world, port, n, seed, samples, empty_rank, q):
+def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,7 +53,7 @@ def _worker(rank, world, port, n, seed, samples, empty_rank, q):
         lay = spec.layout()
         res = giant.weave_distributed(CpuOps(), t(idk[sh]), t(ck[sh]),
                                       torch.from_numpy(kd[sh].copy()), lay.key_bits,
-                                      ts_shift=lay.ts_shift, samples=samples)
+                                      ts_shift=lay.ts_shift, samples=samples, tree=tree)
         if rank == 0:
             q.put((res.weave_perm.numpy().copy(), res.visible_count, res.status, res.n_total,
                    res.max_ts))
@@ -62,11 +62,11 @@ def _worker(rank, world, port, n, seed, samples, empty_rank, q):
         dist.destroy_process_group()
 
 
-def run(world, n, seed, samples=64, empty_rank=None):
+def run(world, n, seed, samples=64, empty_rank=None, tree="auto"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, n, seed, samples, empty_rank, q))
+    ps = [ctx.Process(target=_worker, args=(r, world, port, n, seed, samples, empty_rank, tree, q))
           for r in range(world)]
     for p in ps:
         p.start()
@@ -83,10 +83,13 @@ def run(world, n, seed, samples=64, empty_rank=None):
     return got, owned
 
 
+@pytest.mark.parametrize("tree", ["dist", "root"])
 @pytest.mark.parametrize("world,n,seed,empty", [(2, 3000, 11, None), (3, 5000, 12, None),
                                                 (4, 2000, 13, 2)])
-def test_distributed_weave_matches_oracle(world, n, seed, empty):
-    (wp, vcount, status, N, max_ts), owned = run(world, n, seed, empty_rank=empty)
+def test_distributed_weave_matches_oracle(world, n, seed, empty, tree):
+    """tree="dist": effective parents, sibling runs and threads rank by rank
+    (dist.hip's numpy double); "root": the whole tree on rank 0."""
+    (wp, vcount, status, N, max_ts), owned = run(world, n, seed, empty_rank=empty, tree=tree)
     spec, idk, ck, kd = make_list(n, seed)
     assert N == len(idk) and sum(owned.values()) == N
     perm, vis, st = oracle.batch_lists(np.array([0, N], np.uint64), idk, ck, kd,

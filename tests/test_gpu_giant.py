@@ -162,7 +162,109 @@ def _free_port():
     return p
 
 
-def test_distributed_one_rank_in_process(ops):
+def _dist_inputs(n, seed, lo, hi):
+    """The run [lo, hi) of a ranked list: (par, kind) of those ranks."""
+    par, kd, val = ranked_case(n, seed)
+    return par[lo:hi].copy(), kd[lo:hi].copy(), par, kd, val
+
+
+def _same(a, b):
+    a = a.cpu().numpy() if hasattr(a, "cpu") else np.asarray(a)
+    b = b.cpu().numpy() if hasattr(b, "cpu") else np.asarray(b)
+    if a.shape != b.shape:
+        print("shapes", a.shape, b.shape)
+        return False
+    bad = np.flatnonzero((a != b).reshape(len(a), -1).any(axis=1)) if a.size else []
+    if len(bad):
+        print("differ at", bad[:5], a[bad[:5]], b[bad[:5]], "of", len(bad))
+    return len(bad) == 0
+
+
+@pytest.mark.parametrize("n,seed,lo,hi", [(30_000, 41, 0, 30_000), (30_000, 42, 9_000, 21_000),
+                                          (5_000, 43, 4_000, 5_000)])
+def test_dist_ops_match_the_double(ops, n, seed, lo, hi):
+    """Every building block of the distributed tree (dist.hip) against its numpy
+    restatement (tests/giant_cpu_ops.py) on one rank's run of a list."""
+    import torch
+
+    cpu = CpuOps()
+    par, kd, fpar, fkd, _ = _dist_inputs(n, seed, lo, hi)
+    T = torch.from_numpy
+    assert ops.dist_check(_t(par), _t(kd), lo) == cpu.dist_check(T(par), T(kd), lo) == 0
+    eff = ops.dist_eff(_t(par), _t(kd), lo)
+    ceff = cpu.dist_eff(T(par), T(kd), lo)
+    assert _same(eff, ceff)
+    rng = np.random.default_rng(seed)
+    q = rng.integers(lo, hi, 5000).astype(np.int64)
+    assert _same(ops.dist_climb(_t(par), _t(kd), lo, _t(q)), cpu.dist_climb(T(par), T(kd), lo, T(q)))
+    for mode in (0, 1):
+        assert _same(ops.dist_pending(eff, mode), cpu.dist_pending(ceff, mode))
+    # effective parents of the whole list from the full run: the group keys,
+    # runs, records and links of a one-rank tree
+    feff = cpu.dist_eff(T(fpar), T(fkd), 0)
+    gk = cpu.dist_gkey(feff, T(fkd))
+    assert _same(ops.dist_gkey(_t(feff.numpy()), _t(fkd)), gk)
+    sk, si = cpu.sort_keys(gk, 33)
+    nsc, okey, rec = ops.dist_runs(_t(sk.numpy()), _t(si.numpy()), 0, _t(fkd))
+    cnsc, cokey, crec = cpu.dist_runs(sk, si, 0, T(fkd))
+    assert _same(nsc, cnsc) and _same(okey, cokey)
+    heads = torch.from_numpy(cokey.numpy() != -1)
+    assert _same(rec.cpu()[heads], crec[heads])
+    rs = crec[heads].contiguous()
+    rkey = ops.dist_rkey(_t(rs.numpy()))
+    assert _same(rkey, cpu.dist_rkey(rs))
+    rk, ri = cpu.sort_keys(rkey.cpu(), 64)
+    n = len(fpar)   # (the list has a root besides its n generated nodes)
+    fs, fn = ops.zeros32(n), ops.zeros32(n)
+    cfs, cfn = cpu.zeros32(n), cpu.zeros32(n)
+    reply = ops.dist_link(_t(rk.numpy()), _t(ri.numpy()), _t(rs.numpy()), 0, n, fs, fn)
+    creply = cpu.dist_link(rk, ri, rs, 0, n, cfs, cfn)
+    assert _same(reply, creply) and _same(fs, cfs) and _same(fn, cfn)
+    ops.dist_put(_t(rs.numpy()), reply, 0, nsc)
+    cpu.dist_put(rs, creply, 0, cnsc)
+    assert _same(nsc, cnsc)
+    thr = ops.dist_thr(nsc, 0)
+    cthr = cpu.dist_thr(cnsc, 0)
+    assert _same(thr, cthr)
+    q2 = rng.integers(0, n, 3000).astype(np.int64)
+    assert _same(ops.dist_fetch(thr, 0, _t(q2)), cpu.dist_fetch(cthr, 0, T(q2)))
+    succ = ops.dist_succ(_t(fkd), fs, fn, thr, 0)
+    csucc = cpu.dist_succ(T(fkd), cfs, cfn, cthr, 0)
+    assert _same(succ, csucc)
+
+
+@pytest.mark.parametrize("n,seed", [(1, 1), (50, 2), (20_000, 3), (600_000, 4)])
+def test_weave_linked_equals_weave_ranked(ops, n, seed):
+    """cw_weave_linked on the successors of the one-rank distributed tree gives
+    cw_weave_ranked's weave of the same list."""
+    import torch
+
+    cpu = CpuOps()
+    par, kd, val = ranked_case(n, seed)
+    n = len(par)
+    T = torch.from_numpy
+    eff = ops.dist_eff(_t(par), _t(kd), 0)
+    sk, si = ops.sort_keys(ops.dist_gkey(eff, _t(kd)), 33)
+    nsc, okey, rec = ops.dist_runs(sk, si, 0, _t(kd))
+    heads = okey.cpu().numpy() != -1
+    rs = _t(rec.cpu().numpy()[heads])
+    rk, ri = ops.sort_keys(ops.dist_rkey(rs), 64)
+    fs, fn = ops.zeros32(n), ops.zeros32(n)
+    reply = ops.dist_link(rk, ri, rs, 0, n, fs, fn)
+    ops.dist_put(rs, reply, 0, nsc)
+    succ = ops.dist_succ(_t(kd), fs, fn, ops.dist_thr(nsc, 0), 0)
+    got = ops.weave_linked(succ, _t(val))
+    want = ops.weave_ranked(_t(par), _t(kd), _t(val))
+    ref = cpu.weave_linked(succ.cpu(), T(val))
+    assert int(got["status"][0]) == 0 == int(want["status"][0])
+    for k in ("weave_perm", "visible_count"):
+        assert _same(got[k], want[k]) and _same(got[k], ref[k]), k
+    nb = (n + 31) // 32
+    assert _same(got["visible_bits"][:nb], want["visible_bits"][:nb])
+
+
+@pytest.mark.parametrize("tree", ["root", "dist"])
+def test_distributed_one_rank_in_process(ops, tree):
     import torch
     import torch.distributed as dist
 
@@ -176,7 +278,7 @@ def test_distributed_one_rank_in_process(ops):
     try:
         lay = spec.layout()
         res = giant.weave_distributed(ops, _t(_i64(idk[sh])), _t(_i64(ck[sh])), _t(kd[sh]),
-                                      lay.key_bits, ts_shift=lay.ts_shift)
+                                      lay.key_bits, ts_shift=lay.ts_shift, tree=tree)
     finally:
         dist.destroy_process_group()
     perm, vis, st = oracle.batch_lists(np.array([0, len(idk)], np.uint64), idk, ck, kd,
