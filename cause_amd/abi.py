@@ -96,16 +96,16 @@ class CwRankedList(C.Structure):
 
 
 class CwLinkedList(C.Structure):
-    _fields_ = [("n", C.c_uint64), ("succ", C.c_void_p), ("val", C.c_void_p)]
+    _fields_ = [("n", C.c_uint64), ("succ", C.c_void_p), ("thr", C.c_void_p), ("val", C.c_void_p)]
 
 
 # the distributed tree's building blocks (include/causeweave.h, dist.hip):
 # argument types after the context
 _DIST_ARGS = {
     "check": "U64 U32 P P P", "eff": "U64 U32 P P P", "climb": "U64 U32 P P P U64 P",
-    "pending": "P U64 U32 P", "gkey": "P P U64 P", "runs": "P P U64 U32 P P P P",
+    "pending": "P U64 P P", "gkey": "P P U64 P", "runs": "P P U64 U32 P P P P",
     "rkey": "P U64 P", "link": "P P U64 P U32 U64 P P P", "put": "P P U64 U32 U64 P",
-    "thr": "P U64 U32 P", "fetch": "P U32 U64 P U64 P", "succ": "P P P P U64 U32 P",
+    "thr": "P U64 U32 P", "succ": "P P P U64 U32 P",
 }
 
 
@@ -173,6 +173,8 @@ def lib():
         L.cw_scatter32.argtypes = [P, P, P, U64, P]
         L.cw_weave_ranked.argtypes = [P, C.POINTER(CwRankedList), C.POINTER(CwListResult)]
         L.cw_weave_linked.argtypes = [P, C.POINTER(CwLinkedList), C.POINTER(CwListResult)]
+        L.cw_sort_keys32.argtypes = [P, P, U64, U32, P, P]
+        L.cw_sort_keys32.restype = C.c_int
         for f in ("cw_sort_keys", "cw_lookup_keys", "cw_partition_keys", "cw_gather", "cw_scatter32",
                   "cw_weave_ranked", "cw_weave_linked"):
             getattr(L, f).restype = C.c_int
@@ -449,14 +451,18 @@ class Weaver:
                          None)
         self._check(self._L.cw_weave_ranked(self._h, C.byref(lst), C.byref(r)), "cw_weave_ranked")
 
+    def sort_keys32_device(self, keys_ptr, n, key_bits, keys_out_ptr, idx_out_ptr):
+        self._check(self._L.cw_sort_keys32(self._h, keys_ptr, n, key_bits, keys_out_ptr,
+                                           idx_out_ptr), "cw_sort_keys32")
+
     def dist(self, name, *args):
         """cw_dist_<name>(ctx, *args): a building block of the distributed tree
         (device pointers as ints, sizes, bases)."""
         self._check(getattr(self._L, "cw_dist_" + name)(self._h, *args), "cw_dist_" + name)
 
-    def weave_linked_device(self, n, succ_ptr, val_ptr, out_ptrs):
+    def weave_linked_device(self, n, succ_ptr, thr_ptr, val_ptr, out_ptrs):
         """cw_weave_linked: out_ptrs as weave_ranked_device."""
-        lst = CwLinkedList(n, succ_ptr, val_ptr)
+        lst = CwLinkedList(n, succ_ptr, thr_ptr, val_ptr)
         g = lambda k: C.c_void_p(out_ptrs[k]) if out_ptrs.get(k) else None
         r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), None, g("status"),
                          None)

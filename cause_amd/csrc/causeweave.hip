@@ -4047,6 +4047,30 @@ int sort_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t n64, uint32_t key_b
   return 0;
 }
 
+// The same for 32-bit keys (the distributed tree's group keys).
+int sort_keys32_impl(cw_ctx *c, const uint32_t *keys, uint64_t n64, uint32_t key_bits,
+                     uint32_t *keys_out, uint32_t *idx_out) {
+  if (n64 == 0) return 0;
+  if (!keys || !keys_out || !idx_out) return fail(c, "null array");
+  if (n64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)n64);
+  const uint32_t n = (uint32_t)n64;
+  HIPCHK(c, hipSetDevice(c->device));
+  const uint64_t off[2] = {0, n64};
+  if (ensure_tables(c, 1, off)) return -1;
+  if (key_bits == 0 || key_bits > 32) key_bits = 32;
+  uint32_t *kB = scratch_t<uint32_t>(c, "k32_kB", n), *vB = scratch_t<uint32_t>(c, "k32_vB", n);
+  if (!kB || !vB) return fail(c, "out of device memory (sort)");
+  uint32_t *ko, *vo;
+  if (radix_sort<uint32_t>(c, "ksort32", keys, nullptr, keys_out, idx_out, kB, vB, key_bits, 0, n,
+                           &ko, &vo))
+    return -1;
+  if (ko != keys_out) {
+    HIPCHK(c, hipMemcpyAsync(keys_out, ko, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(idx_out, vo, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  return 0;
+}
+
 int lookup_keys_impl(cw_ctx *c, const uint64_t *sorted, uint64_t n64, const uint64_t *q,
                      uint64_t m, uint32_t base, uint32_t *out, uint32_t *status) {
   if (m == 0 && (!status || n64 == 0)) return 0;
@@ -4884,6 +4908,10 @@ int cw_weave_ranked(cw_ctx *c, const cw_ranked_list *l, cw_list_result *r) {
   if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream)); \
   return c->prof ? collect_prof(c) : 0;
 
+int cw_sort_keys32(cw_ctx *c, const uint32_t *keys, uint64_t n, uint32_t key_bits,
+                   uint32_t *keys_out, uint32_t *idx_out) {
+  CW_DIST_ENTRY(sort_keys32_impl(c, keys, n, key_bits, keys_out, idx_out))
+}
 int cw_dist_check(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
                   uint32_t *status) {
   CW_DIST_ENTRY(dist_check_impl(c, n, base, par, kind, status))
@@ -4896,20 +4924,20 @@ int cw_dist_climb(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, con
                   const uint64_t *q, uint64_t m, uint32_t *out) {
   CW_DIST_ENTRY(dist_climb_impl(c, n, base, par, kind, q, m, out))
 }
-int cw_dist_pending(cw_ctx *c, const uint32_t *w, uint64_t n, uint32_t mode, uint64_t *keys) {
-  CW_DIST_ENTRY(dist_pending_impl(c, w, n, mode, keys))
+int cw_dist_pending(cw_ctx *c, const uint32_t *w, uint64_t n, uint64_t *keys, uint32_t *count) {
+  CW_DIST_ENTRY(dist_pending_impl(c, w, n, keys, count))
 }
-int cw_dist_gkey(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint64_t *key) {
+int cw_dist_gkey(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint32_t *key) {
   CW_DIST_ENTRY(dist_gkey_impl(c, eff, kind, n, key))
 }
-int cw_dist_runs(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
+int cw_dist_runs(cw_ctx *c, const uint32_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
                  const uint8_t *kind, uint32_t *nsc, uint64_t *okey, uint32_t *rec) {
   CW_DIST_ENTRY(dist_runs_impl(c, skey, sidx, n, base, kind, nsc, okey, rec))
 }
-int cw_dist_rkey(cw_ctx *c, const uint32_t *rec, uint64_t m, uint64_t *key) {
+int cw_dist_rkey(cw_ctx *c, const uint32_t *rec, uint64_t m, uint32_t *key) {
   CW_DIST_ENTRY(dist_rkey_impl(c, rec, m, key))
 }
-int cw_dist_link(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t m,
+int cw_dist_link(cw_ctx *c, const uint32_t *skey, const uint32_t *sidx, uint64_t m,
                  const uint32_t *rec, uint32_t base, uint64_t n, uint32_t *fcS, uint32_t *fcN,
                  uint32_t *reply) {
   CW_DIST_ENTRY(dist_link_impl(c, skey, sidx, m, rec, base, n, fcS, fcN, reply))
@@ -4921,13 +4949,9 @@ int cw_dist_put(cw_ctx *c, const uint32_t *rec, const uint32_t *reply, uint64_t 
 int cw_dist_thr(cw_ctx *c, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *T) {
   CW_DIST_ENTRY(dist_thr_impl(c, nsc, n, base, T))
 }
-int cw_dist_fetch(cw_ctx *c, const uint32_t *src, uint32_t base, uint64_t n, const uint64_t *q,
-                  uint64_t m, uint32_t *out) {
-  CW_DIST_ENTRY(dist_fetch_impl(c, src, base, n, q, m, out))
-}
 int cw_dist_succ(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
-                 const uint32_t *T, uint64_t n, uint32_t base, uint32_t *out) {
-  CW_DIST_ENTRY(dist_succ_impl(c, kind, fcS, fcN, T, n, base, out))
+                 uint64_t n, uint32_t base, uint32_t *out) {
+  CW_DIST_ENTRY(dist_succ_impl(c, kind, fcS, fcN, n, base, out))
 }
 #undef CW_DIST_ENTRY
 

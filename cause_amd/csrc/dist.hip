@@ -21,19 +21,21 @@
 //     next run's oldest, and the oldest special's next sibling is e's newest
 //     non-special.  The answers go back (cw_dist_put).
 //   threads: thr(x) = next sibling of x, else thr(e(x)) -- the preorder
-//     successor of a node without children.  cw_dist_thr resolves the local
-//     chains by pointer jumping; pointers into earlier ranks are answered by
-//     their owners (cw_dist_fetch), at most W - 1 rounds since a thread
-//     pointer only moves to a smaller rank.
+//     successor of a node without children.  cw_dist_thr resolves the chains
+//     inside each 1,024-rank tile by pointer jumping in LDS (as k_gthr); a
+//     chain that leaves the tile keeps THRW_PEND | the ancestor, and the walk
+//     on the gathering GPU chases it through the gathered thread words (as
+//     the single-GPU giant path does) -- no exchange rounds.
 //
-// cw_dist_succ then gives every node its successor (first child, else thread)
-// and render bit, and the list ranking runs on one GPU (cw_weave_linked).
+// cw_dist_succ then gives every node its successor (first child, or
+// DIST_FROM_THR: its thread) and render bit, and the list ranking runs on one
+// GPU (cw_weave_linked).
 
 constexpr uint32_t DIST_PEND = 0x80000000u;  // eff: climb goes on at the rank in the low bits
 constexpr uint32_t DIST_NONE = 0xFFFFFFFFu;  // eff of the root
-constexpr uint32_t DIST_RES = 0x80000000u;   // thread word: resolved (low bits: the successor)
+constexpr uint32_t DIST_FROM_THR = 0x7FFFFFFEu;  // successor word: the node's thread
 constexpr uint32_t FCS_HIDE = 0x80000000u;   // fcS word: the newest special child is a hide
-constexpr uint64_t DIST_ROOT_KEY = (1ull << 33) - 1;  // group key of the root: sorts last (33 bits)
+constexpr uint32_t DIST_ROOT_KEY = 0xFFFFFFFFu;  // group key of the root: sorts last
 
 __global__ __launch_bounds__(256) void k_dist_check(const uint32_t *__restrict__ par,
                                                     const uint8_t *__restrict__ kind, uint32_t n,
@@ -86,34 +88,38 @@ __global__ __launch_bounds__(256) void k_dist_climb(const uint32_t *__restrict__
   if (i < m) out[i] = dist_climb((uint32_t)q[i], par, kind, n, base);
 }
 
-// Partition keys of the words still waiting on another rank (UINT64_MAX: none).
-// mode 0: eff words (DIST_PEND | rank); mode 1: thread words (a rank without DIST_RES).
+// Partition keys of the eff words still waiting on another rank (UINT64_MAX:
+// none), and their number.
 __global__ __launch_bounds__(256) void k_dist_pending(const uint32_t *__restrict__ w, uint32_t n,
-                                                      uint32_t mode, uint64_t *__restrict__ keys) {
+                                                      uint64_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ count) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t x = w[i];
-  bool pend;
-  if (mode == 0) pend = (x & DIST_PEND) && x != DIST_NONE;
-  else pend = !(x & DIST_RES);
-  keys[i] = pend ? (uint64_t)(x & ~DIST_PEND) : ~0ull;
+  bool pend = false;
+  if (i < n) {
+    const uint32_t x = w[i];
+    pend = (x & DIST_PEND) && x != DIST_NONE;
+    keys[i] = pend ? (uint64_t)(x & ~DIST_PEND) : ~0ull;
+  }
+  const uint64_t b = __ballot(pend);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (uint32_t)__popcll(b));
 }
 
-// Group keys (e << 1 | class; special = 0; 33 bits) for the local sort; the root last.
+// Group keys (e << 1 | class; special = 0; e < 2^31 - 1) for the local sort;
+// the root last.
 __global__ __launch_bounds__(256) void k_dist_gkey(const uint32_t *__restrict__ eff,
                                                    const uint8_t *__restrict__ kind, uint32_t n,
-                                                   uint64_t *__restrict__ key) {
+                                                   uint32_t *__restrict__ key) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t e = eff[i];
-  key[i] = e == DIST_NONE ? DIST_ROOT_KEY : (((uint64_t)e << 1) | (is_special(kind[i]) ? 0u : 1u));
+  key[i] = e == DIST_NONE ? DIST_ROOT_KEY : ((e << 1) | (is_special(kind[i]) ? 0u : 1u));
 }
 
 // Runs of equal group keys in the locally sorted order: inside a run each node's
 // next sibling is the next older node; a run's oldest node waits for the owner
 // of e (record: group, oldest, newest, kind of the newest; key = e for the
 // partition by owner, UINT64_MAX on the other positions).
-__global__ __launch_bounds__(256) void k_dist_runs(const uint64_t *__restrict__ skey,
+__global__ __launch_bounds__(256) void k_dist_runs(const uint32_t *__restrict__ skey,
                                                    const uint32_t *__restrict__ sidx, uint32_t n,
                                                    uint32_t base, const uint8_t *__restrict__ kind,
                                                    uint32_t *__restrict__ nsc,
@@ -121,7 +127,7 @@ __global__ __launch_bounds__(256) void k_dist_runs(const uint64_t *__restrict__ 
                                                    uint4 *__restrict__ rec) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t k = skey[i];
+  const uint32_t k = skey[i];
   okey[i] = ~0ull;
   const uint32_t x = sidx[i];
   if (k == DIST_ROOT_KEY) {  // the root: no siblings
@@ -132,25 +138,35 @@ __global__ __launch_bounds__(256) void k_dist_runs(const uint64_t *__restrict__ 
     nsc[x] = base + sidx[i - 1];
     return;
   }
-  uint32_t lo = i, hi = n;  // the run's end: first position with a larger key
+  // the run's end (first position with a larger key): runs are short, so
+  // gallop from here, then bisect
+  uint32_t lo = i + 1, step = 1;
+  while (lo < n && skey[lo] == k) {
+    lo = i + 1 + step;
+    step <<= 1;
+  }
+  uint32_t hi = min(lo, n);
+  lo = i + 1 + (step >> 2);
+  if (lo > hi) lo = hi;
   while (lo < hi) {
     const uint32_t mid = lo + ((hi - lo) >> 1);
     if (skey[mid] <= k) lo = mid + 1; else hi = mid;
   }
   const uint32_t newest = sidx[lo - 1];
-  nsc[x] = NSC_UP | (uint32_t)(k >> 1);  // placeholder until the owner answers
+  nsc[x] = NSC_UP | (k >> 1);  // placeholder until the owner answers
   okey[i] = k >> 1;
-  rec[i] = make_uint4((uint32_t)k, base + x, base + newest, kind[newest]);
+  rec[i] = make_uint4(k, base + x, base + newest, kind[newest]);
 }
 
-// At the owner of e: the runs of every group sorted by (group, oldest).
+// At the owner of e: a stable sort by group of the records as received (in
+// sender order, i.e. by rank run) orders every group's runs by their oldest.
 __global__ __launch_bounds__(256) void k_dist_rkey(const uint4 *__restrict__ rec, uint32_t m,
-                                                   uint64_t *__restrict__ key) {
+                                                   uint32_t *__restrict__ key) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < m) key[i] = ((uint64_t)rec[i].x << 32) | rec[i].y;
+  if (i < m) key[i] = rec[i].x;
 }
 
-__global__ __launch_bounds__(256) void k_dist_link(const uint64_t *__restrict__ skey,
+__global__ __launch_bounds__(256) void k_dist_link(const uint32_t *__restrict__ skey,
                                                    const uint32_t *__restrict__ sidx, uint32_t m,
                                                    const uint4 *__restrict__ rec, uint32_t base,
                                                    uint32_t n, uint32_t *__restrict__ fcS,
@@ -158,10 +174,10 @@ __global__ __launch_bounds__(256) void k_dist_link(const uint64_t *__restrict__ 
                                                    uint32_t *__restrict__ reply) {
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= m) return;
-  const uint32_t g = (uint32_t)(skey[j] >> 32), e = g >> 1;
+  const uint32_t g = skey[j], e = g >> 1;
   const uint4 r = rec[sidx[j]];
-  const bool first = j == 0 || (uint32_t)(skey[j - 1] >> 32) != g;
-  const bool last = j + 1 == m || (uint32_t)(skey[j + 1] >> 32) != g;
+  const bool first = j == 0 || skey[j - 1] != g;
+  const bool last = j + 1 == m || skey[j + 1] != g;
   uint32_t ns = NSC_UP | e;
   if (!first) {
     ns = rec[sidx[j - 1]].z;
@@ -170,9 +186,9 @@ __global__ __launch_bounds__(256) void k_dist_link(const uint64_t *__restrict__ 
     uint32_t lo = j, hi = m;
     while (lo < hi) {
       const uint32_t mid = lo + ((hi - lo) >> 1);
-      if ((skey[mid] >> 32) < want) lo = mid + 1; else hi = mid;
+      if (skey[mid] < want) lo = mid + 1; else hi = mid;
     }
-    if (lo > 0 && (uint32_t)(skey[lo - 1] >> 32) == (g | 1u)) ns = rec[sidx[lo - 1]].z;
+    if (lo > 0 && skey[lo - 1] == (g | 1u)) ns = rec[sidx[lo - 1]].z;
   }
   reply[sidx[j]] = ns;
   if (last && e >= base && e - base < n) {
@@ -191,68 +207,89 @@ __global__ __launch_bounds__(256) void k_dist_put(const uint4 *__restrict__ rec,
   if (x < n) nsc[x] = reply[i];
 }
 
-__global__ __launch_bounds__(256) void k_dist_thr_init(const uint32_t *__restrict__ nsc, uint32_t n,
-                                                       uint32_t base, uint32_t *__restrict__ T) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t s = nsc[i];
-  T[i] = base + i == 0 ? (DIST_RES | SUCCW_END) : (s & NSC_UP) ? (s & ~NSC_UP) : (DIST_RES | s);
-}
-
-// One round of pointer jumping over the pointers into this rank's run.
-__global__ __launch_bounds__(256) void k_dist_jump(uint32_t *T, uint32_t n, uint32_t base,
-                                                   uint32_t *open) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool o = false;
-  if (i < n) {
-    const uint32_t a = T[i];
-    if (!(a & DIST_RES) && a >= base && a - base < n) {
-      const uint32_t b = T[a - base];
-      T[i] = b;
-      o = !(b & DIST_RES) && b >= base && b - base < n;
+// Thread words of one 1,024-rank tile of the run: resolved successor, or
+// THRW_PEND | an ancestor outside the tile (chased by the walk); pointer
+// jumping in LDS as k_gthr (pointers go to lower ranks).
+template <int NT, int TT>
+__global__ __launch_bounds__(NT) void k_dist_thr(const uint32_t *__restrict__ nsc, uint32_t n,
+                                                 uint32_t base, uint32_t *__restrict__ thr) {
+  constexpr uint32_t IT = TT / NT;
+  constexpr uint64_t RES = 1ull << 63, OUT = 1ull << 62;
+  __shared__ uint64_t T[TT];
+  const uint32_t r0 = blockIdx.x * TT, tid = threadIdx.x, len = min((uint32_t)TT, n - r0);
+  const uint32_t g0 = base + r0;
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = k * NT + tid;
+    if (j >= len) continue;
+    const uint32_t s = nsc[r0 + j], g = g0 + j;
+    uint64_t tv;
+    if (g == 0) tv = RES | SUCCW_END;
+    else if (!(s & NSC_UP)) tv = RES | s;
+    else {
+      const uint32_t e = s & ~NSC_UP;
+      tv = e >= g0 ? (e < g ? (uint64_t)(e - g0) : (RES | SUCCW_END)) : (OUT | e);
     }
+    T[j] = tv;
   }
-  if (__syncthreads_or(o)) {
-    if (threadIdx.x == 0) atomicOr(open, 1u);
+  __syncthreads();
+  for (;;) {
+    bool open = false;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid;
+      if (j < len) {
+        const uint64_t a = T[j];
+        if (!(a & (RES | OUT))) {
+          const uint64_t b = T[(uint32_t)a];
+          T[j] = b;
+          open |= !(b & (RES | OUT));
+        }
+      }
+    }
+    if (!__syncthreads_or(open)) break;
   }
-}
-
-__global__ __launch_bounds__(256) void k_dist_fetch(const uint32_t *__restrict__ src, uint32_t base,
-                                                    uint32_t n, const uint64_t *__restrict__ q,
-                                                    uint32_t m, uint32_t *__restrict__ out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= m) return;
-  const uint64_t x = q[i] - base;
-  out[i] = x < n ? src[x] : (DIST_RES | SUCCW_END);
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = k * NT + tid;
+    if (j >= len) continue;
+    const uint64_t a = T[j];
+    thr[r0 + j] = (a & RES) ? (uint32_t)a : (THRW_PEND | (uint32_t)a);
+  }
 }
 
 // Successor (first child -- the newest special, else the newest non-special --
 // else the thread) and render bit of every node of the run.
 __global__ __launch_bounds__(256) void k_dist_succ(const uint8_t *__restrict__ kind,
                                                    const uint32_t *__restrict__ fcS,
-                                                   const uint32_t *__restrict__ fcN,
-                                                   const uint32_t *__restrict__ T, uint32_t n,
+                                                   const uint32_t *__restrict__ fcN, uint32_t n,
                                                    uint32_t base, uint32_t *__restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint32_t fs = fcS[i], fn = fcN[i];
-  const uint32_t t = T[i];
-  const uint32_t succ = (fs & ~FCS_HIDE) ? (fs & ~FCS_HIDE) : fn ? fn : (t & ~DIST_RES);
+  const uint32_t succ = (fs & ~FCS_HIDE) ? (fs & ~FCS_HIDE) : fn ? fn : DIST_FROM_THR;
   const bool vis = !is_special(kind[i]) && base + i != 0 && !(fs && (fs & FCS_HIDE));
   out[i] = succ | (vis ? LINK_VIS : 0u);
 }
 
-// cw_weave_linked: link words for the giant walk from successor | render bit.
-__global__ __launch_bounds__(256) void k_linked_words(const uint32_t *__restrict__ sv, uint32_t n,
+// cw_weave_linked: link words for the giant walk from successor | render bit
+// and the thread words (a successor that is a pending thread: LINK_PEND, the
+// walk chases it through thr).
+__global__ __launch_bounds__(256) void k_linked_words(const uint32_t *__restrict__ sv,
+                                                      const uint32_t *__restrict__ th, uint32_t n,
                                                       uint32_t log2k, uint64_t *__restrict__ link,
                                                       uint32_t *__restrict__ thr) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
-  const uint32_t w = sv[r], succ = w & ~LINK_VIS;
-  const bool split = r == split_node(0, r >> log2k, log2k, n);
-  const uint32_t f = (w & LINK_VIS) | (split ? LINK_SPLIT : 0u);
+  const uint32_t w = sv[r], t = th[r];
+  uint32_t succ = w & ~LINK_VIS, f = w & LINK_VIS;
+  if (succ == DIST_FROM_THR) {
+    succ = t & ~THRW_PEND;
+    if (t & THRW_PEND) f |= LINK_PEND;
+  }
+  if (r == split_node(0, r >> log2k, log2k, n)) f |= LINK_SPLIT;
   link[r] = (uint64_t)(succ < n ? succ : SUCCW_END) | ((uint64_t)f << 32);
-  thr[r] = succ < n ? succ : SUCCW_END;
+  thr[r] = (t & THRW_PEND) ? t : (t < n ? t : SUCCW_END);
 }
 
 int dist_launch_ok(cw_ctx *c, const char *nm) { return check_launch(c, nm); }
@@ -281,19 +318,20 @@ int dist_climb_impl(cw_ctx *c, uint64_t n, uint32_t base, const uint32_t *par, c
   return dist_launch_ok(c, "dist_climb");
 }
 
-int dist_pending_impl(cw_ctx *c, const uint32_t *w, uint64_t n, uint32_t mode, uint64_t *keys) {
+int dist_pending_impl(cw_ctx *c, const uint32_t *w, uint64_t n, uint64_t *keys, uint32_t *count) {
+  HIPCHK(c, hipMemsetAsync(count, 0, 4, c->stream));
   if (!n) return 0;
-  hipLaunchKernelGGL(k_dist_pending, DIST_GRID(n), w, (uint32_t)n, mode, keys);
+  hipLaunchKernelGGL(k_dist_pending, DIST_GRID(n), w, (uint32_t)n, keys, count);
   return dist_launch_ok(c, "dist_pending");
 }
 
-int dist_gkey_impl(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint64_t *key) {
+int dist_gkey_impl(cw_ctx *c, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint32_t *key) {
   if (!n) return 0;
   hipLaunchKernelGGL(k_dist_gkey, DIST_GRID(n), eff, kind, (uint32_t)n, key);
   return dist_launch_ok(c, "dist_gkey");
 }
 
-int dist_runs_impl(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
+int dist_runs_impl(cw_ctx *c, const uint32_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
                    const uint8_t *kind, uint32_t *nsc, uint64_t *okey, uint32_t *rec) {
   if (!n) return 0;
   Launch L(c, "dist_runs", (double)n * (8 + 4 + 4 + 8) + (double)n * 0.4 * 16);
@@ -302,13 +340,13 @@ int dist_runs_impl(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64
   return dist_launch_ok(c, "dist_runs");
 }
 
-int dist_rkey_impl(cw_ctx *c, const uint32_t *rec, uint64_t m, uint64_t *key) {
+int dist_rkey_impl(cw_ctx *c, const uint32_t *rec, uint64_t m, uint32_t *key) {
   if (!m) return 0;
   hipLaunchKernelGGL(k_dist_rkey, DIST_GRID(m), reinterpret_cast<const uint4 *>(rec), (uint32_t)m, key);
   return dist_launch_ok(c, "dist_rkey");
 }
 
-int dist_link_impl(cw_ctx *c, const uint64_t *skey, const uint32_t *sidx, uint64_t m,
+int dist_link_impl(cw_ctx *c, const uint32_t *skey, const uint32_t *sidx, uint64_t m,
                    const uint32_t *rec, uint32_t base, uint64_t n, uint32_t *fcS, uint32_t *fcN,
                    uint32_t *reply) {
   if (!m) return 0;
@@ -326,39 +364,19 @@ int dist_put_impl(cw_ctx *c, const uint32_t *rec, const uint32_t *reply, uint64_
   return dist_launch_ok(c, "dist_put");
 }
 
-// Thread words with every pointer into the local run resolved (pointer
-// jumping, one readback per round: O(log depth) rounds).
-int dist_thr_impl(cw_ctx *c, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *T) {
+int dist_thr_impl(cw_ctx *c, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *thr) {
   if (!n) return 0;
-  hipLaunchKernelGGL(k_dist_thr_init, DIST_GRID(n), nsc, (uint32_t)n, base, T);
-  if (dist_launch_ok(c, "dist_thr")) return -1;
-  uint32_t *open = scratch_t<uint32_t>(c, "dist_open", 1);
-  if (!open) return fail(c, "out of device memory (dist_thr)");
-  if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-  Launch L(c, "dist_jump", (double)n * 12);
-  for (int round = 0; round < 64; round++) {
-    HIPCHK(c, hipMemsetAsync(open, 0, 4, c->stream));
-    hipLaunchKernelGGL(k_dist_jump, DIST_GRID(n), T, (uint32_t)n, base, open);
-    if (dist_launch_ok(c, "dist_jump")) return -1;
-    HIPCHK(c, hipMemcpyAsync(c->pin_small, open, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (!c->pin_small[0]) return 0;
-  }
-  return fail(c, "dist_thr: pointer jumping did not converge");
-}
-
-int dist_fetch_impl(cw_ctx *c, const uint32_t *src, uint32_t base, uint64_t n, const uint64_t *q,
-                    uint64_t m, uint32_t *out) {
-  if (!m) return 0;
-  hipLaunchKernelGGL(k_dist_fetch, DIST_GRID(m), src, base, (uint32_t)n, q, (uint32_t)m, out);
-  return dist_launch_ok(c, "dist_fetch");
+  Launch L(c, "dist_thr", (double)n * (4 + 4));
+  hipLaunchKernelGGL((k_dist_thr<256, 1024>), dim3((uint32_t)((n + 1023) / 1024)), dim3(256), 0,
+                     c->stream, nsc, (uint32_t)n, base, thr);
+  return dist_launch_ok(c, "dist_thr");
 }
 
 int dist_succ_impl(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
-                   const uint32_t *T, uint64_t n, uint32_t base, uint32_t *out) {
+                   uint64_t n, uint32_t base, uint32_t *out) {
   if (!n) return 0;
-  Launch L(c, "dist_succ", (double)n * (1 + 4 + 4 + 4 + 4));
-  hipLaunchKernelGGL(k_dist_succ, DIST_GRID(n), kind, fcS, fcN, T, (uint32_t)n, base, out);
+  Launch L(c, "dist_succ", (double)n * (1 + 4 + 4 + 4));
+  hipLaunchKernelGGL(k_dist_succ, DIST_GRID(n), kind, fcS, fcN, (uint32_t)n, base, out);
   return dist_launch_ok(c, "dist_succ");
 }
 
@@ -370,7 +388,7 @@ int weave_linked_impl(cw_ctx *c, const cw_linked_list *in, cw_list_result *out) 
   if (out->yarn_perm || out->max_ts) return fail(c, "yarn_perm / max_ts: not produced from links");
   const uint64_t n64 = in->n;
   if (n64 == 0 || n64 >= SUCCW_END) return fail(c, "list size %llu (1 .. 2^31-2)", (unsigned long long)n64);
-  if (!in->succ) return fail(c, "null input arrays");
+  if (!in->succ || !in->thr) return fail(c, "null input arrays");
   const uint32_t n = (uint32_t)n64;
   HIPCHK(c, hipSetDevice(c->device));
   const uint64_t off[2] = {0, n64};
@@ -383,8 +401,9 @@ int weave_linked_impl(cw_ctx *c, const cw_linked_list *in, cw_list_result *out) 
   uint32_t *thr = scratch_t<uint32_t>(c, "thr", n);
   if (!link || !thr) return fail(c, "out of device memory (linked, n=%u)", n);
   {
-    Launch L(c, "linked", (double)n * (4 + 8 + 4));
-    hipLaunchKernelGGL(k_linked_words, DIST_GRID(n), in->succ, n, c->tab.doc_log2k[0], link, thr);
+    Launch L(c, "linked", (double)n * (4 + 4 + 8 + 4));
+    hipLaunchKernelGGL(k_linked_words, DIST_GRID(n), in->succ, in->thr, n, c->tab.doc_log2k[0], link,
+                       thr);
   }
   if (dist_launch_ok(c, "linked")) return -1;
   if (weave_tail(c, 1, n, true, nullptr, nullptr, in->val, nullptr, nullptr, 0, out, nullptr, nullptr,

@@ -82,6 +82,14 @@ class HipOps:
         return ko, io
 
     @_on_stream
+    def sort_keys32(self, keys, key_bits):
+        n = keys.numel()
+        ko, io = self._e(n, torch.int32), self._e(n, torch.int32)
+        if n:
+            self.w.sort_keys32_device(keys.data_ptr(), n, key_bits, ko.data_ptr(), io.data_ptr())
+        return ko, io
+
+    @_on_stream
     def partition(self, keys, splitters):
         m = keys.numel()
         perm = self._e(m, torch.int32)
@@ -156,14 +164,16 @@ class HipOps:
         return out
 
     @_on_stream
-    def dist_pending(self, w, mode):
+    def dist_pending(self, w):
+        """(partition keys of the eff words waiting on another rank, how many)."""
         keys = self._e(w.numel(), torch.int64)
-        self.w.dist("pending", self._p(w), w.numel(), mode, self._p(keys))
-        return keys
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.w.dist("pending", self._p(w), w.numel(), self._p(keys), cnt.data_ptr())
+        return keys, int(cnt.item())
 
     @_on_stream
     def dist_gkey(self, eff, kind):
-        key = self._e(eff.numel(), torch.int64)
+        key = self._e(eff.numel(), torch.int32)
         self.w.dist("gkey", self._p(eff), self._p(kind), eff.numel(), self._p(key))
         return key
 
@@ -178,7 +188,7 @@ class HipOps:
 
     @_on_stream
     def dist_rkey(self, rec):
-        key = self._e(rec.shape[0], torch.int64)
+        key = self._e(rec.shape[0], torch.int32)
         self.w.dist("rkey", self._p(rec), rec.shape[0], self._p(key))
         return key
 
@@ -195,20 +205,14 @@ class HipOps:
 
     @_on_stream
     def dist_thr(self, nsc, base):
-        T = self._e(nsc.numel(), torch.int32)
-        self.w.dist("thr", self._p(nsc), nsc.numel(), base, self._p(T))
-        return T
+        thr = self._e(nsc.numel(), torch.int32)
+        self.w.dist("thr", self._p(nsc), nsc.numel(), base, self._p(thr))
+        return thr
 
     @_on_stream
-    def dist_fetch(self, src, base, q):
-        out = self._e(q.numel(), torch.int32)
-        self.w.dist("fetch", self._p(src), base, src.numel(), self._p(q), q.numel(), self._p(out))
-        return out
-
-    @_on_stream
-    def dist_succ(self, kind, fcS, fcN, T, base):
-        out = self._e(T.numel(), torch.int32)
-        self.w.dist("succ", self._p(kind), self._p(fcS), self._p(fcN), self._p(T), T.numel(), base,
+    def dist_succ(self, kind, fcS, fcN, base):
+        out = self._e(kind.numel(), torch.int32)
+        self.w.dist("succ", self._p(kind), self._p(fcS), self._p(fcN), kind.numel(), base,
                     self._p(out))
         return out
 
@@ -232,12 +236,12 @@ class HipOps:
         return torch.zeros(n, dtype=torch.int32, device=self.dev)
 
     @_on_stream
-    def weave_linked(self, succ, val):
+    def weave_linked(self, succ, thr, val):
         n = succ.numel()
         o = {"weave_perm": self._e(n, torch.int32),
              "visible_bits": self._e((n + 31) // 32, torch.int32),
              "visible_count": self._e(1, torch.int32), "status": self._e(1, torch.int32)}
-        self.w.weave_linked_device(n, succ.data_ptr(), val.data_ptr(),
+        self.w.weave_linked_device(n, succ.data_ptr(), thr.data_ptr(), val.data_ptr(),
                                    {k: t.data_ptr() for k, t in o.items()})
         return o
 
@@ -324,24 +328,12 @@ def weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift=0, group=
                                   samples, tree)
 
 
-def _route(ops, keys, split_t, W, group, dev):
-    """Send every entry whose key (a global rank) is < N to the owner of that
-    rank: (positions of the sent entries, send counts, receive counts, the
-    keys received).  Keys of UINT64_MAX (-1 as int64) stay home."""
-    perm, counts = ops.partition(keys, split_t)   # W + 1 buckets: the last one stays
-    send = counts[:W]
-    idx = perm[:sum(send)]
-    q = ops.gather(keys, idx)
-    recv = _exchange_counts(send, group, dev)
-    return idx, send, recv, _a2a(q, send, recv, group)
-
-
 def _any(v, group, dev):
     return sum(x[0] for x in _all_gather_ints([v], group, dev))
 
 
 def _tree_distributed(ops, par, kind, base, owns, group, dev):
-    """Preorder successor | render bit of this rank's nodes (global ranks
+    """(successor word, thread word) of this rank's nodes (global ranks
     [base, base + n)) -- the giant path's tree with the
     cross-rank steps as all-to-all rounds (dist.hip)."""
     W = len(owns)
@@ -352,15 +344,21 @@ def _tree_distributed(ops, par, kind, base, owns, group, dev):
     # effective parents: climbs leave the run at most W - 1 times
     eff = ops.dist_eff(par, kind, base)
     for _ in range(W + 1):
-        idx, send, recv, rq = _route(ops, ops.dist_pending(eff, 0), split_t, W, group, dev)
-        if not _any(len(idx), group, dev):
+        keys, waiting = ops.dist_pending(eff)
+        if not _any(waiting, group, dev):
             break
+        # the climbs that left the run go to the owner of the cause they reached
+        perm, counts = ops.partition(keys, split_t)   # W + 1 buckets: the last stays
+        send = counts[:W]
+        idx = perm[:sum(send)]
+        recv = _exchange_counts(send, group, dev)
+        rq = _a2a(ops.gather(keys, idx), send, recv, group)
         ans = ops.dist_climb(par, kind, base, rq)
         ops.scatter_into(eff, _a2a(ans, recv, send, group), idx)
     else:
         raise RuntimeError("distributed tree: effective parents did not converge")
     # siblings: local runs of each (e, class), their records at the owner of e
-    sk, si = ops.sort_keys(ops.dist_gkey(eff, kind), 33)
+    sk, si = ops.sort_keys32(ops.dist_gkey(eff, kind), 32)
     nsc, okey, rec = ops.dist_runs(sk, si, base, kind)
     del eff, sk, si
     perm, counts = ops.partition(okey, split_t)
@@ -370,21 +368,12 @@ def _tree_distributed(ops, par, kind, base, owns, group, dev):
     recv = _exchange_counts(send, group, dev)
     rr = _a2a(rs.reshape(-1), [4 * x for x in send], [4 * x for x in recv], group).view(-1, 4)
     fcS, fcN = ops.zeros32(n), ops.zeros32(n)
-    rk, ri = ops.sort_keys(ops.dist_rkey(rr), 64)
+    rk, ri = ops.sort_keys32(ops.dist_rkey(rr), 32)
     reply = ops.dist_link(rk, ri, rr, base, n, fcS, fcN)
     ops.dist_put(rs, _a2a(reply, recv, send, group), base, nsc)
     del rec, okey, perm, idx, rs, rr, rk, ri, reply
-    # threads: local chains by pointer jumping, pointers into earlier runs by
-    # their owners (one run nearer the root per round)
-    T = ops.dist_thr(nsc, base)
-    for _ in range(W + 1):
-        idx, send, recv, rq = _route(ops, ops.dist_pending(T, 1), split_t, W, group, dev)
-        if not _any(len(idx), group, dev):
-            break
-        ops.scatter_into(T, _a2a(ops.dist_fetch(T, base, rq), recv, send, group), idx)
-    else:
-        raise RuntimeError("distributed tree: threads did not converge")
-    return ops.dist_succ(kind, fcS, fcN, T, base)
+    # threads: chains resolved inside each tile; the rest is chased by the walk
+    return ops.dist_succ(kind, fcS, fcN, base), ops.dist_thr(nsc, base)
 
 
 def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples,
@@ -461,14 +450,15 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
         for v in _all_gather_ints([ops.dist_check(par, okd, own_base)], group, dev):
             st |= v[0]
         if not st and not dups:
-            succ = _tree_distributed(ops, par, okd, own_base, owns, group, dev)
+            succ, thr = _tree_distributed(ops, par, okd, own_base, owns, group, dev)
             gsend = [n_own if j == root else 0 for j in range(W)]
             grecv = [owns[j] if r == root else 0 for j in range(W)]
             g_succ = _a2a(succ, gsend, grecv, group)
+            g_thr = _a2a(thr, gsend, grecv, group)
             g_org = _a2a(oorg, gsend, grecv, group)
             if r != root:
                 return GiantResult(None, None, None, None, N, n_own, max_ts)
-            o = ops.weave_linked(g_succ, g_org)
+            o = ops.weave_linked(g_succ, g_thr, g_org)
             return GiantResult(o["weave_perm"], o["visible_bits"], int(o["visible_count"][0]),
                                int(o["status"][0]), N, n_own, max_ts)
 

@@ -360,8 +360,10 @@ int cw_weave_ranked(cw_ctx *ctx, const cw_ranked_list *list, cw_list_result *res
  * caller routes the queries and records between the ranks. */
 #define CW_DIST_PEND 0x80000000u /* eff word: the climb goes on at the rank in the low bits */
 #define CW_DIST_NONE 0xFFFFFFFFu /* eff word of the root                                   */
-#define CW_DIST_RES 0x80000000u  /* thread word: resolved (low bits: the successor rank)   */
 
+/* cw_sort_keys for 32-bit keys (key_bits 0 = 32). */
+int cw_sort_keys32(cw_ctx *ctx, const uint32_t *keys, uint64_t n, uint32_t key_bits,
+                   uint32_t *keys_out, uint32_t *idx_out);
 /* status (device, one word) |= ROOT / ORPHAN / NON_LAMPORT for this run. */
 int cw_dist_check(cw_ctx *ctx, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
                   uint32_t *status);
@@ -373,43 +375,47 @@ int cw_dist_eff(cw_ctx *ctx, uint64_t n, uint32_t base, const uint32_t *par, con
  * node at or above q[i] inside the run, or CW_DIST_PEND | the next rank. */
 int cw_dist_climb(cw_ctx *ctx, uint64_t n, uint32_t base, const uint32_t *par, const uint8_t *kind,
                   const uint64_t *q, uint64_t m, uint32_t *out);
-/* keys[i] = the rank word w[i] waits on (mode 0: eff words, 1: thread words),
- * UINT64_MAX when it waits on nothing (for cw_partition_keys by owner). */
-int cw_dist_pending(cw_ctx *ctx, const uint32_t *w, uint64_t n, uint32_t mode, uint64_t *keys);
-/* key[i] = eff << 1 | (non-special), 2^33 - 1 for the root (33-bit keys). */
-int cw_dist_gkey(cw_ctx *ctx, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint64_t *key);
+/* keys[i] = the rank the eff word w[i] waits on, UINT64_MAX when it waits on
+ * nothing (for cw_partition_keys by owner); *count (device) = how many wait. */
+int cw_dist_pending(cw_ctx *ctx, const uint32_t *w, uint64_t n, uint64_t *keys, uint32_t *count);
+/* key[i] = eff << 1 | (non-special), 0xFFFFFFFF for the root. */
+int cw_dist_gkey(cw_ctx *ctx, const uint32_t *eff, const uint8_t *kind, uint64_t n, uint32_t *key);
 /* After a stable local sort of the group keys (skey, sidx): nsc = next
  * sibling inside each run; per run a record {group, oldest, newest, kind of
  * newest} (rec: 4 words per sorted position) and okey = its e (UINT64_MAX on
  * the other positions). */
-int cw_dist_runs(cw_ctx *ctx, const uint64_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
+int cw_dist_runs(cw_ctx *ctx, const uint32_t *skey, const uint32_t *sidx, uint64_t n, uint32_t base,
                  const uint8_t *kind, uint32_t *nsc, uint64_t *okey, uint32_t *rec);
-/* key[i] = group << 32 | oldest of received record i. */
-int cw_dist_rkey(cw_ctx *ctx, const uint32_t *rec, uint64_t m, uint64_t *key);
+/* key[i] = group of received record i (a stable sort by it, the records in
+ * sender order, orders each group's runs by their oldest node). */
+int cw_dist_rkey(cw_ctx *ctx, const uint32_t *rec, uint64_t m, uint32_t *key);
 /* At the owner of the parents, records sorted by cw_dist_rkey's key: the
  * first children fcS / fcN of its nodes (zeroed before; fcS bit 31 = that
  * child is a hide) and reply[i] = the next sibling of record i's oldest node
  * (NSC_UP-style 0x80000000 | e when it has none). */
-int cw_dist_link(cw_ctx *ctx, const uint64_t *skey, const uint32_t *sidx, uint64_t m,
+int cw_dist_link(cw_ctx *ctx, const uint32_t *skey, const uint32_t *sidx, uint64_t m,
                  const uint32_t *rec, uint32_t base, uint64_t n, uint32_t *fcS, uint32_t *fcN,
                  uint32_t *reply);
 /* nsc[oldest of rec i - base] = reply[i]. */
 int cw_dist_put(cw_ctx *ctx, const uint32_t *rec, const uint32_t *reply, uint64_t m, uint32_t base,
                 uint64_t n, uint32_t *nsc);
-/* Thread words from nsc, every pointer into this run resolved (pointer jumping). */
-int cw_dist_thr(cw_ctx *ctx, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *T);
-/* out[i] = src[q[i] - base]. */
-int cw_dist_fetch(cw_ctx *ctx, const uint32_t *src, uint32_t base, uint64_t n, const uint64_t *q,
-                  uint64_t m, uint32_t *out);
-/* out[i] = preorder successor of base + i | render bit (bit 31). */
+/* Thread words from nsc (the preorder successor of a childless node): the
+ * successor rank, or 0x80000000 | an ancestor outside the node's 1,024-rank
+ * tile whose thread it is (resolved inside each tile by pointer jumping). */
+int cw_dist_thr(cw_ctx *ctx, const uint32_t *nsc, uint64_t n, uint32_t base, uint32_t *thr);
+/* out[i] = first child of base + i, or CW_DIST_FROM_THR (its thread), | the
+ * render bit (bit 31). */
+#define CW_DIST_FROM_THR 0x7FFFFFFEu
 int cw_dist_succ(cw_ctx *ctx, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
-                 const uint32_t *T, uint64_t n, uint32_t base, uint32_t *out);
+                 uint64_t n, uint32_t base, uint32_t *out);
 
-/* One list given every node's preorder successor: succ[r] = successor rank
- * (>= n: the last node) | bit 31 when r renders.  val as cw_ranked_list. */
+/* One list given every node's successor word (cw_dist_succ) and thread word
+ * (cw_dist_thr), in rank order; the walk chases pending threads.  val as
+ * cw_ranked_list. */
 typedef struct {
   uint64_t n;
   const uint32_t *succ;
+  const uint32_t *thr;
   const uint32_t *val;
 } cw_linked_list;
 

@@ -39,6 +39,11 @@ class CpuOps:
         dup = 2 if len(s) > 1 and bool((s[1:] == s[:-1]).any()) else 0  # CW_STATUS_DUP
         return torch.from_numpy(out.view(np.int32)), dup
 
+    def sort_keys32(self, keys, key_bits):
+        k = keys.numpy().view(np.uint32)
+        o = np.argsort(k, kind="stable")
+        return torch.from_numpy(k[o].view(np.int32).copy()), torch.from_numpy(o.astype(np.int32))
+
     def gather(self, src, idx):
         return src[idx.long()]
 
@@ -67,7 +72,7 @@ class CpuOps:
     NONE = 0xFFFFFFFF
     NSC_UP = 0x80000000
     END = 0x7FFFFFFF
-    ROOT_KEY = (1 << 33) - 1
+    ROOT_KEY = 0xFFFFFFFF
 
     @staticmethod
     def _special(k):
@@ -122,23 +127,20 @@ class CpuOps:
         p, k = self._u32(par), kind.numpy()
         return self._t32([self._climb(int(x), p, k, base) for x in _u64(q)])
 
-    def dist_pending(self, w, mode):
+    def dist_pending(self, w):
         x = self._u32(w).astype(np.uint64)
-        if mode == 0:
-            pend = ((x & self.PEND) != 0) & (x != self.NONE)
-        else:
-            pend = (x & self.RES) == 0
+        pend = ((x & self.PEND) != 0) & (x != self.NONE)
         keys = np.where(pend, x & ~np.uint64(self.PEND), np.uint64(2**64 - 1))
-        return torch.from_numpy(keys.view(np.int64))
+        return torch.from_numpy(keys.view(np.int64)), int(pend.sum())
 
     def dist_gkey(self, eff, kind):
         e = self._u32(eff).astype(np.uint64)
         cls = np.where(self._special(kind.numpy()), 0, 1).astype(np.uint64)
         key = np.where(e == self.NONE, np.uint64(self.ROOT_KEY), (e << np.uint64(1)) | cls)
-        return torch.from_numpy(key.view(np.int64))
+        return self._t32(key.astype(np.uint32))
 
     def dist_runs(self, skey, sidx, base, kind):
-        sk, si, k = _u64(skey), sidx.numpy().view(np.uint32), kind.numpy()
+        sk, si, k = skey.numpy().view(np.uint32), sidx.numpy().view(np.uint32), kind.numpy()
         n = len(sk)
         nsc = np.zeros(n, np.uint32)
         okey = np.full(n, 2**64 - 1, np.uint64)
@@ -162,15 +164,15 @@ class CpuOps:
                 torch.from_numpy(rec.view(np.int32)))
 
     def dist_rkey(self, rec):
-        r = rec.numpy().view(np.uint32).astype(np.uint64)
-        return torch.from_numpy(((r[:, 0] << np.uint64(32)) | r[:, 1]).view(np.int64))
+        r = rec.numpy().view(np.uint32)
+        return self._t32(np.ascontiguousarray(r[:, 0]))
 
     def dist_link(self, skey, sidx, rec, base, n, fcS, fcN):
-        sk, si = _u64(skey), sidx.numpy().view(np.uint32)
+        sk, si = skey.numpy().view(np.uint32), sidx.numpy().view(np.uint32)
         r = rec.numpy().view(np.uint32)
         fs, fn = fcS.numpy().view(np.uint32), fcN.numpy().view(np.uint32)
         m = len(sk)
-        g = (sk >> np.uint64(32)).astype(np.uint64)
+        g = sk.astype(np.uint64)
         reply = np.zeros(m, np.uint32)
         for j in range(m):
             gj, e = int(g[j]), int(g[j]) >> 1
@@ -197,29 +199,41 @@ class CpuOps:
         for i in range(len(rp)):
             ns[int(r[i, 1]) - base] = rp[i]
 
-    def dist_thr(self, nsc, base):
+    def dist_thr(self, nsc, base, tile=1024):
+        """Thread words: chains followed inside each tile of the run; one that
+        leaves the tile ends as PEND | the ancestor outside."""
         s = self._u32(nsc)
         n = len(s)
-        T = np.where((s & self.NSC_UP) != 0, s & ~np.uint32(self.NSC_UP), s | np.uint32(self.RES))
-        if base == 0 and n:
-            T[0] = self.RES | self.END
-        while True:   # pointer jumping over the local pointers
-            loc = ((T & self.RES) == 0) & (T >= base) & (T < base + n)
-            if not loc.any():
-                return self._t32(T)
-            T = np.where(loc, T[np.where(loc, T - base, 0)], T)
+        out = np.zeros(n, np.uint32)
+        for i in range(n):
+            g0 = base + (i // tile) * tile
+            j = i
+            while True:
+                g = base + j
+                if g == 0:
+                    out[i] = self.END
+                    break
+                x = int(s[j])
+                if not x & self.NSC_UP:
+                    out[i] = x
+                    break
+                e = x & ~self.NSC_UP
+                if e < g0:
+                    out[i] = self.PEND | e
+                    break
+                if e >= g:   # (out of domain)
+                    out[i] = self.END
+                    break
+                j = e - base
+        return self._t32(out)
 
-    def dist_fetch(self, src, base, q):
-        s = self._u32(src)
-        return self._t32([s[int(x) - base] for x in _u64(q)])
-
-    def dist_succ(self, kind, fcS, fcN, T, base):
+    def dist_succ(self, kind, fcS, fcN, base):
         k = kind.numpy()
-        fs, fn, t = self._u32(fcS), self._u32(fcN), self._u32(T)
-        out = np.zeros(len(t), np.uint32)
-        for i in range(len(t)):
+        fs, fn = self._u32(fcS), self._u32(fcN)
+        out = np.zeros(len(k), np.uint32)
+        for i in range(len(k)):
             f = int(fs[i]) & 0x7FFFFFFF
-            succ = f if f else (int(fn[i]) if fn[i] else int(t[i]) & 0x7FFFFFFF)
+            succ = f if f else (int(fn[i]) if fn[i] else 0x7FFFFFFE)
             vis = not self._special(k[i]) and base + i != 0 and not (fs[i] and fs[i] & 0x80000000)
             out[i] = succ | (0x80000000 if vis else 0)
         return self._t32(out)
@@ -233,16 +247,23 @@ class CpuOps:
     def zeros32(self, n):
         return torch.zeros(n, dtype=torch.int32)
 
-    def weave_linked(self, succ, val):
-        """The list ranking by walking the successors from the root (rank 0)."""
-        s = self._u32(succ)
+    def weave_linked(self, succ, thr, val):
+        """The list ranking by walking the successors from the root (rank 0);
+        a thread successor is chased through the thread words."""
+        s, th = self._u32(succ), self._u32(thr)
         n = len(s)
         order, vis = np.empty(n, np.int64), np.zeros(n, np.uint8)
         x, g = 0, 0
         while x < n and g < n:
             order[g] = x
             vis[g] = 1 if s[x] & 0x80000000 else 0
-            x = int(s[x]) & 0x7FFFFFFF
+            nx = int(s[x]) & 0x7FFFFFFF
+            if nx == 0x7FFFFFFE:
+                t = int(th[x])
+                while t & self.PEND:
+                    t = int(th[t & 0x7FFFFFFF])
+                nx = t
+            x = nx
             g += 1
         st = 0 if g == n else 32   # CW_STATUS_INTERNAL
         wp = val.numpy()[order[:g]] if g == n else np.zeros(n, np.int32)

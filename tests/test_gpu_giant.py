@@ -197,14 +197,14 @@ def test_dist_ops_match_the_double(ops, n, seed, lo, hi):
     rng = np.random.default_rng(seed)
     q = rng.integers(lo, hi, 5000).astype(np.int64)
     assert _same(ops.dist_climb(_t(par), _t(kd), lo, _t(q)), cpu.dist_climb(T(par), T(kd), lo, T(q)))
-    for mode in (0, 1):
-        assert _same(ops.dist_pending(eff, mode), cpu.dist_pending(ceff, mode))
+    (k1, c1), (k2, c2) = ops.dist_pending(eff), cpu.dist_pending(ceff)
+    assert _same(k1, k2) and c1 == c2
     # effective parents of the whole list from the full run: the group keys,
     # runs, records and links of a one-rank tree
     feff = cpu.dist_eff(T(fpar), T(fkd), 0)
     gk = cpu.dist_gkey(feff, T(fkd))
     assert _same(ops.dist_gkey(_t(feff.numpy()), _t(fkd)), gk)
-    sk, si = cpu.sort_keys(gk, 33)
+    sk, si = cpu.sort_keys32(gk, 32)
     nsc, okey, rec = ops.dist_runs(_t(sk.numpy()), _t(si.numpy()), 0, _t(fkd))
     cnsc, cokey, crec = cpu.dist_runs(sk, si, 0, T(fkd))
     assert _same(nsc, cnsc) and _same(okey, cokey)
@@ -213,7 +213,7 @@ def test_dist_ops_match_the_double(ops, n, seed, lo, hi):
     rs = crec[heads].contiguous()
     rkey = ops.dist_rkey(_t(rs.numpy()))
     assert _same(rkey, cpu.dist_rkey(rs))
-    rk, ri = cpu.sort_keys(rkey.cpu(), 64)
+    rk, ri = cpu.sort_keys32(rkey.cpu(), 32)
     n = len(fpar)   # (the list has a root besides its n generated nodes)
     fs, fn = ops.zeros32(n), ops.zeros32(n)
     cfs, cfn = cpu.zeros32(n), cpu.zeros32(n)
@@ -226,10 +226,10 @@ def test_dist_ops_match_the_double(ops, n, seed, lo, hi):
     thr = ops.dist_thr(nsc, 0)
     cthr = cpu.dist_thr(cnsc, 0)
     assert _same(thr, cthr)
-    q2 = rng.integers(0, n, 3000).astype(np.int64)
-    assert _same(ops.dist_fetch(thr, 0, _t(q2)), cpu.dist_fetch(cthr, 0, T(q2)))
-    succ = ops.dist_succ(_t(fkd), fs, fn, thr, 0)
-    csucc = cpu.dist_succ(T(fkd), cfs, cfn, cthr, 0)
+    # a run that starts mid-list: tiles counted from the run's start
+    assert _same(ops.dist_thr(_t(cnsc.numpy()[lo:hi]), lo), cpu.dist_thr(cnsc[lo:hi], lo))
+    succ = ops.dist_succ(_t(fkd), fs, fn, 0)
+    csucc = cpu.dist_succ(T(fkd), cfs, cfn, 0)
     assert _same(succ, csucc)
 
 
@@ -244,18 +244,18 @@ def test_weave_linked_equals_weave_ranked(ops, n, seed):
     n = len(par)
     T = torch.from_numpy
     eff = ops.dist_eff(_t(par), _t(kd), 0)
-    sk, si = ops.sort_keys(ops.dist_gkey(eff, _t(kd)), 33)
+    sk, si = ops.sort_keys32(ops.dist_gkey(eff, _t(kd)), 32)
     nsc, okey, rec = ops.dist_runs(sk, si, 0, _t(kd))
     heads = okey.cpu().numpy() != -1
     rs = _t(rec.cpu().numpy()[heads])
-    rk, ri = ops.sort_keys(ops.dist_rkey(rs), 64)
+    rk, ri = ops.sort_keys32(ops.dist_rkey(rs), 32)
     fs, fn = ops.zeros32(n), ops.zeros32(n)
     reply = ops.dist_link(rk, ri, rs, 0, n, fs, fn)
     ops.dist_put(rs, reply, 0, nsc)
-    succ = ops.dist_succ(_t(kd), fs, fn, ops.dist_thr(nsc, 0), 0)
-    got = ops.weave_linked(succ, _t(val))
+    succ, thr = ops.dist_succ(_t(kd), fs, fn, 0), ops.dist_thr(nsc, 0)
+    got = ops.weave_linked(succ, thr, _t(val))
     want = ops.weave_ranked(_t(par), _t(kd), _t(val))
-    ref = cpu.weave_linked(succ.cpu(), T(val))
+    ref = cpu.weave_linked(succ.cpu(), thr.cpu(), T(val))
     assert int(got["status"][0]) == 0 == int(want["status"][0])
     for k in ("weave_perm", "visible_count"):
         assert _same(got[k], want[k]) and _same(got[k], ref[k]), k
