@@ -152,3 +152,49 @@ def test_choose_splitters_weighted():
     w2 = np.concatenate([np.full(50, 10.0), np.full(50, 1.0)])
     assert giant.choose_splitters(s2, w2, 2)[0] < 50
     assert len(giant.choose_splitters(np.zeros(0, np.int64), np.zeros(0), 3)) == 0
+
+
+def _orphan_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from tests.giant_cpu_ops import CpuOps
+
+        class Ops(CpuOps):
+            linked = 0
+
+            def weave_linked(self, *a):
+                Ops.linked += 1
+                return super().weave_linked(*a)
+
+        spec, idk, ck, kd = make_list(2000, 41)
+        ck = ck.copy()
+        ck[7] = idk.max() + np.uint64(5)   # a cause that is no node: an orphan
+        sh = shares(len(idk), world, 41)[rank]
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int64))
+        lay = spec.layout()
+        res = giant.weave_distributed(Ops(), t(idk[sh]), t(ck[sh]), torch.from_numpy(kd[sh].copy()),
+                                      lay.key_bits + 1, ts_shift=lay.ts_shift, samples=64,
+                                      tree="dist")
+        if rank == 0:
+            q.put((res.status, Ops.linked))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_distributed_tree_leaves_out_of_domain_lists_to_the_root():
+    """A list with an orphan cause is outside the fast path's domain: every rank's
+    cw_dist_check sees it and the list goes to the rank-0 weave (and its exact
+    path) instead of the tree by rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_orphan_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    status, linked = q.get(timeout=120)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert status & 4 and linked == 0  # CW_STATUS_ORPHAN, no cw_weave_linked
