@@ -2840,6 +2840,8 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
+  bool x_cached = false;           // x_status holds the status of this call's giant document,
+  uint32_t x_status = 0;           // read back with the walk's counter (exact.hip skips a sync)
   uint32_t map_fused = 1;          // CW_MAP_FUSED: one-kernel map weave of small collections
   struct MapPacks {                // k_map_pack's pack table, cached by collection layout
     std::vector<uint64_t> off;
@@ -3426,7 +3428,11 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     if (giant) {
       if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
       HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
+      // the document's status rides along: its domain bits are final by now
+      HIPCHK(c, hipMemcpyAsync(c->pin_small + 4, out->status, 4, hipMemcpyDeviceToHost, c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->x_cached = true;
+      c->x_status = c->pin_small[4];
       const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
       // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
       const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
@@ -3723,6 +3729,7 @@ int weave_lists_dev_all(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id,
     t_giant += n >= c->giant_min ? 0.4e-3 + nd * 0.3e-9 : 0.1e-3 + nd * 22e-9;
   }
   bool x_hint = false;
+  c->x_cached = false;
   if (D > 1 && D <= c->giant_docs_max && nd_max >= c->giant_min && t_giant < t_tree) {
     if (dres.visible_bits)
       HIPCHK(c, hipMemsetAsync(dres.visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
