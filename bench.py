@@ -470,7 +470,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
         st_bad[0] += int(np.count_nonzero(o.status))
         vis_total[0] += int(o.visible_count.sum(dtype=np.uint64))
 
-    s = stream.BatchStreamer(w, dev, B * n, B, layout, depth=a.depth, k32=k32)
+    perm16 = k32 and n < 65536
+    s = stream.BatchStreamer(w, dev, B * n, B, layout, depth=a.depth, k32=k32, perm16=perm16)
     s.run(min(a.warmup, nb), fill)          # warm-up batches (not timed)
     w.reset_kernel_stats()
     w.set_profiling(True)
@@ -529,8 +530,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
         cpu = None
         if world == 1 and not a.no_cpu:
             cpu = cpu_baseline(spec, a.cpu_seconds, max_docs=64)
-        kw = 4 if k32 else 8
-        pcie = total // world * (kw + kw + 1 + 4) + total // world // 8
+        kw, pw = (4 if k32 else 8), (2 if perm16 else 4)
+        pcie = total // world * (kw + kw + 1 + pw) + total // world // 8
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
             "value": total / t_dev_max, "unit": "nodes/s", "n_gpus": world, "steps": nb,
@@ -543,7 +544,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                        "sites": spec.n_sites, "p_hide": spec.p_hide, "p_show": spec.p_show,
                        "p_conj": spec.p_conj, "key_bits": layout.key_bits,
                        "pipeline_depth": a.depth, "key_words": "u32 (cw_weave_lists_k32)" if k32
-                       else "u64 (cw_weave_lists)", "parallelism": f"docs sharded x{world}"},
+                       else "u64 (cw_weave_lists)", "weave_perm": "u16" if perm16 else "u32",
+                       "parallelism": f"docs sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "launches_per_step": launches / nb,

@@ -49,6 +49,13 @@ class CwListBatch(C.Structure):
                 ("site_bits", C.c_uint32)]
 
 
+class CwListBatchK32(C.Structure):
+    _fields_ = [("n_docs", C.c_uint64), ("doc_offsets", C.POINTER(C.c_uint64)),
+                ("id_key", C.c_void_p), ("cause_key", C.c_void_p), ("kind", C.c_void_p),
+                ("key_bits", C.c_uint32), ("ts_shift", C.c_uint32), ("site_shift", C.c_uint32),
+                ("site_bits", C.c_uint32), ("perm16", C.c_uint32)]
+
+
 class CwListBatchK128(C.Structure):
     _fields_ = [("n_docs", C.c_uint64), ("doc_offsets", C.POINTER(C.c_uint64)),
                 ("id_key", C.c_void_p), ("cause_key", C.c_void_p), ("kind", C.c_void_p)]
@@ -150,7 +157,7 @@ def lib():
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
                                      C.c_int]
         L.cw_weave_lists.restype = C.c_int
-        L.cw_weave_lists_k32.argtypes = [C.c_void_p, C.POINTER(CwListBatch),
+        L.cw_weave_lists_k32.argtypes = [C.c_void_p, C.POINTER(CwListBatchK32),
                                          C.POINTER(CwListResult), C.c_int]
         L.cw_weave_lists_k32.restype = C.c_int
         L.cw_weave_lists_k128.argtypes = [C.c_void_p, C.POINTER(CwListBatchK128),
@@ -344,7 +351,7 @@ class Weaver:
         D, N = len(off) - 1, len(i)
         if int(off[-1]) != N or len(c) != N or len(k) != N:
             raise ValueError("offsets[-1] / id_key / cause_key / kind sizes differ")
-        b, off = self._batch(off, _ptr(i), _ptr(c), _ptr(k), layout, key_bits)
+        b, off = self._batch_k32(off, _ptr(i), _ptr(c), _ptr(k), layout, key_bits)
         out = ListResult(np.zeros(N, np.uint32), np.zeros((N + 31) // 32, np.uint32),
                          np.zeros(D, np.uint32), np.zeros(D, np.uint64), np.zeros(D, np.uint32),
                          np.zeros(N, np.uint32) if (yarns and layout.site_bits) else None)
@@ -354,12 +361,24 @@ class Weaver:
                     "cw_weave_lists_k32")
         return out
 
+    @staticmethod
+    def _batch_k32(offsets, id_ptr, cause_ptr, kind_ptr, layout, key_bits=None, perm16=False):
+        off = np.ascontiguousarray(offsets, np.uint64)
+        b = CwListBatchK32()
+        b.n_docs = len(off) - 1
+        b.doc_offsets = off.ctypes.data_as(C.POINTER(C.c_uint64))
+        b.id_key, b.cause_key, b.kind = id_ptr, cause_ptr, kind_ptr
+        b.key_bits = layout.key_bits if key_bits is None else key_bits
+        b.ts_shift, b.site_shift, b.site_bits = layout.ts_shift, layout.site_shift, layout.site_bits
+        b.perm16 = int(perm16)
+        return b, off
+
     def weave_lists_k32_device(self, offsets, id_ptr, cause_ptr, kind_ptr, layout, out_ptrs,
-                               key_bits=None):
+                               key_bits=None, perm16=False):
         """Device-memory call of cw_weave_lists_k32 (u32 keys; out_ptrs as
-        weave_lists_device)."""
-        b, off = self._batch(offsets, C.c_void_p(id_ptr), C.c_void_p(cause_ptr),
-                             C.c_void_p(kind_ptr), layout, key_bits)
+        weave_lists_device; perm16: weave_perm is uint16 per node)."""
+        b, off = self._batch_k32(offsets, C.c_void_p(id_ptr), C.c_void_p(cause_ptr),
+                                 C.c_void_p(kind_ptr), layout, key_bits, perm16)
         g = lambda n: C.c_void_p(out_ptrs[n]) if out_ptrs.get(n) else None
         r = CwListResult(g("weave_perm"), g("visible_bits"), g("visible_count"), g("max_ts"),
                          g("status"), g("yarn_perm"))

@@ -3884,6 +3884,12 @@ __global__ __launch_bounds__(256) void k_widen32(const uint32_t *__restrict__ id
   ca[i] = c >= CW_K32_RESERVED ? (uint64_t)(int64_t)(int32_t)c : (uint64_t)c;
 }
 
+__global__ __launch_bounds__(256) void k_narrow16(const uint32_t *__restrict__ src, uint32_t n,
+                                                  uint16_t *__restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (uint16_t)src[i];
+}
+
 int weave_lists_k32_impl(cw_ctx *c, const cw_list_batch_k32 *b, cw_list_result *res, int memspace) {
   if (!b || !res) return fail(c, "null batch/result");
   if (!b->doc_offsets) return fail(c, "doc_offsets is required (host memory)");
@@ -3927,7 +3933,24 @@ int weave_lists_k32_impl(cw_ctx *c, const cw_list_batch_k32 *b, cw_list_result *
   wb.ts_shift = b->ts_shift;
   wb.site_shift = b->site_shift;
   wb.site_bits = b->site_bits;
-  return weave_lists_impl(c, &wb, res, memspace, true);
+  if (!b->perm16) return weave_lists_impl(c, &wb, res, memspace, true);
+  // 16-bit weave_perm: documents below 2^16 nodes, the weave into scratch, narrowed
+  if (memspace != CW_MEM_DEVICE) return fail(c, "perm16 needs device memory");
+  for (uint64_t d = 0; d < D; d++)
+    if (b->doc_offsets[d + 1] - b->doc_offsets[d] > 0xFFFFull)
+      return fail(c, "perm16: document %llu has more than 65535 nodes", (unsigned long long)d);
+  cw_list_result r32 = *res;
+  r32.weave_perm = scratch_t<uint32_t>(c, "k32_perm", Ns);
+  if (!r32.weave_perm || !res->weave_perm) return fail(c, "out of device memory (perm16)");
+  if (weave_lists_impl(c, &wb, &r32, memspace, true)) return -1;
+  if (N) {
+    Launch L(c, "narrow16", (double)N * 6);
+    hipLaunchKernelGGL(k_narrow16, dim3((N + 255) / 256), dim3(256), 0, c->stream, r32.weave_perm, N,
+                       reinterpret_cast<uint16_t *>(res->weave_perm));
+  }
+  if (check_launch(c, "narrow16")) return -1;
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
+  return c->prof ? collect_prof(c) : 0;
 }
 
 // --- building blocks of the distributed giant list (cause_amd/giant.py) ---------

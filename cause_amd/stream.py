@@ -35,7 +35,7 @@ class BatchOut:
     index: int
     n_docs: int
     n_nodes: int
-    weave_perm: np.ndarray      # u32[n_nodes], per document doc-local input index
+    weave_perm: np.ndarray      # u32[n_nodes] (u16 with perm16), doc-local input index
     visible_bits: np.ndarray    # u32[(n_nodes+31)//32]
     visible_count: np.ndarray   # u32[n_docs]
     max_ts: np.ndarray          # u64[n_docs]
@@ -63,15 +63,16 @@ class StreamStats:
 
 
 class _Slot:
-    def __init__(self, dev, max_nodes, max_docs, k32=False):
+    def __init__(self, dev, max_nodes, max_docs, k32=False, perm16=False):
         pin = dict(pin_memory=True)
         kt = torch.int32 if k32 else torch.int64
+        pt = torch.int16 if perm16 else torch.int32
         self.k32 = k32
         self.h_id = torch.empty(max_nodes, dtype=kt, **pin)
         self.h_ca = torch.empty(max_nodes, dtype=kt, **pin)
         self.h_kd = torch.empty(max_nodes, dtype=torch.uint8, **pin)
         nb = (max_nodes + 31) // 32
-        self.h_perm = torch.empty(max_nodes, dtype=torch.int32, **pin)
+        self.h_perm = torch.empty(max_nodes, dtype=pt, **pin)
         self.h_bits = torch.empty(nb, dtype=torch.int32, **pin)
         self.h_vc = torch.empty(max_docs, dtype=torch.int32, **pin)
         self.h_mt = torch.empty(max_docs, dtype=torch.int64, **pin)
@@ -79,7 +80,7 @@ class _Slot:
         e = lambda n, t: torch.empty(n, dtype=t, device=dev)
         self.d_id, self.d_ca, self.d_kd = (e(max_nodes, kt), e(max_nodes, kt),
                                            e(max_nodes, torch.uint8))
-        self.d_perm, self.d_bits = e(max_nodes, torch.int32), e(nb, torch.int32)
+        self.d_perm, self.d_bits = e(max_nodes, pt), e(nb, torch.int32)
         self.d_vc, self.d_mt, self.d_st = (e(max_docs, torch.int32), e(max_docs, torch.int64),
                                            e(max_docs, torch.int32))
         ev = lambda: torch.cuda.Event(enable_timing=True)
@@ -110,10 +111,13 @@ class BatchStreamer:
     synchronous mode.
 
     k32: the slots hold 4-byte keys (cw_weave_lists_k32; fill writes u32 ids
-    and causes, nil = abi.NIL32): 9 instead of 17 input bytes a node over PCIe."""
+    and causes, nil = abi.NIL32): 9 instead of 17 input bytes a node over PCIe.
+    perm16 (with k32; documents < 65536 nodes): weave_perm comes back as u16."""
 
     def __init__(self, weaver: abi.Weaver, device, max_nodes, max_docs, layout, depth=2,
-                 k32=False):
+                 k32=False, perm16=False):
+        if perm16 and not k32:
+            raise ValueError("perm16 needs k32")
         if depth < 2:
             raise ValueError("depth >= 2")
         self.w = weaver
@@ -123,8 +127,9 @@ class BatchStreamer:
         self.s_in = torch.cuda.Stream(self.dev)
         self.s_w = torch.cuda.Stream(self.dev)
         self.s_out = torch.cuda.Stream(self.dev)
-        self.k32 = k32
-        self.slots = [_Slot(self.dev, self.max_nodes, self.max_docs, k32) for _ in range(depth)]
+        self.k32, self.perm16 = k32, perm16
+        self.slots = [_Slot(self.dev, self.max_nodes, self.max_docs, k32, perm16)
+                      for _ in range(depth)]
         weaver.set_stream(self.s_w.cuda_stream)
         weaver.set_async(True)
         self._open = True
@@ -172,8 +177,13 @@ class BatchStreamer:
         outs = {"weave_perm": slot.d_perm.data_ptr(), "visible_bits": slot.d_bits.data_ptr(),
                 "visible_count": slot.d_vc.data_ptr(), "max_ts": slot.d_mt.data_ptr(),
                 "status": slot.d_st.data_ptr()}
-        call = self.w.weave_lists_k32_device if self.k32 else self.w.weave_lists_device
-        call(off, slot.d_id.data_ptr(), slot.d_ca.data_ptr(), slot.d_kd.data_ptr(), self.layout, outs)
+        if self.k32:
+            self.w.weave_lists_k32_device(off, slot.d_id.data_ptr(), slot.d_ca.data_ptr(),
+                                          slot.d_kd.data_ptr(), self.layout, outs,
+                                          perm16=self.perm16)
+        else:
+            self.w.weave_lists_device(off, slot.d_id.data_ptr(), slot.d_ca.data_ptr(),
+                                      slot.d_kd.data_ptr(), self.layout, outs)
         slot.ev_w.record(self.s_w)
         nb = (N + 31) // 32
         with torch.cuda.stream(self.s_out):
@@ -197,7 +207,8 @@ class BatchStreamer:
         stats.batches += 1
         stats.nodes += N
         if consume is not None:
-            consume(BatchOut(i, D, N, slot.h_perm[:N].numpy().view(np.uint32),
+            consume(BatchOut(i, D, N, slot.h_perm[:N].numpy().view(
+                             np.uint16 if self.perm16 else np.uint32),
                              slot.h_bits[:(N + 31) // 32].numpy().view(np.uint32),
                              slot.h_vc[:D].numpy().view(np.uint32),
                              slot.h_mt[:D].numpy().view(np.uint64),

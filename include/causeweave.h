@@ -161,6 +161,8 @@ typedef struct {
   uint32_t ts_shift;
   uint32_t site_shift;
   uint32_t site_bits;
+  uint32_t perm16;             /* 1: result->weave_perm is uint16_t[N] (every document
+                                  < 65536 nodes; device memory only): half the bytes back */
 } cw_list_batch_k32;
 
 int cw_weave_lists_k32(cw_ctx *ctx, const cw_list_batch_k32 *batch, cw_list_result *result,

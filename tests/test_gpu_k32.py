@@ -64,6 +64,14 @@ def _both_ways(w, off, idk, ck, kd, lay):
     nb = (N + 31) // 32
     np.testing.assert_array_equal(outs["visible_bits"][:nb].cpu().numpy().view(np.uint32),
                                   want.visible_bits)
+    # 16-bit weave_perm (documents below 2^16 nodes)
+    if N and int(np.diff(off).max()) < 65536:
+        p16 = torch.empty(N, dtype=torch.int16, device=dev)
+        w.weave_lists_k32_device(off, gi.data_ptr(), gc.data_ptr(), gk.data_ptr(), lay,
+                                 dict({k: v.data_ptr() for k, v in outs.items()},
+                                      weave_perm=p16.data_ptr()), perm16=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(p16.cpu().numpy().view(np.uint16), want.weave_perm)
     return want
 
 
@@ -117,6 +125,19 @@ def test_golden_vectors(weaver):
         np.testing.assert_array_equal(res.weave_perm, z[nm + "_weave_perm"])
         done += 1
     assert done
+
+
+def test_perm16_rejects_large_documents(weaver):
+    import torch
+
+    off = np.array([0, 70_000], np.uint64)
+    dev = torch.device("cuda", 0)
+    z = torch.zeros(70_000, dtype=torch.int32, device=dev)
+    o = {k: torch.zeros(70_000, dtype=torch.int32, device=dev).data_ptr()
+         for k in ("weave_perm", "visible_bits", "visible_count", "max_ts", "status")}
+    with pytest.raises(abi.WeaveError):
+        weaver.weave_lists_k32_device(off, z.data_ptr(), z.data_ptr(), z.data_ptr(),
+                                      pack.KeyLayout(17, 0, 0), o, perm16=True)
 
 
 def test_narrow_rejects_wide_keys():

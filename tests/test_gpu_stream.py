@@ -19,8 +19,9 @@ def _batch(spec, i, docs):
     return gen.generate(spec, d0, d0 + docs[i], nthreads=4)
 
 
-@pytest.mark.parametrize("depth,k32", [(2, False), (3, False), (2, True)])
-def test_stream_matches_direct_and_oracle(depth, k32):
+@pytest.mark.parametrize("depth,k32,perm16", [(2, False, False), (3, False, False),
+                                              (2, True, False), (2, True, True)])
+def test_stream_matches_direct_and_oracle(depth, k32, perm16):
     import torch
 
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=700)
@@ -44,7 +45,7 @@ def test_stream_matches_direct_and_oracle(depth, k32):
 
     with abi.Weaver(0) as w:
         s = stream.BatchStreamer(w, "cuda:0", max_nodes, max(docs), spec.layout(), depth=depth,
-                                 k32=k32)
+                                 k32=k32, perm16=perm16)
         st = s.run(len(docs), fill, consume)
         del s
         torch.cuda.synchronize()
