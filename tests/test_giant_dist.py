@@ -198,3 +198,21 @@ def test_distributed_tree_leaves_out_of_domain_lists_to_the_root():
         p.join(60)
         assert p.exitcode == 0
     assert status & 4 and linked == 0  # CW_STATUS_ORPHAN, no cw_weave_linked
+
+
+def test_config5_list_order_crosses_ranks():
+    """Why the list ranking stays on the gathering GPU: in a
+    config-5 list the preorder successor of a node lies on another rank of the
+    id order for ~21% of the nodes at W = 2 and ~42% at W = 8 (30% of causes
+    are uniformly random earlier nodes, whose newest child follows them), so
+    rank-local sublists would be a few nodes long and a distributed ranking
+    pays O(N) cross-rank messages."""
+    spec, idk, ck, kd = make_list(200_000, 5)
+    off = np.array([0, len(idk)], np.uint64)
+    p, _, _ = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF)
+    rank = np.empty(len(idk), np.int64)
+    rank[np.argsort(idk, kind="stable")] = np.arange(len(idk))
+    r = rank[p.astype(np.int64)]
+    N = len(idk)
+    frac = {W: np.count_nonzero(np.diff(r * W // N)) / N for W in (2, 8)}
+    assert 0.15 < frac[2] < 0.3 and 0.35 < frac[8] < 0.5, frac
