@@ -616,7 +616,7 @@ __device__ __forceinline__ uint32_t fr_rank(const uint4 *__restrict__ dir, uint3
 // shared.cljc:243-249), group prefix counts, copy to the document's directory
 // slot.  An id past the slot marks the document FR_BIG and counts it in
 // big[0]; big[1] = the largest group count.
-template <int NT>
+template <int NT, uint32_t U = 4>
 __global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key,
                                              const uint32_t *__restrict__ doc_off,
                                              uint32_t slot_groups, uint4 *__restrict__ dir,
@@ -640,7 +640,6 @@ __global__ __launch_bounds__(NT) void k_fdir(const uint64_t *__restrict__ id_key
   const uint64_t lim = (uint64_t)slot_groups * FR_GROUP_BITS;
   uint64_t mx = 0;
   bool dup = false, far = false;
-  constexpr uint32_t U = 4;
   for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
     uint64_t x[U];
 #pragma unroll
@@ -1788,21 +1787,27 @@ __global__ __launch_bounds__(256) void k_lvl_apply(const uint32_t *__restrict__ 
   }
 }
 
+constexpr uint32_t SUP_MAX = 8192;  // elements k_sup_rank ranks in LDS (12 B each)
+
 __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ scnt,
                                                    const uint32_t *__restrict__ ssub,
                                                    const uint32_t *__restrict__ snext, uint32_t S2,
                                                    uint32_t n, uint32_t Weff, uint32_t *__restrict__ nb,
                                                    uint32_t *__restrict__ tb,
-                                                   uint32_t *__restrict__ status) {
+                                                   uint32_t *__restrict__ status,
+                                                   uint32_t *__restrict__ order = nullptr) {
   // the top level (<= 8192 elements) ranked by pointer jumping in LDS: suffix
-  // sums of nodes and sublists along the list, element 0 (the root's) first
+  // sums of nodes and sublists along the list, element 0 (the root's) first.
+  // ssub == nullptr: the elements are the sublists themselves (one each), and
+  // order[tour index] = element replaces tb (a giant document of few sublists
+  // ranks them here directly, without the walk levels)
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // next, count, sublists
   constexpr uint32_t PT = 8;  // elements per thread: S2 <= 8192
   uint32_t *nx = sm, *cn = sm + S2, *sb = sm + 2 * S2;
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
     nx[i] = snext[i];
     cn[i] = scnt[i];
-    sb[i] = ssub[i];
+    sb[i] = ssub ? ssub[i] : 1u;
   }
   __syncthreads();
   for (uint32_t round = 0; (1u << round) < 2 * S2; round++) {
@@ -1834,7 +1839,9 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
     atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
     nb[i] = n - min(cn[i], n);
-    tb[i] = Weff - min(sb[i], Weff);
+    const uint32_t t = Weff - min(sb[i], Weff);
+    if (!order) tb[i] = t;
+    else if (t < Weff) order[t] = i;
   }
 }
 
@@ -3434,10 +3441,15 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       c->x_cached = true;
       c->x_status = c->pin_small[4];
       const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
+      if (Weff <= SUP_MAX) {  // few sublists: one LDS ranking, no walk levels
+        Launch L(c, "rank", (double)Weff * 20);
+        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)Weff * 12, c->stream, wcnt, nullptr,
+                           wnext, Weff, N, Weff, sbase, nullptr, out->status, order);
+      } else {
       // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
       const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
       uint32_t K3 = 1;
-      while ((S2 + K3 - 1) / K3 > 8192) K3 <<= 1;
+      while ((S2 + K3 - 1) / K3 > SUP_MAX) K3 <<= 1;
       const uint32_t S3 = (S2 + K3 - 1) / K3;
       const bool three = K3 > 1;
       uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
@@ -3464,6 +3476,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
         }
         hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
                            ba2, bb2, Weff, sbase, nullptr, order);
+      }
       }
       if (check_launch(c, "rank")) return -1;
     } else {
@@ -3598,9 +3611,12 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
       {
         Launch L(c, "fdir", (double)N * 8 + (double)N / 6.0 * 1.0);  // ids once + directory
-        hipLaunchKernelGGL(k_fdir<1024>, dim3((uint32_t)D), dim3(1024), (size_t)SG * 16, c->stream,
-                           id_key, doc_off, SG, dir, dkmin, dgroups, out->max_ts, bt->ts_shift,
-                           out->status, big);
+        // few documents: one workgroup reads a whole large document, so keep
+        // 16 loads in flight per lane instead of 4
+        auto *fdir = D <= 64 ? k_fdir<1024, 16> : k_fdir<1024, 4>;
+        hipLaunchKernelGGL(fdir, dim3((uint32_t)D), dim3(1024),
+                           (size_t)SG * 16, c->stream, id_key, doc_off, SG, dir, dkmin, dgroups,
+                           out->max_ts, bt->ts_shift, out->status, big);
       }
       if (check_launch(c, "fdir")) return -1;
       HIPCHK(c, hipMemcpyAsync(c->pin_small, big, 8, hipMemcpyDeviceToHost, c->stream));
