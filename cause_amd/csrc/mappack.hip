@@ -583,7 +583,7 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
   // pack table, cached while the collection layout repeats
   auto &pc = c->mpack;
   const uint32_t PKN = c->map_pack == 1 ? 1024u : MPK;  // CW_MAP_PACK=1: packs of 1024 nodes
-  if (!(pc.pk == PKN && pc.off.size() == D + 1 && memcmp(pc.off.data(), off, (D + 1) * 8) == 0)) {
+  if (!(pc.pk == PKN && pc.same)) {
     pc.off.assign(off, off + D + 1);
     pc.pk = PKN;
     pc.doc0.clear();
