@@ -3180,8 +3180,10 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scan", tag);
-    if (D == 1 && t.T > 16) {
-      // one document of many tiles: chunked scan over all workgroups
+    if (D == 1 && t.T > GSCAN_CHUNK) {
+      // one document of many tiles: chunked scan over all workgroups (up to
+      // one chunk of tiles, the one-workgroup scan is a single launch instead
+      // of four)
       const uint32_t nc = (t.T + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
       uint32_t *cs = scratch_t<uint32_t>(c, "gscan_cs", (size_t)nc * nb);
       uint32_t *tot = scratch_t<uint32_t>(c, "gscan_tot", nb);
