@@ -247,6 +247,65 @@ __device__ __forceinline__ void rank_subdigit(const uint32_t (&sd)[ITEMS], uint3
   __syncthreads();
 }
 
+// rank_subdigit for many waves (k_tree_l: 16): the per-bin prefix over the
+// waves is a segmented shuffle scan over all threads (NW lanes per bin) rather
+// than one lane walking NW rows, and every wave scans the 64 bin totals itself
+// (its digits pick their bin start by a lane shuffle), so there is no serial
+// chain of NW dependent LDS round trips.  btot is [64].
+template <int NT, int ITEMS>
+__device__ __forceinline__ void rank_subdigit_par(const uint32_t (&sd)[ITEMS], uint32_t len,
+                                                  uint32_t sbits, uint32_t (&pos)[ITEMS],
+                                                  uint32_t (*wcnt)[SUB_BINS], uint32_t *btot) {
+  constexpr int NW = NT / 64;
+  static_assert(NW >= 2 && (NW & (NW - 1)) == 0 && NW <= 64, "power-of-two wave count");
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t *cw = wcnt[w];
+  cw[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (uint32_t k = 0; k < ITEMS; k++) {
+    const bool valid = wb_elem<ITEMS>(k) < len;
+    const uint32_t dd = sd[k];
+    uint64_t m = __ballot(valid);
+    for (uint32_t bit = 0; bit < sbits; bit++) {
+      const bool on = (dd >> bit) & 1u;
+      const uint64_t bb = __ballot(on);
+      m &= on ? bb : ~bb;
+    }
+    const uint32_t lr = lanes_below(m);
+    const uint32_t before = cw[dd];
+    pos[k] = before + lr;
+    __builtin_amdgcn_wave_barrier();
+    if (valid && lr == 0) cw[dd] = before + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  {
+    const uint32_t ww = threadIdx.x & (NW - 1), bn = threadIdx.x / NW;
+    const uint32_t c = wcnt[ww][bn];
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < NW; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, NW);
+      if (ww >= (uint32_t)o) x += y;
+    }
+    wcnt[ww][bn] = x - c;
+    if (ww == NW - 1) btot[bn] = x;
+  }
+  __syncthreads();
+  const uint32_t v = lane < (1u << sbits) ? btot[lane] : 0u;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  const uint32_t ex = x - v;
+#pragma unroll
+  for (uint32_t k = 0; k < ITEMS; k++) pos[k] += __shfl(ex, (int)sd[k], 64) + cw[sd[k]];
+  __syncthreads();
+}
+
 // Stable scatter of one tile by digit (key >> shift) & (2^dbits - 1).
 // vals_in == nullptr means "value = doc-local index of the element".
 // inv != nullptr (last pass only) also records each input node's rank.
@@ -900,7 +959,7 @@ __global__ __launch_bounds__(NT) void k_front(
     uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof) {
+    unsigned long long *__restrict__ tprof, uint32_t eff) {
   extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -1036,8 +1095,20 @@ __global__ __launch_bounds__(NT) void k_front(
   __syncthreads();
   stamp(1);
   // par, skind, special/hide bitmaps per 4096-rank tile, coalesced
+  // eff: a non-special's parent goes out as its effective parent (SURVEY F5:
+  // it climbs through special causes, here in LDS), so the tree need not climb
+  auto spec = [&](uint32_t x) { return ((clsA[x >> 5] | clsB[x >> 5]) >> (x & 31)) & 1u; };
   for (uint32_t r = tid; r < n; r += NT) {
-    par[base + r] = p16[r];
+    uint32_t p = p16[r];
+    if (eff) {
+      p = p < r ? p : 0u;
+      if (!spec(r))
+        while (p != 0 && spec(p)) {
+          const uint32_t pp = p16[p];
+          p = pp < p ? pp : 0u;
+        }
+    }
+    par[base + r] = p;
     const uint32_t a = (clsA[r >> 5] >> (r & 31)) & 1u, b = (clsB[r >> 5] >> (r & 31)) & 1u;
     skind[base + r] = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
   }
@@ -1409,6 +1480,400 @@ __global__ __launch_bounds__(NT) void k_tree(
     if (r0 + TILE_T < n) load_dep(r0 + TILE_T);
   }
   if (tprof && tid == 0)
+    for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+}
+
+// --- tree with its random-access tables in LDS (documents of <= tree_l_max nodes) --
+// The same two sweeps as k_tree, one document per workgroup and one workgroup
+// per CU: the last-child table of the non-special class (sweep 1) and the
+// thread table (sweep 2) are u16 arrays over the whole document in LDS, so the
+// accesses to far parents -- k_tree's random HBM line traffic, 1.3 requests a
+// node -- become LDS accesses.  What stays in HBM: the special
+// class's table fcS (specials are a minority), nsc, and fcN as written once at
+// the end of sweep 1 (sweep 2 reads it coalesced, and at random only for the
+// oldest special of a parent, whose next sibling is the parent's newest
+// non-special).  The thread table's u16 sentinel for SUCC_END is TL_END.
+constexpr uint32_t TL_END = 0xFFFFu;
+
+__host__ __device__ constexpr uint32_t tree_l_static_bytes(uint32_t nt, uint32_t tile) {
+  return 4 * tile * 4 + tile * 2 + (nt / 64) * SUB_BINS * 4 + 64 * 4 + 4;
+}
+__host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
+  return ((nmax + 31) / 32) * 8 + ((nmax + 1) / 2) * 4;  // two bitmaps + u16 table
+}
+
+// MODE (A/B knob CW_TL_MODE): bit 0 = one CAS per insert (else CAS + exchange),
+// bit 1 = the special-table reads and the next parents go out before the keys
+template <int NT, int TILE_T, bool PROF, int MODE>
+__global__ __launch_bounds__(NT) void k_tree_l(
+    const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ doc_log2k, uint32_t kbits,
+    uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+    uint32_t *__restrict__ fcN, uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
+    unsigned long long *__restrict__ tprof,
+    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first) {
+  constexpr uint32_t IT = TILE_T / NT;
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
+    if (PROF) {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      if (ph >= 0) tacc[ph] += now - tlast;
+      tlast = now;
+    }
+  };
+  stamp(-1);
+  // one tile's group-key hash: slot word = group key << HB | the head of the
+  // slot's member list (a tile index), 0 = empty; nxt: next member, TL_END
+  // ends.  The fallback sort's tkey/trank/tns and sweep 2's T live in the
+  // same buffer.
+  constexpr uint32_t HS = 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
+  static_assert(TILE_T <= (1u << HB) && 17 + HB <= 32, "slot word layout");
+  __shared__ uint32_t hbuf[3 * TILE_T > 2 * HS ? 3 * TILE_T : 2 * HS];
+  __shared__ uint16_t nxt[TILE_T];
+  uint32_t *const hw = hbuf, *const hk = hbuf, *const hh = hbuf + HS;  // MODE 1 / MODE 0
+  uint32_t *const tkey = hbuf, *const trank = hbuf + TILE_T, *const tns = hbuf + 2 * TILE_T;
+  uint32_t *const ptab = tns;
+  __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
+  __shared__ uint32_t run[64];
+  __shared__ uint32_t n_osp;
+  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
+  const uint32_t d = blockIdx.x, tid = threadIdx.x;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  uint32_t *const spec_bm = bm, *const hide_bm = bm + bm_words;
+  uint16_t *const tab = reinterpret_cast<uint16_t *>(bm + 2 * bm_words);
+  const uint32_t nw = (n + 31) >> 5;
+  if (kbm) {
+    const uint32_t *src = kbm + (size_t)tile_first[d] * KBM_WORDS;
+    for (uint32_t wi = tid; wi < nw; wi += NT) {
+      const uint32_t *tw = src + (size_t)(wi >> 7) * KBM_WORDS + (wi & 127);
+      spec_bm[wi] = tw[0];
+      hide_bm[wi] = tw[TILE / 32];
+    }
+  } else {
+    for (uint32_t rb = (tid >> 6) << 6; rb < n; rb += NT) {
+      const uint32_t r = rb + (tid & 63);
+      const uint8_t kd = r < n ? skind[base + r] : 0;
+      const uint64_t sm = __ballot(r < n && is_special(kd));
+      const uint64_t hm = __ballot(r < n && is_hide(kd));
+      if ((tid & 63) == 0) {
+        spec_bm[rb >> 5] = (uint32_t)sm;
+        hide_bm[rb >> 5] = (uint32_t)hm;
+        if ((rb >> 5) + 1 < nw) {
+          spec_bm[(rb >> 5) + 1] = (uint32_t)(sm >> 32);
+          hide_bm[(rb >> 5) + 1] = (uint32_t)(hm >> 32);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  stamp(0);
+  auto special_at = [&](uint32_t r) -> bool { return (spec_bm[r >> 5] >> (r & 31)) & 1u; };
+  auto hide_at = [&](uint32_t r) -> bool { return (hide_bm[r >> 5] >> (r & 31)) & 1u; };
+  uint32_t qpar[IT];
+  auto load_par = [&](uint32_t r0) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t r = r0 + wb_elem<IT>(k);
+      qpar[k] = r < n ? par[base + r] : 0u;
+    }
+  };
+  // sweep 1: group keys, next siblings, last-child tables.  A group (effective
+  // parent, class) rarely has more than one member in a tile: members are
+  // hashed by key into per-slot lists; a member's next sibling is the largest
+  // smaller member of its list, or the group's last node of earlier tiles
+  // (tab / fcS); the list's largest member updates the table.  A tile with a
+  // group of more than GMAX members (e.g. many children of the root) is
+  // sorted by group key instead, as in k_tree.
+  auto clear_hash = [&]() {
+    for (uint32_t i = tid; i < HS; i += NT) {
+      hw[i] = 0;
+      if (!(MODE & 1)) hh[i] = TL_END;
+    }
+  };
+  clear_hash();
+  if (tid == 0) n_osp = 0;
+  load_par(0);
+  __syncthreads();
+  for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
+    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+    uint32_t key[IT], cpar[IT], ptv[IT], ptvS[IT], slot[IT];
+    bool rdS[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) cpar[k] = qpar[k];
+    // specials keep their cause: their table reads are unconditional (a node
+    // without one reads entry 0), so no later wait has to be conservative
+    auto load_ptvS = [&]() {
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = wb_elem<IT>(k), r = r0 + j, c = cpar[k] < r ? cpar[k] : 0u;
+        rdS[k] = j < len && r > 0 && c < r0 && special_at(r);
+        ptvS[k] = fcS[base + (rdS[k] ? c : 0u)];
+      }
+      if (r0 + TILE_T < n) load_par(r0 + TILE_T);
+    };
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) ptv[k] = 0;
+    if (MODE & 2) load_ptvS();
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = wb_elem<IT>(k), r = r0 + j;
+      key[k] = 0;
+      if (j < len) {
+        tab[r] = 0;
+        fcS[base + r] = 0;
+      }
+      if (j < len && r > 0) {
+        const bool sp = special_at(r);
+        uint32_t c = cpar[k];
+        c = c < r ? c : 0u;
+        if (!sp)
+          while (c != 0 && special_at(c)) {
+            const uint32_t pc = par[base + c];
+            c = pc < c ? pc : 0u;
+          }
+        key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
+        if (!sp) ptv[k] = c < r0 ? (uint32_t)tab[c] : 0u;
+      }
+    }
+    if (!(MODE & 2)) load_ptvS();
+    // insert: claim the key's slot (linear probing), push onto its list
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = wb_elem<IT>(k), kk = key[k];
+      slot[k] = 0;
+      if (j < len && kk) {
+        uint32_t h = (kk * 0x9E3779B1u) >> (32 - __builtin_ctz(HS)), cmp = 0u;
+        if (MODE & 1) {
+          for (;;) {  // one CAS for a new group; pushes onto a group's list retry
+            const uint32_t old = atomicCAS(&hw[h], cmp, (kk << HB) | j);
+            if (old == cmp) {
+              nxt[j] = (uint16_t)(cmp ? (cmp & ((1u << HB) - 1)) : TL_END);
+              break;
+            }
+            if ((old >> HB) == kk) {
+              cmp = old;
+            } else {
+              h = (h + 1) & (HS - 1);
+              cmp = 0u;
+            }
+          }
+        } else {
+          for (;;) {  // claim the key (hk), then push (exchange on hh)
+            const uint32_t old = atomicCAS(&hk[h], 0u, kk);
+            if (old == 0u || old == kk) break;
+            h = (h + 1) & (HS - 1);
+          }
+          nxt[j] = (uint16_t)atomicExch(&hh[h], j);
+        }
+        slot[k] = h;
+      }
+    }
+    __syncthreads();
+    stamp(1);
+    // walk the slot's list: prv1 = 1 + the largest smaller member (0: none)
+    uint32_t prv1[IT];
+    bool last[IT], big = false;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = wb_elem<IT>(k);
+      uint32_t x = !(j < len && key[k]) ? TL_END : (MODE & 1) ? (hw[slot[k]] & ((1u << HB) - 1)) : hh[slot[k]];
+      uint32_t p1 = 0, steps = 0;
+      bool ls = true;
+#pragma unroll 1
+      for (; x != TL_END && steps <= GMAX; steps++) {
+        p1 = x < j ? max(p1, x + 1) : p1;
+        ls = ls && x <= j;
+        x = nxt[x];
+      }
+      big |= x != TL_END;
+      prv1[k] = p1;
+      last[k] = ls;
+    }
+    if (__syncthreads_or(big)) {
+      // fallback: stable LDS sort of the tile by group key (k_tree's sweep 1)
+      uint32_t rk[IT], sd[IT], pos[IT];
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) rk[k] = wb_elem<IT>(k);
+      for (uint32_t shift = 0; shift < kbits; shift += SUB_BITS) {
+#pragma unroll
+        for (uint32_t k = 0; k < IT; k++) sd[k] = (key[k] >> shift) & (SUB_BINS - 1);
+        rank_subdigit<NT, IT>(sd, len, min(SUB_BITS, kbits - shift), pos, wcnt, run);
+#pragma unroll
+        for (uint32_t k = 0; k < IT; k++)
+          if (wb_elem<IT>(k) < len) {
+            tkey[pos[k]] = key[k];
+            trank[pos[k]] = rk[k];
+          }
+        if (shift + SUB_BITS >= kbits) {
+#pragma unroll
+          for (uint32_t k = 0; k < IT; k++) ptab[wb_elem<IT>(k)] = rdS[k] ? ptvS[k] : ptv[k];
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t k = 0; k < IT; k++) {
+          const uint32_t j = wb_elem<IT>(k);
+          if (j < len) {
+            key[k] = tkey[j];
+            rk[k] = trank[j];
+          }
+        }
+        __syncthreads();
+      }
+      uint32_t pv[IT];
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = wb_elem<IT>(k);
+        const uint32_t kk = key[k];
+        pv[k] = 0;
+        if (j < len && kk != 0) pv[k] = (j > 0 && tkey[j - 1] == kk) ? r0 + trank[j - 1] : ptab[rk[k]];
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++)
+        if (wb_elem<IT>(k) < len) {
+          const uint32_t kk = key[k], e = (kk >> 1) - 1;
+          tns[rk[k]] = pv[k] ? pv[k] : (NSC_UP | e);
+          if (kk && !(kk & 1) && !pv[k]) osp[base + atomicAdd(&n_osp, 1u)] = ((r0 + rk[k]) << 16) | e;
+        }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = wb_elem<IT>(k);
+        if (j >= len) continue;
+        const uint32_t kk = key[k];
+        if (kk != 0 && !(j + 1 < len && tkey[j + 1] == kk)) {
+          const uint32_t e = (kk >> 1) - 1, v = r0 + rk[k];
+          if (kk & 1) tab[e] = (uint16_t)v;
+          else fcS[base + e] = v;
+        }
+      }
+      for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
+      __syncthreads();
+      clear_hash();
+    } else {
+#pragma unroll
+      for (uint32_t k = 0; k < IT; k++) {
+        const uint32_t j = wb_elem<IT>(k), r = r0 + j, kk = key[k];
+        if (j >= len) continue;
+        const uint32_t e = (kk >> 1) - 1;
+        const uint32_t pv = prv1[k] ? r0 + prv1[k] - 1 : (rdS[k] ? ptvS[k] : ptv[k]);
+        nsc[base + r] = kk == 0 ? 0u : (pv ? pv : (NSC_UP | e));
+        if (kk && !(kk & 1) && !pv) osp[base + atomicAdd(&n_osp, 1u)] = (r << 16) | e;
+        if (kk && last[k]) {
+          if (kk & 1) tab[e] = (uint16_t)r;
+          else fcS[base + e] = r;
+        }
+        if (kk) {
+          hw[slot[k]] = 0;
+          if (!(MODE & 1)) hh[slot[k]] = TL_END;
+        }
+      }
+    }
+    __syncthreads();
+    stamp(3);
+  }
+  // the newest non-special children go out once (sweep 2 reads them back
+  // coalesced; the oldest specials' parents at random)
+  // the oldest special child's next sibling is its parent's newest
+  // non-special (weave-later?): patched into nsc now that tab is final
+  for (uint32_t r = tid; r < n; r += NT) fcN[base + r] = tab[r];
+  for (uint32_t i = tid; i < n_osp; i += NT) {
+    const uint32_t v = osp[base + i], f = tab[v & 0xFFFFu];
+    if (f) nsc[base + (v >> 16)] = f;
+  }
+  __syncthreads();
+  // sweep 2: preorder successors; thr(r) = ns(r) ?: thr(e(r)) with the earlier
+  // tiles' threads in tab (u16) and this tile's resolved by pointer jumping.
+  // Tile loads run two tiles ahead.
+  constexpr uint32_t RES = 0x80000000u;
+  uint32_t *const T = tkey;
+  struct Q {
+    uint32_t fs[IT], fn[IT], ns[IT];
+  };
+  auto load_tile = [&](Q &q, uint32_t r0) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t r = r0 + k * NT + tid;
+      const bool ok = r < n;
+      q.fs[k] = ok ? fcS[base + r] : 0u;
+      q.fn[k] = ok ? fcN[base + r] : 0u;
+      q.ns[k] = ok ? nsc[base + r] : 0u;
+    }
+  };
+  // one tile: X holds its loads (and is refilled with tile r0 + 2 TILE_T)
+  auto tile2 = [&](uint32_t r0, Q &X) {
+    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+    uint32_t flg[IT], fcr[IT];
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid, r = r0 + j;
+      flg[k] = 0;
+      fcr[k] = X.fs[k] ? X.fs[k] : X.fn[k];
+      if (j >= len) continue;
+      const bool sp = special_at(r);
+      uint32_t tv;
+      if (r == 0) {
+        tv = RES | SUCC_END;
+      } else {
+        uint32_t ns = X.ns[k], e = 0;
+        if (ns & NSC_UP) {
+          e = ns & ~NSC_UP;
+          ns = 0;
+        }
+        if (ns) {
+          tv = RES | ns;
+        } else if (e >= r0) {
+          tv = e - r0;
+        } else {
+          const uint32_t t = tab[e];
+          tv = RES | (t == TL_END ? SUCC_END : t);
+        }
+      }
+      T[j] = tv;
+      const uint32_t fs = X.fs[k];
+      const bool vis = !sp && r != 0 && !(fs && hide_at(fs));
+      const bool split = r == split_node(d, r >> log2k, log2k, n);
+      flg[k] = (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
+    }
+    if (r0 + 2 * TILE_T < n) load_tile(X, r0 + 2 * TILE_T);
+    __syncthreads();
+    stamp(5);
+    // pointer jumping without barriers: every value in T is an ancestor's
+    // pointer or a resolved thread at any time, so a lane may read its
+    // target's entry whenever it likes; each lane stops when its own entries
+    // are resolved (targets are smaller indices of the same tile)
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid;
+      if (j < len) {
+        uint32_t t = T[j];
+        while (!(t & RES)) {
+          t = T[t];
+          T[j] = t;
+        }
+      }
+    }
+    __syncthreads();
+    stamp(6);
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = k * NT + tid, r = r0 + j;
+      if (j >= len) continue;
+      const uint32_t th = T[j] & ~RES;
+      tab[r] = (uint16_t)(th == SUCC_END ? TL_END : th);
+      link[base + r] = (fcr[k] ? fcr[k] : th) | flg[k];
+    }
+    __syncthreads();
+    stamp(7);
+  };
+  Q qa, qb;
+  load_tile(qa, 0);
+  if (TILE_T < n) load_tile(qb, TILE_T);
+  stamp(4);
+  for (uint32_t r0 = 0; r0 < n; r0 += 2 * TILE_T) {
+    tile2(r0, qa);
+    if (r0 + TILE_T < n) tile2(r0 + TILE_T, qb);
+  }
+  if (PROF && tid == 0)
     for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
 }
 
@@ -2838,6 +3303,9 @@ struct cw_ctx {
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
   uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
+  uint32_t tree_l = 1;             // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits
+  uint32_t tl_mode = 0;            // CW_TL_MODE: k_tree_l variant bits (A/B)
+  uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
@@ -3347,8 +3815,40 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 8);
       HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
     }
-    Launch L(c, "tree", (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
-    if (c->tree_cfg == 2)
+    constexpr uint32_t TL_NT = 1024;
+    const uint32_t tl_dyn = tree_l_lds_bytes(t.nmax);
+    // k_tree_l with 2,048-rank tiles, or 1,024 when the document needs the room
+    const uint32_t tree_l = !c->tree_l || c->tree_pad ? 0
+                            : tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= 160 * 1024 ? 2048
+                            : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= 160 * 1024 ? 1024 : 0;
+    // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4, fcN 4 out; sweep 2 reads
+    // fcS, fcN, nsc (12) and writes link 4
+    Launch L(c, "tree", tree_l ? (double)N * (4 + 1 + 4 + 4 + 4 + 12 + 4)
+                               : (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
+    auto tree_l_kernel = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(TL_NT), (size_t)tl_dyn, c->stream, par, skind,
+                         doc_off, doc_log2k, kbits, (t.nmax + 31) / 32, nsc, fcS, fcN,
+                         (uint32_t *)link, thr, tprof, kbm, dev_tab(c, "t_tile_first"));
+    };
+    auto tree_l_mode = [&](auto prof, auto mode) {
+      constexpr bool P = decltype(prof)::value;
+      constexpr int M = decltype(mode)::value;
+      if (tree_l == 2048) tree_l_kernel(k_tree_l<TL_NT, 2048, P, M>);
+      else tree_l_kernel(k_tree_l<TL_NT, 1024, P, M>);
+    };
+    auto tree_l_prof = [&](auto prof) {
+      switch (c->tl_mode & 3) {
+        case 0: tree_l_mode(prof, std::integral_constant<int, 0>()); break;
+        case 1: tree_l_mode(prof, std::integral_constant<int, 1>()); break;
+        case 2: tree_l_mode(prof, std::integral_constant<int, 2>()); break;
+        default: tree_l_mode(prof, std::integral_constant<int, 3>()); break;
+      }
+    };
+    if (tree_l) {
+      if (tprof) tree_l_prof(std::true_type());
+      else tree_l_prof(std::false_type());
+    }
+    else if (c->tree_cfg == 2)
       hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
                          (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
                          kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
@@ -3388,8 +3888,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     for (uint64_t d = 0; d < D; d++)
       for (int ph = 0; ph < 8; ph++) acc[ph] += (double)h[d * 8 + ph];
     fprintf(stderr, "tree phases (memtime ticks per doc): bitmap %.0f climb %.0f sort %.0f prv %.0f "
-            "s2load %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
-            acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D);
+            "s2load %.0f s2calc %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
+            acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D, acc[7] / D);
   }
 
   if (t.tour && !giant) {
@@ -3578,7 +4078,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            (size_t)front_lds_bytes(t.nmax, FRONT_FUSED_SG), c->stream, id_key,
                            cause_key, kind, doc_off, dev_tab(c, "t_tile_first"), FRONT_FUSED_SG, par,
                            skind, sval, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status, big,
-                           tprof_f);
+                           tprof_f, c->front_eff);
       }
       if (check_launch(c, "front")) return -1;
       if (tprof_f) {
@@ -4802,6 +5302,9 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->tree_pad = knob("CW_TREE_PAD", 0);
+  c->tree_l = knob("CW_TREE_L", 1);
+  c->tl_mode = knob("CW_TL_MODE", 0);
+  c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
   c->map_pack = knob("CW_MAP_PACK", 0);

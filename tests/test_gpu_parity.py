@@ -27,7 +27,8 @@ FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"},
           "front3": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0", "CW_FRONT_FUSED": "0"},
           "radix": {"CW_FRONT": "0"},
           "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"},  # no LDS pack sorts
-          "hbm-walk": {"CW_TOUR": "0"}}  # walk + rank + emit instead of the LDS tour
+          "hbm-walk": {"CW_TOUR": "0"},  # walk + rank + emit instead of the LDS tour
+          "hbm-tree": {"CW_TREE_L": "0"}}  # k_tree, tables in HBM
 
 
 @pytest.fixture(scope="module", params=sorted(FRONTS))
@@ -198,6 +199,45 @@ def test_all_caused_by_root(weaver):
                 method=oracle.METHOD_LINKED)
 
 
+def _sibling_group_doc(rng, n, sizes):
+    """Runs of g consecutive ids caused by one earlier node, g drawn from
+    ``sizes``: sibling groups of every size around k_tree_l's per-tile hash
+    list limit (16) and across its tile boundaries, with hides and shows
+    among them so both classes form groups."""
+    s = "aaaaaaaaaaaaa"
+    doc = [R.ROOT_NODE]
+    normal = [R.ROOT_ID]
+    t = 1
+    while t < n:
+        g = rng.choice(sizes)
+        parent = rng.choice(normal[-64:] if rng.random() < 0.5 else normal)
+        for _ in range(g):
+            if t >= n:
+                break
+            nid = (t, s, 0)
+            u = rng.random()
+            if u < 0.15 and parent != R.ROOT_ID:
+                doc.append((nid, parent, R.HIDE))
+            elif u < 0.2 and parent != R.ROOT_ID:
+                doc.append((nid, parent, R.H_SHOW))
+            else:
+                doc.append((nid, parent, "x"))
+                normal.append(nid)
+            t += 1
+    rng.shuffle(doc)
+    return doc
+
+
+def test_sibling_groups_of_every_size(weaver):
+    rng = random.Random(11)
+    docs = [_sibling_group_doc(rng, n, sizes)
+            for n, sizes in ((5000, (1, 2, 3)), (9000, (15, 16, 17, 18)), (12_000, (1, 2, 40, 100)),
+                             (3000, (2047, 2048, 2049)), (20_000, (1, 1, 1, 5, 16, 33)))]
+    b = pack.pack_lists(docs)
+    check_batch(weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout,
+                method=oracle.METHOD_LINKED)
+
+
 def test_repeat_calls_are_identical(weaver):
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000)
     off, idk, ck, kd = gen.generate(spec, 0, 30)
@@ -257,7 +297,11 @@ KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2C
          {"CW_MAX_DIGIT": "8"}, dict(_W, CW_WALK_THREADS="256", CW_WALK_SPAN="512"),
          dict(_W, CW_WALK_THREADS="1024", CW_WALK_SPAN="2048"),
          {"CW_TOUR_LOG2K": "3"}, {"CW_TOUR_LOG2K": "4"}, {"CW_TOUR_LOG2K": "7"},
-         {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"}, {"CW_TREE": "0"}, {"CW_TREE": "1"}]
+         {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"},
+         # the tree: k_tree (tables in HBM) and its geometries, k_tree_l's A/B modes,
+         # raw parents from the front end (the tree climbs)
+         {"CW_TREE_L": "0"}, {"CW_TREE_L": "0", "CW_TREE": "0"}, {"CW_TREE_L": "0", "CW_TREE": "1"},
+         {"CW_TL_MODE": "1"}, {"CW_TL_MODE": "2"}, {"CW_TL_MODE": "3"}, {"CW_FRONT_EFF": "1"}]
 
 
 @pytest.mark.parametrize("n", [59_204, 60_000, 65_534, 65_535])
