@@ -1480,7 +1480,7 @@ __global__ __launch_bounds__(NT) void k_tree(
     if (r0 + TILE_T < n) load_dep(r0 + TILE_T);
   }
   if (tprof && tid == 0)
-    for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+    for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 16 + ph] = tacc[ph];
 }
 
 // --- tree with its random-access tables in LDS (documents of <= tree_l_max nodes) --
@@ -1513,7 +1513,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     unsigned long long *__restrict__ tprof,
     const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first) {
   constexpr uint32_t IT = TILE_T / NT;
-  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+  unsigned long long tacc[16] = {}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (PROF) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -1600,6 +1600,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     bool rdS[IT];
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) cpar[k] = qpar[k];
+    stamp(8);
     // specials keep their cause: their table reads are unconditional (a node
     // without one reads entry 0), so no later wait has to be conservative
     auto load_ptvS = [&]() {
@@ -1635,7 +1636,9 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         if (!sp) ptv[k] = c < r0 ? (uint32_t)tab[c] : 0u;
       }
     }
+    stamp(9);
     if (!(MODE & 2)) load_ptvS();
+    stamp(10);
     // insert: claim the key's slot (linear probing), push onto its list
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
@@ -1668,6 +1671,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         slot[k] = h;
       }
     }
+    stamp(11);
     __syncthreads();
     stamp(1);
     // walk the slot's list: prv1 = 1 + the largest smaller member (0: none)
@@ -1689,7 +1693,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       prv1[k] = p1;
       last[k] = ls;
     }
-    if (__syncthreads_or(big)) {
+    stamp(12);
+    const bool any_big = __syncthreads_or(big);
+    stamp(13);
+    if (any_big) {
       // fallback: stable LDS sort of the tile by group key (k_tree's sweep 1)
       uint32_t rk[IT], sd[IT], pos[IT];
 #pragma unroll
@@ -1749,6 +1756,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
       __syncthreads();
       clear_hash();
+      __syncthreads();
     } else {
 #pragma unroll
       for (uint32_t k = 0; k < IT; k++) {
@@ -1767,8 +1775,8 @@ __global__ __launch_bounds__(NT) void k_tree_l(
           if (!(MODE & 1)) hh[slot[k]] = TL_END;
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
     stamp(3);
   }
   // the newest non-special children go out once (sweep 2 reads them back
@@ -1785,7 +1793,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   // tiles' threads in tab (u16) and this tile's resolved by pointer jumping.
   // Tile loads run two tiles ahead.
   constexpr uint32_t RES = 0x80000000u;
-  uint32_t *const T = tkey;
+  uint32_t *const T = hbuf;
   struct Q {
     uint32_t fs[IT], fn[IT], ns[IT];
   };
@@ -1874,7 +1882,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     if (r0 + TILE_T < n) tile2(r0 + TILE_T, qb);
   }
   if (PROF && tid == 0)
-    for (int ph = 0; ph < 8; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+    for (int ph = 0; ph < 16; ph++) tprof[(size_t)d * 16 + ph] = tacc[ph];
 }
 
 // --- tree for one giant document (all tiles in parallel) -------------------------
@@ -3812,8 +3820,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     // and the tables back
     unsigned long long *tprof = nullptr;
     if (c->tree_prof) {
-      tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 8);
-      HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 64, c->stream));
+      tprof = scratch_t<unsigned long long>(c, "tprof", (size_t)D * 16);
+      HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)D * 128, c->stream));
     }
     constexpr uint32_t TL_NT = 1024;
     const uint32_t tl_dyn = tree_l_lds_bytes(t.nmax);
@@ -3881,15 +3889,17 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   }
   if (check_launch(c, "tree")) return -1;
   if (c->tree_prof && !giant) {
-    std::vector<unsigned long long> h((size_t)D * 8);
+    std::vector<unsigned long long> h((size_t)D * 16);
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 64, hipMemcpyDeviceToHost));
-    double acc[8] = {0};
+    HIPCHK(c, hipMemcpy(h.data(), c->bufs["tprof"].p, (size_t)D * 128, hipMemcpyDeviceToHost));
+    double acc[16] = {0};
     for (uint64_t d = 0; d < D; d++)
-      for (int ph = 0; ph < 8; ph++) acc[ph] += (double)h[d * 8 + ph];
-    fprintf(stderr, "tree phases (memtime ticks per doc): bitmap %.0f climb %.0f sort %.0f prv %.0f "
-            "s2load %.0f s2calc %.0f jump %.0f s2write %.0f\n", acc[0] / D, acc[1] / D, acc[2] / D,
-            acc[3] / D, acc[4] / D, acc[5] / D, acc[6] / D, acc[7] / D);
+      for (int ph = 0; ph < 16; ph++) acc[ph] += (double)h[d * 16 + ph];
+    // k_tree: bitmap climb sort prv s2load jump s2write; k_tree_l: bitmap barA . end
+    // s2init s2calc jump s2write head keys issue insert walk barB
+    fprintf(stderr, "tree phases (memtime ticks per doc):");
+    for (int ph = 0; ph < 16; ph++) fprintf(stderr, " %d:%.0f", ph, acc[ph] / D);
+    fprintf(stderr, "\n");
   }
 
   if (t.tour && !giant) {
