@@ -13,7 +13,7 @@ import os
 import re
 import sys
 
-ALIAS = {"pack_bits": "packbits"}
+ALIAS = {"pack_bits": "packbits", "tree_l": "tree"}  # k_tree_l is the library's "tree" stat
 
 
 def stat_name(sym):
