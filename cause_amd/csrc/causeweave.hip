@@ -1594,8 +1594,11 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   if (tid == 0) n_osp = 0;
   load_par(0);
   __syncthreads();
-  for (uint32_t r0 = 0; r0 < n; r0 += TILE_T) {
-    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+  // full tiles and the document's last, partial tile compile separately (the
+  // guards of a full tile fold away)
+  auto tile1 = [&](uint32_t r0, auto fullc) {
+    constexpr bool F = decltype(fullc)::value;
+    const uint32_t len = F ? TILE_T : min((uint32_t)TILE_T, n - r0);
     uint32_t key[IT], cpar[IT], ptv[IT], ptvS[IT], slot[IT];
     bool rdS[IT];
 #pragma unroll
@@ -1778,7 +1781,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       __syncthreads();
     }
     stamp(3);
-  }
+  };
+  uint32_t r0t = 0;
+  for (; r0t + TILE_T <= n; r0t += TILE_T) tile1(r0t, std::true_type());
+  if (r0t < n) tile1(r0t, std::false_type());
   // the newest non-special children go out once (sweep 2 reads them back
   // coalesced; the oldest specials' parents at random)
   // the oldest special child's next sibling is its parent's newest
@@ -1808,8 +1814,9 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     }
   };
   // one tile: X holds its loads (and is refilled with tile r0 + 2 TILE_T)
-  auto tile2 = [&](uint32_t r0, Q &X) {
-    const uint32_t len = min((uint32_t)TILE_T, n - r0);
+  auto tile2f = [&](uint32_t r0, Q &X, auto fullc) {
+    constexpr bool F = decltype(fullc)::value;
+    const uint32_t len = F ? TILE_T : min((uint32_t)TILE_T, n - r0);
     uint32_t flg[IT], fcr[IT];
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
@@ -1872,6 +1879,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     }
     __syncthreads();
     stamp(7);
+  };
+  auto tile2 = [&](uint32_t r0, Q &X) {
+    if (r0 + TILE_T <= n) tile2f(r0, X, std::true_type());
+    else tile2f(r0, X, std::false_type());
   };
   Q qa, qb;
   load_tile(qa, 0);
