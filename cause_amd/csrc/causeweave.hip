@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1495,6 +1496,15 @@ __global__ __launch_bounds__(NT) void k_tree(
 // non-special).  The thread table's u16 sentinel for SUCC_END is TL_END.
 constexpr uint32_t TL_END = 0xFFFFu;
 
+// Element i of a wave-uniform base pointer, addressed as base + zext(4 i): the
+// global access takes the scalar base and a 32-bit lane offset (saddr form), no
+// 64-bit address arithmetic per lane.
+template <typename T>
+__device__ __forceinline__ T &lane_at(T *b, uint32_t i) {
+  using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return *reinterpret_cast<T *>(reinterpret_cast<C *>(b) + (size_t)(i * (uint32_t)sizeof(T)));
+}
+
 __host__ __device__ constexpr uint32_t tree_l_static_bytes(uint32_t nt, uint32_t tile) {
   return 4 * tile * 4 + tile * 2 + (nt / 64) * SUB_BINS * 4 + 64 * 4 + 4;
 }
@@ -1539,6 +1549,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
   const uint32_t d = blockIdx.x, tid = threadIdx.x;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  // this document's slices (wave-uniform bases, lane offsets: lane_at)
+  const uint32_t *const parD = par + base;
+  uint32_t *const fcSD = fcS + base, *const fcND = fcN + base, *const nscD = nsc + base;
+  uint32_t *const linkD = link + base, *const ospD = osp + base;
   uint32_t *const spec_bm = bm, *const hide_bm = bm + bm_words;
   uint16_t *const tab = reinterpret_cast<uint16_t *>(bm + 2 * bm_words);
   const uint32_t nw = (n + 31) >> 5;
@@ -1574,7 +1588,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + wb_elem<IT>(k);
-      qpar[k] = r < n ? par[base + r] : 0u;
+      qpar[k] = r < n ? lane_at(parD, r) : 0u;
     }
   };
   // sweep 1: group keys, next siblings, last-child tables.  A group (effective
@@ -1611,7 +1625,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       for (uint32_t k = 0; k < IT; k++) {
         const uint32_t j = wb_elem<IT>(k), r = r0 + j, c = cpar[k] < r ? cpar[k] : 0u;
         rdS[k] = j < len && r > 0 && c < r0 && special_at(r);
-        ptvS[k] = fcS[base + (rdS[k] ? c : 0u)];
+        ptvS[k] = lane_at(fcSD, rdS[k] ? c : 0u);
       }
       if (r0 + TILE_T < n) load_par(r0 + TILE_T);
     };
@@ -1624,7 +1638,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       key[k] = 0;
       if (j < len) {
         tab[r] = 0;
-        fcS[base + r] = 0;
+        lane_at(fcSD, r) = 0;
       }
       if (j < len && r > 0) {
         const bool sp = special_at(r);
@@ -1632,7 +1646,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         c = c < r ? c : 0u;
         if (!sp)
           while (c != 0 && special_at(c)) {
-            const uint32_t pc = par[base + c];
+            const uint32_t pc = lane_at(parD, c);
             c = pc < c ? pc : 0u;
           }
         key[k] = ((c + 1) << 1) | (sp ? 0u : 1u);
@@ -1742,7 +1756,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         if (wb_elem<IT>(k) < len) {
           const uint32_t kk = key[k], e = (kk >> 1) - 1;
           tns[rk[k]] = pv[k] ? pv[k] : (NSC_UP | e);
-          if (kk && !(kk & 1) && !pv[k]) osp[base + atomicAdd(&n_osp, 1u)] = ((r0 + rk[k]) << 16) | e;
+          if (kk && !(kk & 1) && !pv[k]) lane_at(ospD, atomicAdd(&n_osp, 1u)) = ((r0 + rk[k]) << 16) | e;
         }
       __syncthreads();
 #pragma unroll
@@ -1753,10 +1767,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         if (kk != 0 && !(j + 1 < len && tkey[j + 1] == kk)) {
           const uint32_t e = (kk >> 1) - 1, v = r0 + rk[k];
           if (kk & 1) tab[e] = (uint16_t)v;
-          else fcS[base + e] = v;
+          else lane_at(fcSD, e) = v;
         }
       }
-      for (uint32_t j = tid; j < len; j += NT) nsc[base + r0 + j] = tns[j];
+      for (uint32_t j = tid; j < len; j += NT) lane_at(nscD, r0 + j) = tns[j];
       __syncthreads();
       clear_hash();
       __syncthreads();
@@ -1767,11 +1781,11 @@ __global__ __launch_bounds__(NT) void k_tree_l(
         if (j >= len) continue;
         const uint32_t e = (kk >> 1) - 1;
         const uint32_t pv = prv1[k] ? r0 + prv1[k] - 1 : (rdS[k] ? ptvS[k] : ptv[k]);
-        nsc[base + r] = kk == 0 ? 0u : (pv ? pv : (NSC_UP | e));
-        if (kk && !(kk & 1) && !pv) osp[base + atomicAdd(&n_osp, 1u)] = (r << 16) | e;
+        lane_at(nscD, r) = kk == 0 ? 0u : (pv ? pv : (NSC_UP | e));
+        if (kk && !(kk & 1) && !pv) lane_at(ospD, atomicAdd(&n_osp, 1u)) = (r << 16) | e;
         if (kk && last[k]) {
           if (kk & 1) tab[e] = (uint16_t)r;
-          else fcS[base + e] = r;
+          else lane_at(fcSD, e) = r;
         }
         if (kk) {
           hw[slot[k]] = 0;
@@ -1789,10 +1803,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   // coalesced; the oldest specials' parents at random)
   // the oldest special child's next sibling is its parent's newest
   // non-special (weave-later?): patched into nsc now that tab is final
-  for (uint32_t r = tid; r < n; r += NT) fcN[base + r] = tab[r];
+  for (uint32_t r = tid; r < n; r += NT) lane_at(fcND, r) = tab[r];
   for (uint32_t i = tid; i < n_osp; i += NT) {
-    const uint32_t v = osp[base + i], f = tab[v & 0xFFFFu];
-    if (f) nsc[base + (v >> 16)] = f;
+    const uint32_t v = lane_at(ospD, i), f = tab[v & 0xFFFFu];
+    if (f) lane_at(nscD, (v >> 16)) = f;
   }
   __syncthreads();
   // sweep 2: preorder successors; thr(r) = ns(r) ?: thr(e(r)) with the earlier
@@ -1808,9 +1822,9 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + k * NT + tid;
       const bool ok = r < n;
-      q.fs[k] = ok ? fcS[base + r] : 0u;
-      q.fn[k] = ok ? fcN[base + r] : 0u;
-      q.ns[k] = ok ? nsc[base + r] : 0u;
+      q.fs[k] = ok ? lane_at(fcSD, r) : 0u;
+      q.fn[k] = ok ? lane_at(fcND, r) : 0u;
+      q.ns[k] = ok ? lane_at(nscD, r) : 0u;
     }
   };
   // one tile: X holds its loads (and is refilled with tile r0 + 2 TILE_T)
@@ -1875,7 +1889,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       if (j >= len) continue;
       const uint32_t th = T[j] & ~RES;
       tab[r] = (uint16_t)(th == SUCC_END ? TL_END : th);
-      link[base + r] = (fcr[k] ? fcr[k] : th) | flg[k];
+      lane_at(linkD, r) = (fcr[k] ? fcr[k] : th) | flg[k];
     }
     __syncthreads();
     stamp(7);
