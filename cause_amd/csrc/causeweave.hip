@@ -976,6 +976,11 @@ __global__ __launch_bounds__(NT) void k_front(
   __shared__ uint32_t bst;
   const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, nw = (n + 31) / 32;
+  const uint64_t *const idD = id_key + base, *const causeD = cause_key + base;
+  const uint8_t *const kindD = kind + base;
+  uint16_t *const rankD = rank16 + base;
+  uint32_t *const parD = par + base, *const svalD = sval + base;
+  uint8_t *const skindD = skind + base;
   if (n == 0) return;
   uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
   uint16_t *p16 = reinterpret_cast<uint16_t *>(sdir + sg);  // par, then sval, by rank
@@ -994,7 +999,7 @@ __global__ __launch_bounds__(NT) void k_front(
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t i = i0 + u * NT;
-      x[u] = i < n ? id_key[base + i] : 0ull;
+      x[u] = i < n ? lane_at(idD, i) : 0ull;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
@@ -1049,9 +1054,9 @@ __global__ __launch_bounds__(NT) void k_front(
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t i = i0 + u * NT;
-      qk[u] = i < n ? id_key[base + i] : 0ull;
-      qc[u] = i < n ? cause_key[base + i] : 0ull;
-      qd[u] = i < n ? kind[base + i] : 0;
+      qk[u] = i < n ? lane_at(idD, i) : 0ull;
+      qc[u] = i < n ? lane_at(causeD, i) : 0ull;
+      qd[u] = i < n ? lane_at(kindD, i) : 0;
     }
   };
   load_group(tid);
@@ -1089,7 +1094,7 @@ __global__ __launch_bounds__(NT) void k_front(
         if (cls & 1) atomicOr(&clsA[r >> 5], 1u << (r & 31));
         if (cls & 2) atomicOr(&clsB[r >> 5], 1u << (r & 31));
       }
-      rank16[base + i] = (uint16_t)min(r, 0xFFFFu);
+      lane_at(rankD, i) = (uint16_t)min(r, 0xFFFFu);
     }
   }
   if (st) atomicOr(&bst, st);
@@ -1109,9 +1114,9 @@ __global__ __launch_bounds__(NT) void k_front(
           p = pp < p ? pp : 0u;
         }
     }
-    par[base + r] = p;
+    lane_at(parD, r) = p;
     const uint32_t a = (clsA[r >> 5] >> (r & 31)) & 1u, b = (clsB[r >> 5] >> (r & 31)) & 1u;
-    skind[base + r] = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
+    lane_at(skindD, r) = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
   }
   uint32_t *kb = kbm + (size_t)tile_first[d] * KBM_WORDS;
   for (uint32_t w = tid; w < nw; w += NT) {  // word w of the document = word w & 127 of tile w >> 7
@@ -1133,7 +1138,7 @@ __global__ __launch_bounds__(NT) void k_front(
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t i = i0 + u * NT;
-      r[u] = i < n ? rank16[base + i] : 0xFFFFu;
+      r[u] = i < n ? lane_at(rankD, i) : 0xFFFFu;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
@@ -1143,8 +1148,8 @@ __global__ __launch_bounds__(NT) void k_front(
   stamp(3);
   for (uint32_t r = tid; r < n; r += NT) {
     const uint32_t v = p16[r];
-    sval[base + r] = v;
-    if (skey) skey[base + r] = id_key[base + (v < n ? v : 0u)];  // ids in rank order (yarns)
+    lane_at(svalD, r) = v;
+    if (skey) skey[base + r] = lane_at(idD, (v < n ? v : 0u));  // ids in rank order (yarns)
   }
   stamp(4);
   if (tprof && tid == 0)
@@ -1496,14 +1501,6 @@ __global__ __launch_bounds__(NT) void k_tree(
 // non-special).  The thread table's u16 sentinel for SUCC_END is TL_END.
 constexpr uint32_t TL_END = 0xFFFFu;
 
-// Element i of a wave-uniform base pointer, addressed as base + zext(4 i): the
-// global access takes the scalar base and a 32-bit lane offset (saddr form), no
-// 64-bit address arithmetic per lane.
-template <typename T>
-__device__ __forceinline__ T &lane_at(T *b, uint32_t i) {
-  using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
-  return *reinterpret_cast<T *>(reinterpret_cast<C *>(b) + (size_t)(i * (uint32_t)sizeof(T)));
-}
 
 __host__ __device__ constexpr uint32_t tree_l_static_bytes(uint32_t nt, uint32_t tile) {
   return 4 * tile * 4 + tile * 2 + (nt / 64) * SUB_BINS * 4 + 64 * 4 + 4;
@@ -2480,6 +2477,8 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   stamp(-1);
   const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
+  const uint32_t *const linkD = link + base;
+  uint32_t *const locD = loc + base, *const permD = perm + base;
   if (tid == 0 && max_ts) max_ts[d] = n ? (skey[base + n - 1] >> ts_shift) : 0ull;
   if (n == 0) return;
   const uint32_t S = (n + (1u << log2k) - 1) >> log2k, nw = (n + 31) / 32;
@@ -2498,7 +2497,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT + lane;
-      L[k] = r < n ? link[base + r] : 0u;
+      L[k] = r < n ? lane_at(linkD, r) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2527,7 +2526,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
     bool live = j < S;
     if (live) {
       const uint32_t v = split_node(d, j, log2k, n);
-      loc[base + v] = j << 16;
+      lane_at(locD, v) = j << 16;
       u = succ[v];
       cnt = 1;
     }
@@ -2541,12 +2540,12 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
         live = j < S;
         if (live) {
           const uint32_t v = split_node(d, j, log2k, n);
-          loc[base + v] = j << 16;
+          lane_at(locD, v) = j << 16;
           u = succ[v];
           cnt = 1;
         }
       } else {
-        loc[base + u] = (j << 16) | cnt;
+        lane_at(locD, u) = (j << 16) | cnt;
         cnt++;
         u = succ[u];
       }
@@ -2595,8 +2594,8 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT;
-      lc[k] = r < n ? loc[base + r] : 0u;
-      x[k] = r < n ? (sval ? sval[base + r] : r) : 0u;
+      lc[k] = r < n ? lane_at(locD, r) : 0u;
+      x[k] = r < n ? (sval ? lane_at(sval + base, r) : r) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2615,7 +2614,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   __syncthreads();
   stamp(3);
   uint32_t nvis = 0;
-  for (uint32_t g = tid; g < n; g += NT) perm[base + g] = out[g];
+  for (uint32_t g = tid; g < n; g += NT) lane_at(permD, g) = out[g];
   for (uint32_t w = tid; w < nw; w += NT) nvis += __popc(pvis[w]);
   if (vbits) {
     // the render bits straight into the batch's bitmap: global word W holds

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace cw {
 
 // Sort tiles: a tile is a run of <= TILE consecutive nodes of ONE document.
@@ -54,6 +56,15 @@ __device__ __forceinline__ bool is_hide(uint8_t k) {
 // Number of lanes below this one whose bit is set in m (wave64).
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Element i of a wave-uniform base pointer, addressed as base + zext(i * size):
+// the global access takes the scalar base and a 32-bit lane offset (saddr
+// form), no 64-bit address arithmetic per lane.  i * sizeof(T) < 2^32.
+template <typename T>
+__device__ __forceinline__ T &lane_at(T *b, uint32_t i) {
+  using C = typename std::conditional<std::is_const<T>::value, const char, char>::type;
+  return *reinterpret_cast<T *>(reinterpret_cast<C *>(b) + (size_t)(i * (uint32_t)sizeof(T)));
 }
 
 // Blocks b, b+8, b+16, ... are dealt to the same XCD (MI355X_MICROARCH.md,
