@@ -75,23 +75,26 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nb) {
   return x * q + min(x, r) + (b >> 3);
 }
 
+// 32-bit mix of (a, b): murmur3's finalizer over a * golden + b (three
+// 32-bit multiplies; split_node runs for every node of the tree's sweep 2).
 __device__ __forceinline__ uint32_t mix32(uint32_t a, uint32_t b) {
-  uint64_t x = (((uint64_t)a << 32) | b) * 0x9E3779B97F4A7C15ull;
-  x ^= x >> 29;
-  x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 32;
-  return (uint32_t)x;
+  uint32_t h = a * 0x9E3779B1u + b;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
 }
 
 // The splitter node of block j (nodes [j*K, (j+1)*K) of a document of n nodes):
-// the root for block 0, else a hashed position inside the block.  Hashing
+// the root for block 0, else a hashed position inside the block (a multiply-
+// high reduction of the hash onto the block's length, no division).  Hashing
 // avoids the periodicity of interleaved site chains.
 __device__ __forceinline__ uint32_t split_node(uint32_t doc, uint32_t j, uint32_t log2k, uint32_t n) {
   if (j == 0) return 0;
-  uint32_t lo = j << log2k;
-  uint32_t k = 1u << log2k;
-  uint32_t h = mix32(doc, j);
-  return lo + ((n - lo >= k) ? (h & (k - 1)) : (h % (n - lo)));
+  const uint32_t lo = j << log2k, m = min(1u << log2k, n - lo);
+  return lo + __umulhi(mix32(doc, j), m);
 }
 
 }  // namespace cw
