@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ doc_log2k, uint32_t kbits,
     uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
-    uint32_t *__restrict__ fcN, uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
+    uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
     unsigned long long *__restrict__ tprof,
     const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first) {
   constexpr uint32_t IT = TILE_T / NT;
@@ -1548,7 +1548,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   // this document's slices (wave-uniform bases, lane offsets: lane_at)
   const uint32_t *const parD = par + base;
-  uint32_t *const fcSD = fcS + base, *const fcND = fcN + base, *const nscD = nsc + base;
+  uint32_t *const fcSD = fcS + base, *const nscD = nsc + base;
   uint32_t *const linkD = link + base, *const ospD = osp + base;
   uint32_t *const spec_bm = bm, *const hide_bm = bm + bm_words;
   uint16_t *const tab = reinterpret_cast<uint16_t *>(bm + 2 * bm_words);
@@ -1796,11 +1796,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   uint32_t r0t = 0;
   for (; r0t + TILE_T <= n; r0t += TILE_T) tile1(r0t, std::true_type());
   if (r0t < n) tile1(r0t, std::false_type());
-  // the newest non-special children go out once (sweep 2 reads them back
-  // coalesced; the oldest specials' parents at random)
   // the oldest special child's next sibling is its parent's newest
-  // non-special (weave-later?): patched into nsc now that tab is final
-  for (uint32_t r = tid; r < n; r += NT) lane_at(fcND, r) = tab[r];
+  // non-special (weave-later?): patched into nsc now that tab is final.  The
+  // newest non-special children stay in tab: sweep 2 reads tile t's entries
+  // before it overwrites them with tile t's threads.
   for (uint32_t i = tid; i < n_osp; i += NT) {
     const uint32_t v = lane_at(ospD, i), f = tab[v & 0xFFFFu];
     if (f) lane_at(nscD, (v >> 16)) = f;
@@ -1812,7 +1811,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   constexpr uint32_t RES = 0x80000000u;
   uint32_t *const T = hbuf;
   struct Q {
-    uint32_t fs[IT], fn[IT], ns[IT];
+    uint32_t fs[IT], ns[IT];
   };
   auto load_tile = [&](Q &q, uint32_t r0) {
 #pragma unroll
@@ -1820,7 +1819,6 @@ __global__ __launch_bounds__(NT) void k_tree_l(
       const uint32_t r = r0 + k * NT + tid;
       const bool ok = r < n;
       q.fs[k] = ok ? lane_at(fcSD, r) : 0u;
-      q.fn[k] = ok ? lane_at(fcND, r) : 0u;
       q.ns[k] = ok ? lane_at(nscD, r) : 0u;
     }
   };
@@ -1833,8 +1831,9 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = k * NT + tid, r = r0 + j;
       flg[k] = 0;
-      fcr[k] = X.fs[k] ? X.fs[k] : X.fn[k];
+      fcr[k] = 0;
       if (j >= len) continue;
+      fcr[k] = X.fs[k] ? X.fs[k] : (uint32_t)tab[r];
       const bool sp = special_at(r);
       uint32_t tv;
       if (r == 0) {
@@ -3853,13 +3852,13 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     const uint32_t tree_l = !c->tree_l || c->tree_pad ? 0
                             : tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= 160 * 1024 ? 2048
                             : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= 160 * 1024 ? 1024 : 0;
-    // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4, fcN 4 out; sweep 2 reads
-    // fcS, fcN, nsc (12) and writes link 4
-    Launch L(c, "tree", tree_l ? (double)N * (4 + 1 + 4 + 4 + 4 + 12 + 4)
+    // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4 out; sweep 2 reads
+    // fcS, nsc (8) and writes link 4
+    Launch L(c, "tree", tree_l ? (double)N * (4 + 1 + 4 + 4 + 8 + 4)
                                : (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
     auto tree_l_kernel = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(TL_NT), (size_t)tl_dyn, c->stream, par, skind,
-                         doc_off, doc_log2k, kbits, (t.nmax + 31) / 32, nsc, fcS, fcN,
+                         doc_off, doc_log2k, kbits, (t.nmax + 31) / 32, nsc, fcS,
                          (uint32_t *)link, thr, tprof, kbm, dev_tab(c, "t_tile_first"));
     };
     auto tree_l_mode = [&](auto prof, auto mode) {
