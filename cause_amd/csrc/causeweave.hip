@@ -3334,7 +3334,7 @@ struct cw_ctx {
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
   uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
-  uint32_t tree_l = 1;             // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits
+  uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
   uint32_t tl_mode = 0;            // CW_TL_MODE: k_tree_l variant bits (A/B)
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
@@ -3850,7 +3850,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     const uint32_t tl_dyn = tree_l_lds_bytes(t.nmax);
     // k_tree_l with 2,048-rank tiles, or 1,024 when the document needs the room
     const uint32_t tree_l = !c->tree_l || c->tree_pad ? 0
-                            : tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= 160 * 1024 ? 2048
+                            : c->tree_l == 2048 && tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= 160 * 1024 ? 2048
                             : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= 160 * 1024 ? 1024 : 0;
     // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4 out; sweep 2 reads
     // fcS, nsc (8) and writes link 4
@@ -5335,7 +5335,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->tree_pad = knob("CW_TREE_PAD", 0);
-  c->tree_l = knob("CW_TREE_L", 1);
+  c->tree_l = knob("CW_TREE_L", 2048);
   c->tl_mode = knob("CW_TL_MODE", 0);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 V='[{"CW_TREE_L":"0","CW_FRONT_EFF":"0"},{"CW_TL_MODE":"0","CW_FRONT_EFF":"0"},{"CW_TL_MODE":"2","CW_FRONT_EFF":"0"},{"CW_TL_MODE":"0","CW_FRONT_EFF":"1"},{"CW_TL_MODE":"1","CW_FRONT_EFF":"1"},{"CW_TL_MODE":"2","CW_FRONT_EFF":"1"},{"CW_TL_MODE":"3","CW_FRONT_EFF":"1"}]'
 timeout -k 10 400 python -u scripts/sweep.py "${TL_VARIANTS:-$V}" --check --rounds 3 > gpurun_out/ab_treel.log 2>&1
 echo ab-ok
-CW_TREE_PROF=1 timeout -k 10 200 python -u scripts/sweep.py '[{"CW_TREE_L":"1"}]' --rounds 1 > gpurun_out/prof_treel.log 2>&1
+CW_TREE_PROF=1 timeout -k 10 200 python -u scripts/sweep.py '[{"CW_TREE_L":"2048"}]' --rounds 1 > gpurun_out/prof_treel.log 2>&1
 echo prof-ok
 [ -n "$NO_TESTS" ] && exit 0
 timeout -k 10 300 python __graft_entry__.py smoke > gpurun_out/smoke.log 2>&1

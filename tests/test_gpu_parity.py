@@ -301,6 +301,7 @@ KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2C
          # the tree: k_tree (tables in HBM) and its geometries, k_tree_l's A/B modes,
          # raw parents from the front end (the tree climbs)
          {"CW_TREE_L": "0"}, {"CW_TREE_L": "0", "CW_TREE": "0"}, {"CW_TREE_L": "0", "CW_TREE": "1"},
+         {"CW_TREE_L": "1024"},
          {"CW_TL_MODE": "1"}, {"CW_TL_MODE": "2"}, {"CW_TL_MODE": "3"}, {"CW_FRONT_EFF": "1"}]
 
 
