@@ -1011,8 +1011,9 @@ __global__ __launch_bounds__(NT) void k_front(
       }
       const uint32_t xi = (uint32_t)x[u];
       const uint32_t g = xi / FR_GROUP_BITS, b = xi - g * FR_GROUP_BITS, m = 1u << (b & 31);
-      const uint32_t old = atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
-      dup |= (old & m) != 0;
+      // no returned value (a non-returning LDS atomic): a repeated id shows as
+      // fewer directory bits than ids, counted below
+      atomicOr(&sw[g * 4 + 1 + (b >> 5)], m);
     }
   }
 #pragma unroll
@@ -1036,7 +1037,9 @@ __global__ __launch_bounds__(NT) void k_front(
       const uint4 q = sdir[g];
       cnt += __popc(q.y) + __popc(q.z) + __popc(q.w);
     }
-    uint32_t run = block_exscan<NT>(cnt, wtot, nullptr);
+    uint32_t distinct;
+    uint32_t run = block_exscan<NT>(cnt, wtot, &distinct);
+    dup = distinct != n;  // every id is < lim here: one bit per distinct id
     for (uint32_t g = g0; g < g1; g++) {
       const uint4 q = sdir[g];
       sw[g * 4] = run;
