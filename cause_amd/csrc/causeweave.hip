@@ -2486,7 +2486,8 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   const uint32_t S = (n + (1u << log2k) - 1) >> log2k, nw = (n + 31) / 32;
   uint16_t *succ = reinterpret_cast<uint16_t *>(sm);
   uint32_t *vbm = sm + (n + 1) / 2, *sbm = vbm + nw;
-  uint16_t *acc = reinterpret_cast<uint16_t *>(sbm + nw), *nx = acc + S;
+  // per sublist: acc (nodes, later the suffix sum) | next sublist << 16, one word
+  uint32_t *const sub = sbm + nw;
   if (tid == 0) {
     bad_s = 0;
     next_j = NT;  // the first NT walkers are handed out by thread index
@@ -2536,8 +2537,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
       const bool end = u == TOUR_END || u >= n || split_at(u) || cnt > n;
       if (end) {
         bad |= (u != TOUR_END && u >= n) || cnt > n;
-        acc[j] = (uint16_t)min(cnt, 0xFFFFu);
-        nx[j] = (uint16_t)(u < n ? (u >> log2k) : TOUR_END);
+        sub[j] = min(cnt, 0xFFFFu) | (u < n ? (u >> log2k) : TOUR_END) << 16;
         j = atomicAdd(&next_j, 1u);
         live = j < S;
         if (live) {
@@ -2556,7 +2556,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   __syncthreads();
   if (tid == 0) next_j = NT;
   stamp(1);
-  // suffix sums along the sublist list by pointer jumping: acc[j] = nodes from
+  // suffix sums along the sublist list by pointer jumping: sub[j] & 0xFFFF = nodes from
   // sublist j to the end of the tour (<= n < 2^16)
   for (uint32_t round = 0; (1u << round) < 2 * S; round++) {
     uint32_t na[SPT], nn[SPT];
@@ -2564,9 +2564,10 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
     for (uint32_t k = 0; k < SPT; k++) {
       const uint32_t j = tid + k * NT;
       if (j < S) {
-        const uint32_t q = nx[j];
-        na[k] = acc[j] + (q < S ? acc[q] : 0u);
-        nn[k] = q < S ? nx[q] : TOUR_END;
+        const uint32_t sj = sub[j], q = sj >> 16;
+        const uint32_t sq = q < S ? sub[q] : TOUR_END << 16;
+        na[k] = (sj & 0xFFFFu) + (sq & 0xFFFFu);
+        nn[k] = sq >> 16;
       }
     }
     __syncthreads();
@@ -2574,14 +2575,13 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
     for (uint32_t k = 0; k < SPT; k++) {
       const uint32_t j = tid + k * NT;
       if (j < S) {
-        acc[j] = (uint16_t)min(na[k], 0xFFFFu);
-        nx[j] = (uint16_t)nn[k];
+        sub[j] = min(na[k], 0xFFFFu) | nn[k] << 16;
       }
     }
     __syncthreads();
   }
   stamp(2);
-  if (tid == 0 && acc[0] != n) bad_s = 1;  // the root's sublist starts the tour
+  if (tid == 0 && (sub[0] & 0xFFFFu) != n) bad_s = 1;  // the root's sublist starts the tour
   // place: coalesced over nodes, position = sublist base + index; the weave
   // (sval as u16) and its render bits are assembled in LDS where the
   // successors and splitter bits were, then written out coalesced.  (The
@@ -2604,7 +2604,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
       const uint32_t r = r0 + k * NT;
       if (r >= n) continue;
       const uint32_t j = lc[k] >> 16;
-      const uint32_t pos = (j < S ? n - min((uint32_t)acc[j], n) : n) + (lc[k] & 0xFFFFu);
+      const uint32_t pos = (j < S ? n - min(sub[j] & 0xFFFFu, n) : n) + (lc[k] & 0xFFFFu);
       if (pos >= n) {
         bad = true;
         continue;
