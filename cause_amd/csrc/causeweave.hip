@@ -1497,11 +1497,13 @@ __global__ __launch_bounds__(NT) void k_tree(
 // per CU: the last-child table of the non-special class (sweep 1) and the
 // thread table (sweep 2) are u16 arrays over the whole document in LDS, so the
 // accesses to far parents -- k_tree's random HBM line traffic, 1.3 requests a
-// node -- become LDS accesses.  What stays in HBM: the special
-// class's table fcS (specials are a minority), nsc, and fcN as written once at
-// the end of sweep 1 (sweep 2 reads it coalesced, and at random only for the
-// oldest special of a parent, whose next sibling is the parent's newest
-// non-special).  The thread table's u16 sentinel for SUCC_END is TL_END.
+// node -- become LDS accesses.  The table ends sweep 1 as each
+// node's newest non-special child, which sweep 2 reads for a tile before it
+// overwrites the tile's entries with their threads.  What stays in HBM: the
+// special class's table fcS (specials are a minority), nsc, and the list of
+// oldest special children, whose next sibling (their parent's newest
+// non-special) is patched into nsc once the table is final.  The thread
+// table's u16 sentinel for SUCC_END is TL_END.
 constexpr uint32_t TL_END = 0xFFFFu;
 
 
@@ -1532,10 +1534,10 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     }
   };
   stamp(-1);
-  // one tile's group-key hash: slot word = group key << HB | the head of the
-  // slot's member list (a tile index), 0 = empty; nxt: next member, TL_END
-  // ends.  The fallback sort's tkey/trank/tns and sweep 2's T live in the
-  // same buffer.
+  // one tile's group-key hash: hk[slot] = group key (0 = empty), hh[slot] =
+  // the head of the slot's member list (a tile index; MODE bit 0 packs both
+  // into hw[slot] = key << HB | head); nxt: next member, TL_END ends.  The
+  // fallback sort's tkey/trank/tns and sweep 2's T live in the same buffer.
   constexpr uint32_t HS = 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
   static_assert(TILE_T <= (1u << HB) && 17 + HB <= 32, "slot word layout");
   __shared__ uint32_t hbuf[3 * TILE_T > 2 * HS ? 3 * TILE_T : 2 * HS];
