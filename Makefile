@@ -17,8 +17,12 @@ HIP_HDR := include/causeweave.h cause_amd/csrc/cw_internal.h cause_amd/csrc/exac
 
 all: $(LIB) $(GENLIB) $(ORACLE)
 
-$(LIB): $(HIP_SRC) $(HIP_HDR)
-	$(HIPCC) $(HIPFLAGS) -Iinclude -Icause_amd/csrc $(HIP_SRC) -o $@
+# build id = hash of every source of the product library: profiles/pmc_traffic.json
+# records the id it was measured on, and bench.py reports traffic only for that build
+BUILD_ID = $(shell cat $(HIP_SRC) $(HIP_HDR) Makefile | sha1sum | cut -c1-16)
+
+$(LIB): $(HIP_SRC) $(HIP_HDR) Makefile
+	$(HIPCC) $(HIPFLAGS) -DCW_BUILD_ID='"$(BUILD_ID)"' -Iinclude -Icause_amd/csrc $(HIP_SRC) -o $@
 
 $(GENLIB): cause_amd/csrc/gen.cpp cause_amd/csrc/gen.h
 	$(CXX) -O3 -march=x86-64-v2 -std=c++17 -fPIC -shared -Wall -pthread $< -o $@

@@ -65,7 +65,7 @@ def parse():
                          "exchange, gather; always taken when N > 1)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, every rank compares its outputs with the CPU oracle "
-                         "(configs 2 and 4; the JSON line gets a 'check' object)")
+                         "(configs 2, 3 and 4; the JSON line gets a 'check' object)")
     return ap.parse_args()
 
 
@@ -169,6 +169,30 @@ class heartbeat:
     def __exit__(self, *a):
         self.stop.set()
         self.t.join()
+
+
+def pmc_traffic(kernel, workload, default_size):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, scripts/pmc_traffic.py: FETCH_SIZE doubled per
+    MI355X_MICROARCH.md), only when they were measured on THIS library build
+    (cw_build_id) and this workload at its default size.  -> (bytes or None, note)."""
+    from cause_amd import abi
+
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not default_size:
+        return None, "no PMC pass at this size"
+    if not os.path.exists(path):
+        return None, "profiles/pmc_traffic.json missing"
+    t = json.load(open(path))
+    bid = abi.build_id()
+    if t.get("build_id") != bid:
+        return None, (f"stale counters: measured on build {t.get('build_id')}, "
+                      f"this library is build {bid}")
+    entry = t.get("workloads", {}).get(workload, {}).get(kernel)
+    if not entry:
+        return None, f"no PMC pass of kernel {kernel} on {workload}"
+    return entry["bytes"], (f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                            f"{workload}, build {bid}")
 
 
 def cpu_baseline_prefix(idk, ck, kd, prefix):
@@ -277,7 +301,7 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     g_id = torch.from_numpy(np.ascontiguousarray(idk[sel]).view(np.int64)).to(dev)
     g_ca = torch.from_numpy(np.ascontiguousarray(ck[sel]).view(np.int64)).to(dev)
     g_kd = torch.from_numpy(np.ascontiguousarray(kd[sel])).to(dev)
-    if rank != 0 or world > 1 or a.no_cpu:
+    if rank != 0 or a.no_cpu:
         del idk, ck, kd
     torch.cuda.synchronize()
     group = None
@@ -322,8 +346,9 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     if rank == 0:
         name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
         achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+        traffic, tnote = pmc_traffic(name, f"config5dist_w{world}", a.giant == 1 << 26)
         cpu = None
-        if world == 1 and not a.no_cpu:
+        if not a.no_cpu:  # after the GPU region, on rank 0 at every N
             cpu = cpu_baseline_prefix(idk, ck, kd, 100_000)
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
@@ -339,7 +364,8 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
                        "parallelism": f"sample sort x{world} ({dist.get_backend()})"},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "launches_per_step": launches / a.steps,
+                         "traffic": traffic, "traffic_note": tnote,
+                         "launches_per_step": launches / a.steps,
                          "kernel_ms_per_step": ms / a.steps},
             "cpu_baseline": cpu,
             "kernels_ms_per_step_rank0": {k: round(v[1] / a.steps, 4) for k, v in
@@ -403,6 +429,7 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     value = N * world * a.steps / dt_max
     name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
     achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    traffic, tnote = pmc_traffic(name, "config4", a.colls == 1_000_000)
     check = None
     if a.check:
         bad = check_maps(off, idk, ck, ci, kd, o, S)
@@ -410,7 +437,8 @@ def main_maps(a, world, rank, local, dist, torch, dev):
         check = {"collections_checked": tot[1], "mismatches": tot[0],
                  "against": "literal c.map/weave fold + active-node (oracle, C)"}
     if rank == 0:
-        cpu = cpu_baseline_maps(spec, a.cpu_seconds) if (world == 1 and not a.no_cpu) else None
+        # timed after the GPU region, on rank 0 at every N (the other ranks are done)
+        cpu = cpu_baseline_maps(spec, a.cpu_seconds) if not a.no_cpu else None
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
             "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
@@ -422,7 +450,8 @@ def main_maps(a, world, rank, local, dist, torch, dev):
                        "zipf_s": spec.zipf_s, "parallelism": f"collections sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "launches_per_step": launches / a.steps,
+                         "traffic": traffic, "traffic_note": tnote,
+                         "launches_per_step": launches / a.steps,
                          "kernel_ms_per_step": ms / a.steps},
             "cpu_baseline": cpu,
             "kernels_ms_per_step": {k: round(v[1] / a.steps, 4) for k, v in
@@ -515,20 +544,43 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                        f"cycled over the slots), H2D + weave + D2H pipelined, no generation"}
         if st_bad[0]:
             raise SystemExit(f"rank {rank}: {st_bad[0]} documents out of domain")
+    check = None
+    if a.check:  # after timing: every streamed batch again, each compared with the oracle
+        import oracle
+
+        bad = [0, 0]
+
+        def consume_check(o):
+            b0 = d0 + o.index * B
+            b1 = min(d1, b0 + B)
+            off, idk, ck, kd = gen.generate(spec, b0, b1, nthreads=16)
+            want, vis, wst = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF,
+                                                nthreads=16)
+            got = o.weave_perm.astype(np.uint32)
+            gvis = np.unpackbits(o.visible_bits.view(np.uint8), bitorder="little")[:len(got)]
+            for dd in range(b1 - b0):
+                lo, hi = int(off[dd]), int(off[dd + 1])
+                ok = (o.status[dd] == wst[dd] and np.array_equal(got[lo:hi], want[lo:hi]) and
+                      np.array_equal(gvis[lo:hi], vis[lo:hi]) and
+                      int(o.visible_count[dd]) == int(vis[lo:hi].sum()))
+                bad[0] += 0 if ok else 1
+            bad[1] += b1 - b0
+
+        s.run(nb, fill, consume_check)
+        tot = shard.reduce_sum(bad, dist, dev) if world > 1 else bad
+        check = {"documents_checked": tot[1], "mismatches": tot[0],
+                 "against": "effective-tree preorder + visibility (oracle, C)"}
     t_dev = sum(st.weave_ms) / 1e3
     t_dev_max = shard.reduce_max_time(t_dev, dist, dev) if world > 1 else t_dev
     wall_max = shard.reduce_max_time(st.wall_s, dist, dev) if world > 1 else st.wall_s
     total = T * n
     name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
     achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and B == 10_000 and a.nodes == 50_000:
-        entry = json.load(open(pmc)).get(name)
-        traffic = entry["bytes"] if entry else None
+    # a config-3 batch has the config-2 batch's shape: the same kernels' counters
+    traffic, tnote = pmc_traffic(name, "config2", B == 10_000 and a.nodes == 50_000)
     if rank == 0:
         cpu = None
-        if world == 1 and not a.no_cpu:
+        if not a.no_cpu:  # after the GPU region, on rank 0 at every N
             cpu = cpu_baseline(spec, a.cpu_seconds, max_docs=64)
         kw, pw = (4 if k32 else 8), (2 if perm16 else 4)
         pcie = total // world * (kw + kw + 1 + pw) + total // world // 8
@@ -548,7 +600,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                        "parallelism": f"docs sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic, "launches_per_step": launches / nb,
+                         "traffic": traffic, "traffic_note": tnote,
+                         "launches_per_step": launches / nb,
                          "kernel_ms_per_step": ms / nb},
             "cpu_baseline": cpu,
             "end_to_end": {"value": total / wall_max, "unit": "nodes/s", "wall_s": wall_max,
@@ -564,6 +617,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = line["value"] / cpu["value"]
+        if check:
+            line["check"] = check
         print(json.dumps(line), flush=True)
     del s
     w.close()
@@ -724,15 +779,14 @@ def main():
     kernel_ms_total = sum(v[1] for v in stats.values())
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc) and a.config == 2 and a.docs == 10_000 and a.nodes == 50_000:
-        entry = json.load(open(pmc)).get(name)
-        traffic = entry["bytes"] if entry else None
+    traffic, tnote = pmc_traffic(name, f"config{a.config}",
+                                 a.keys == 64 and (a.config == 1 or (a.config == 2 and a.docs == 10_000
+                                                   and a.nodes == 50_000) or
+                                                   (a.config == 5 and a.giant == 1 << 26)))
 
     if rank == 0:
         cpu = None
-        if world == 1 and not a.no_cpu:
+        if not a.no_cpu:  # after the GPU region, on rank 0 at every N
             cpu = (cpu_baseline_prefix(*_k64(idk, ck), kd, 100_000) if a.config == 5 else
                    cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64))
         line = {
@@ -750,7 +804,7 @@ def main():
                                        else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_note": tnote,
                          "launches_per_step": launches / a.steps,
                          "kernel_ms_per_step": ms / a.steps},
             "cpu_baseline": cpu,
@@ -766,7 +820,7 @@ def main():
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]
         if check:
             line["check"] = check
-        if world == 1 and not a.no_cpu and a.config == 2:
+        if not a.no_cpu and a.config == 2:
             par = cpu_baseline_parallel(spec)
             line["cpu_baseline_parallel"] = par
             line["speedup_vs_cpu_parallel"] = value / par["value"]

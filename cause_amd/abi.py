@@ -134,6 +134,11 @@ def header_functions():
     return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(cw_\w+)\s*\(", src, re.M)))
 
 
+def build_id() -> str:
+    """The loaded library's build id (a hash of its sources, see Makefile)."""
+    return lib().cw_build_id().decode()
+
+
 def lib():
     """Load libcauseweave.so (raises if it was not built)."""
     global _LIB
@@ -143,6 +148,7 @@ def lib():
                              "'import __graft_entry__ as g; g.build()' or `make`)")
         L = C.CDLL(LIB_PATH)
         L.cw_abi_version.restype = C.c_int
+        L.cw_build_id.restype = C.c_char_p
         L.cw_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.cw_ctx_create.restype = C.c_int
         L.cw_ctx_destroy.argtypes = [C.c_void_p]

@@ -3305,6 +3305,7 @@ struct PendingEvt {
 
 struct cw_ctx {
   int device = 0;
+  uint32_t lds_max = 160 * 1024;  // LDS a workgroup may use on this device (queried at create)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   bool async = false;
@@ -3505,10 +3506,10 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
   t.tour = false;
   t.tour_log2k = c->tour_log2k;
   if (c->tour && !giant && nmax <= TOUR_END) {
-    while (t.tour_log2k < 8 && (tour_lds_bytes((uint32_t)nmax, t.tour_log2k) > TOUR_LDS_MAX ||
+    while (t.tour_log2k < 8 && (tour_lds_bytes((uint32_t)nmax, t.tour_log2k) > std::min(TOUR_LDS_MAX, c->lds_max - 1024) ||
                                 ((nmax + (1u << t.tour_log2k) - 1) >> t.tour_log2k) > 8 * 1024))
       t.tour_log2k++;
-    t.tour = tour_lds_bytes((uint32_t)nmax, t.tour_log2k) <= TOUR_LDS_MAX;
+    t.tour = tour_lds_bytes((uint32_t)nmax, t.tour_log2k) <= std::min(TOUR_LDS_MAX, c->lds_max - 1024);
   }
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
@@ -3855,8 +3856,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     const uint32_t tl_dyn = tree_l_lds_bytes(t.nmax);
     // k_tree_l with 2,048-rank tiles, or 1,024 when the document needs the room
     const uint32_t tree_l = !c->tree_l || c->tree_pad ? 0
-                            : c->tree_l == 2048 && tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= 160 * 1024 ? 2048
-                            : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= 160 * 1024 ? 1024 : 0;
+                            : c->tree_l == 2048 && tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= c->lds_max ? 2048
+                            : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= c->lds_max ? 1024 : 0;
     // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4 out; sweep 2 reads
     // fcS, nsc (8) and writes link 4
     Launch L(c, "tree", tree_l ? (double)N * (4 + 1 + 4 + 4 + 8 + 4)
@@ -4096,7 +4097,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     uint32_t *kbm = nullptr;  // special / hide bitmaps per tile (front end -> tree)
     // fused front end: documents of < 2^16 nodes whose ids fit a 40 KiB directory
     if (c->front && c->front_fused && N >= (uint64_t)c->front_min_avg * D &&
-        t.nmax <= 0xFFFFu && front_lds_bytes(t.nmax, FRONT_FUSED_SG) <= 159 * 1024) {
+        t.nmax <= 0xFFFFu && front_lds_bytes(t.nmax, FRONT_FUSED_SG) <= c->lds_max - 1024) {
       uint32_t *big = scratch_t<uint32_t>(c, "fr_big", 4);
       uint16_t *rank16 = scratch_t<uint16_t>(c, "fr_rank16", N);
       kbm = scratch_t<uint32_t>(c, "fr_kbm", (size_t)t.T * KBM_WORDS);
@@ -5309,6 +5310,11 @@ extern "C" {
 
 int cw_abi_version(void) { return CW_ABI_VERSION; }
 
+#ifndef CW_BUILD_ID
+#define CW_BUILD_ID "unknown"
+#endif
+const char *cw_build_id(void) { return CW_BUILD_ID; }
+
 int cw_ctx_create(int device, cw_ctx **out) {
   if (!out) return -1;
   *out = nullptr;
@@ -5323,6 +5329,12 @@ int cw_ctx_create(int device, cw_ctx **out) {
     return -1;
   }
   c->stream = c->own_stream;
+  {
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess &&
+        lds > 0)
+      c->lds_max = (uint32_t)lds;
+  }
   auto knob = [](const char *name, uint32_t dflt) {
     const char *v = getenv(name);
     return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;

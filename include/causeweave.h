@@ -83,6 +83,9 @@ typedef struct cw_ctx cw_ctx;
 
 /* ABI version (CW_ABI_VERSION). */
 int cw_abi_version(void);
+/* Build id of this library: a hash of its sources (Makefile).  Counter tables
+ * under profiles/ name the build they were measured on. */
+const char *cw_build_id(void);
 
 /* Create a context on HIP device `device` (its own stream).  0 on success. */
 int cw_ctx_create(int device, cw_ctx **out);

@@ -22,12 +22,15 @@ for s in $steps; do
     pmc)
       # HBM traffic per kernel: FETCH_SIZE and WRITE_SIZE in separate passes
       # PMC_PASSES: passes separated by ';', counters of one pass by spaces
+      # PMC_DIR: where the pmc_<counters> directories go (default gpurun_out)
+      P="${PMC_DIR:-gpurun_out}"
+      mkdir -p "$R/$P"
       IFS=';' read -ra passes <<< "${PMC_PASSES:-FETCH_SIZE;WRITE_SIZE}"
       for pass in "${passes[@]}"; do
         tag=$(echo $pass | tr ' ' '_')
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace \
-          --pmc $pass --output-format csv -d "$R/gpurun_out/pmc_$tag" -o run -- \
-          python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu ${PMC_BENCH_ARGS:-} > "$R/gpurun_out/pmc_$tag.log" 2>&1)
+          --pmc $pass --output-format csv -d "$R/$P/pmc_$tag" -o run -- \
+          python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu ${PMC_BENCH_ARGS:-} > "$R/$P/pmc_$tag.log" 2>&1)
       done ;;
     list)
       (cd /tmp && rocprofv3 -L > "$R/gpurun_out/counters.txt" 2>&1) ;;

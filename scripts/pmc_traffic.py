@@ -1,18 +1,25 @@
 """HBM traffic per launch for every weave kernel, from rocprofv3 --pmc passes.
 
-    python scripts/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json]
+    python scripts/pmc_traffic.py gpurun_out [profiles/pmc_traffic.json] [--workload config2]
 
 Reads the pmc.json written by scripts/pmc_summary.py (average counter value per
 launch, FETCH_SIZE / WRITE_SIZE in KiB).  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of wide
 reads, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  Keys are the kernel
 names of cw_get_kernel_stats (bench.py's "kernels_ms_per_step").
+
+The table records the build id of the library the counters were taken on
+(cw_build_id, a hash of the sources): bench.py reports `traffic` only when the
+library it times has that id, so a kernel change cannot inherit stale counters.
+Workloads measured on the same build accumulate in one file.
 """
+import argparse
 import json
 import os
 import re
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ALIAS = {"pack_bits": "packbits", "tree_l": "tree"}  # k_tree_l is the library's "tree" stat
 
 
@@ -23,12 +30,22 @@ def stat_name(sym):
 
 
 def main():
-    d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
-    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join("profiles", "pmc_traffic.json")
-    pmc = json.load(open(os.path.join(d, "pmc.json")))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir", nargs="?", default="gpurun_out")
+    ap.add_argument("out", nargs="?", default=os.path.join("profiles", "pmc_traffic.json"))
+    ap.add_argument("--workload", default="config2",
+                    help="bench workload the passes ran (bench.py --config N -> configN)")
+    a = ap.parse_args()
+    sys.path.insert(0, ROOT)
+    from cause_amd import abi
+
+    bid = abi.build_id()
+    pmc = json.load(open(os.path.join(a.dir, "pmc.json")))
     res = {}
     for sym, ctr in pmc.items():
         if "FETCH_SIZE" not in ctr or "WRITE_SIZE" not in ctr or sym.startswith("__"):
+            continue
+        if not sym.startswith("k_"):  # torch's own kernels (status readbacks)
             continue
         name = stat_name(sym)
         if name.startswith("radix_"):  # sort passes are reported per key width by the library
@@ -36,7 +53,14 @@ def main():
         res[name] = {"kernel": sym, "fetch_kib": ctr["FETCH_SIZE"], "write_kib": ctr["WRITE_SIZE"],
                      "bytes": (2 * ctr["FETCH_SIZE"] + ctr["WRITE_SIZE"]) * 1024.0,
                      "launches_sampled": ctr.get("launches")}
-    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    table = {"build_id": bid, "workloads": {}}
+    if os.path.exists(a.out):
+        old = json.load(open(a.out))
+        if old.get("build_id") == bid:
+            table = old
+    table["workloads"][a.workload] = res
+    json.dump(table, open(a.out, "w"), indent=1, sort_keys=True)
+    print(f"build {bid}, workload {a.workload}")
     for k, v in sorted(res.items()):
         print(f"{k:12s} {v['bytes'] / 1e9:9.3f} GB/launch  ({v['kernel']})")
 

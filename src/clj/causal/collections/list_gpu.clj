@@ -95,10 +95,12 @@
                                   (CauseWeave$Node. ts site tx 2 0 nil 0 (kind-of v false))))
                               d))
                       docs)
+        ;; one token per node, aligned with the node order (CauseWeave.weaveMaps reads
+        ;; keyToken[j] for node j); id-caused nodes carry 0, which is never read
         key-tokens (mapv (fn [d]
-                           (long-array (keep (fn [[_ [cause]]]
-                                               (when-not (spec/valid? ::s/id cause) (tok cause)))
-                                             d)))
+                           (long-array (map (fn [[_ [cause]]]
+                                              (if (spec/valid? ::s/id cause) 0 (tok cause)))
+                                            d)))
                          docs)
         token-bits (max 1 (- 64 (Long/numberOfLeadingZeros (max 1 (dec (count @tokens))))))
         res (.weaveMaps ^CauseWeave (.get weaver) natives key-tokens (int token-bits))]

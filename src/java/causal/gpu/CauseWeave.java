@@ -170,7 +170,9 @@ public final class CauseWeave implements AutoCloseable {
       }
       N += d.size();
     }
-    int tsBits = bits(mts), siteBits = bits(msite), txBits = bits(mtx);
+    // at least one site bit: the ids are packed with the same width the yarn
+    // partition (site_bits) reads, also when every node is on site "0"
+    int tsBits = bits(mts), siteBits = Math.max(bits(msite), 1), txBits = bits(mtx);
     boolean k128 = tsBits + siteBits + txBits > 63;
     if (k128 && (siteBits > 32 || txBits > 32))
       throw new IllegalArgumentException("ids do not fit K128 (site ranks and tx < 2^32)");
@@ -243,7 +245,7 @@ public final class CauseWeave implements AutoCloseable {
         b.set(JAVA_INT, 40, tsBits + siteBits + txBits);  // key_bits
         b.set(JAVA_INT, 44, siteBits + txBits);            // ts_shift
         b.set(JAVA_INT, 48, txBits);                       // site_shift
-        b.set(JAVA_INT, 52, Math.max(siteBits, 1));        // site_bits (yarns)
+        b.set(JAVA_INT, 52, siteBits);                     // site_bits (yarns)
         check((int) WEAVE_LISTS.invokeExact(ctx, b, res, CW_MEM_HOST), "cw_weave_lists");
       }
       ListResult[] out = new ListResult[D];

@@ -31,19 +31,51 @@ def _bench(*args, timeout=300):
     return json.loads(lines[0])
 
 
+def _measured(line):
+    """An N > 1 line carries the CPU baseline (rank 0, after the GPU region) and a
+    traffic field: the PMC bytes, or null with the reason."""
+    cpu = line["cpu_baseline"]
+    assert cpu and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    assert "traffic" in line["roofline"] and line["roofline"]["traffic_note"]
+
+
 def test_config2_two_ranks_every_document_checked():
     line = _bench("--gpus", "2", "--config", "2", "--docs", "40", "--nodes", "3000",
-                  "--steps", "2", "--warmup", "1", "--no-cpu", "--no-h2d", "--check")
+                  "--steps", "2", "--warmup", "1", "--cpu-seconds", "1", "--no-h2d", "--check")
     assert line["n_gpus"] == 2
     assert line["config"]["parallelism"] == "docs sharded x2"
     assert line["check"]["documents_checked"] == 80
     assert line["check"]["mismatches"] == 0
     assert line["value"] > 0
+    _measured(line)
+
+
+def test_config2_two_ranks_full_size_line_is_measured():
+    # the driver's SCALE line at N = 2: the default per-GPU batch, so the PMC
+    # traffic of this build applies (null only when profiles/ are stale)
+    line = _bench("--gpus", "2", "--steps", "2", "--warmup", "1", "--cpu-seconds", "2",
+                  timeout=600)
+    assert line["n_gpus"] == 2 and line["config"]["nodes_per_gpu"] == 500_010_000
+    _measured(line)
+    r = line["roofline"]
+    assert r["traffic"] is not None, r["traffic_note"]
+    assert line["cpu_baseline_parallel"]["value"] > 0
+
+
+def test_config3_two_ranks_every_streamed_document_checked():
+    line = _bench("--gpus", "2", "--config", "3", "--stream-docs", "120", "--docs", "20",
+                  "--nodes", "3000", "--warmup", "1", "--cpu-seconds", "1", "--check")
+    assert line["n_gpus"] == 2
+    assert line["config"]["parallelism"] == "docs sharded x2"
+    assert line["check"]["documents_checked"] == 120
+    assert line["check"]["mismatches"] == 0
+    _measured(line)
 
 
 def test_config4_two_ranks_every_collection_checked():
     line = _bench("--gpus", "2", "--config", "4", "--colls", "3000", "--steps", "2",
-                  "--warmup", "1", "--no-cpu", "--check")
+                  "--warmup", "1", "--cpu-seconds", "1", "--check")
     assert line["n_gpus"] == 2
     assert line["check"]["collections_checked"] == 6000
     assert line["check"]["mismatches"] == 0
+    _measured(line)
