@@ -135,7 +135,7 @@ def check_maps(off, idk, ck, ci, kd, o, S):
     bad = 0
     for d in range(len(off) - 1):
         a, b = int(off[d]), int(off[d + 1])
-        c = np.where(ci[a:b] == 1, ck[a:b], ck[a:b] | tok)
+        c = oracle.map_causes(ck[a:b], ci[a:b])
         nk, npos, skk, saa = oracle.map_weave(idk[a:b], c, ci[a:b], kd[a:b], 0)
         order = np.lexsort((npos, nk))
         groups = {}
@@ -264,7 +264,7 @@ def cpu_baseline_maps(spec, budget_s):
     tok = np.uint64(1 << 63)
     while t_total < budget_s and colls < 200_000:
         off, idk, ck, ci, kd = gen.generate_maps(spec, colls, colls + 1000, nthreads=1)
-        c = np.where(ci == 1, ck, ck | tok)
+        c = oracle.map_causes(ck, ci)
         t0 = time.perf_counter()
         for d in range(1000):
             a, b = int(off[d]), int(off[d + 1])

@@ -2724,16 +2724,25 @@ __global__ __launch_bounds__(256) void k_key_range(const uint64_t *__restrict__ 
 // ============================================================================
 constexpr uint32_t MAP_NO_PARENT = 0xFFFFFFFFu;  // cause-in-weave = the virtual root
 constexpr uint32_t MAP_CHAIN = 0xFFFFFFFEu;      // orphan: appended after its predecessor
+constexpr uint32_t MAP_ORPHAN = 0xFFFFFFFDu;     // nil key: the absent cause id itself (the
+                                                 // list pipeline flags ORPHAN, the literal fold
+                                                 // appends the node)
 
 // Per id-sorted node: the key (map.cljc:31-34) as a grouping value and the
 // rank of its cause-in-weave (map.cljc:35-37).  Grouping values, with
 // W = max(token_bits, key_bits):
 //   token t                         t              (cause is a key)
 //   id X               1 << W | X     (the cause node is id-caused by X)
-//   nil                             2 << W         (the cause node is absent)
-// In an id or nil key weave no node's cause is in the weave (each is an
-// orphan there), so weave-node appends every node at the end: the weave is
-// the root then the nodes in id order (shared.cljc:226-241, asap never holds).
+//   nil                             2 << W         (the cause node is absent, or
+//                                                   the cause or the cause node's
+//                                                   cause is nil: cause_is_id = 2)
+// In an id key weave no node's cause is in the weave (each is an orphan
+// there), so weave-node appends every node at the end: the weave is the root
+// then the nodes in id order (shared.cljc:226-241, asap never holds) -- a chain.
+// The nil key weave also holds nodes caused by the root id [0 "0" 0] or by nil
+// (cause-in-weave = the root, map.cljc:35-37) and their children, next to the
+// appended orphans: its nodes keep their real cause-in-weave, the list pipeline
+// flags the orphans and the literal fold (exact.hip) weaves that key weave.
 __global__ __launch_bounds__(256) void k_map_key(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ cause, const uint8_t *__restrict__ cause_is_id,
@@ -2752,23 +2761,30 @@ __global__ __launch_bounds__(256) void k_map_key(
     uint64_t key;
     uint32_t p;
     if (i > base && skey[i - 1] == skey[i]) bad |= CW_STATUS_DUP;
-    if (cause_is_id[gi]) {
+    const uint8_t ci = cause_is_id[gi];
+    if (ci == 1) {
       const uint32_t r = lower_bound_u64(skey + base, n, c);
       if (r < n && skey[base + r] == c) {
         const uint32_t gc = base + sval[base + r];
-        if (cause_is_id[gc]) {
+        const uint8_t cci = cause_is_id[gc];
+        if (cci == 1) {
           key = (1ull << W) | cause[gc];
           p = MAP_CHAIN;
+        } else if (cci == 2) {  // the cause node's cause is nil: the nil key, under it
+          key = 2ull << W;
+          p = r;
         } else {
           key = cause[gc] & tmask;
           if (cause[gc] > tmask) bad |= CW_STATUS_MAP_KEY;
           p = r;
         }
-      } else {
+      } else {  // the cause node is absent: the nil key; the root id is its root
         key = 2ull << W;
-        p = MAP_CHAIN;
-        if (c == 0) bad |= CW_STATUS_MAP_KEY;  // caused by the root id itself
+        p = c == 0 ? MAP_NO_PARENT : MAP_ORPHAN;
       }
+    } else if (ci == 2) {  // a nil cause: the nil key, woven under its root
+      key = 2ull << W;
+      p = MAP_NO_PARENT;
     } else {
       key = c & tmask;
       if (c > tmask) bad |= CW_STATUS_MAP_KEY;
@@ -2837,6 +2853,7 @@ __global__ __launch_bounds__(256) void k_seg_mark(
 // their packing (real ids are > 0, the virtual root is id 0).
 __global__ __launch_bounds__(256) void k_seg_build(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ cause,
     const uint32_t *__restrict__ mpar, const uint8_t *__restrict__ mkind,
     const uint32_t *__restrict__ rank_s, const uint32_t *__restrict__ seg_of,
     const uint32_t *__restrict__ seg_coll, const uint32_t *__restrict__ coll_off, uint32_t N,
@@ -2853,6 +2870,8 @@ __global__ __launch_bounds__(256) void k_seg_build(
     lc = 0ull;
   } else if (p == MAP_CHAIN) {  // the previous node of the key weave (or its root)
     lc = (j > 0 && seg_of[j - 1] == sg) ? skey[cbase + rank_s[j - 1]] : 0ull;
+  } else if (p == MAP_ORPHAN) {  // the absent cause id: an orphan of the key weave
+    lc = cause[cbase + sval[i]];
   } else {
     lc = skey[cbase + p];
   }
@@ -2925,7 +2944,10 @@ __global__ __launch_bounds__(256) void k_seg_active(
     }
   }
   seg_active[sg] = act;
-  if (lstatus[sg]) atomicOr(&status[seg_coll[sg]], lstatus[sg]);
+  // an orphan is how the nil key weave appends (its literal fold ran): not a
+  // status of the map; NON_LAMPORT stays as information
+  const uint32_t ls = lstatus[sg] & ~(uint32_t)CW_STATUS_ORPHAN;
+  if (ls) atomicOr(&status[seg_coll[sg]], ls);
 }
 
 // ============================================================================
@@ -4969,7 +4991,7 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
   {
     Launch L(c, "m_segbuild", (double)N * (4 + 4 + 4 + 8 + 4 + 8 + 1 + 8 + 8 + 1 + 4));
     hipLaunchKernelGGL(k_seg_build, dim3((N + 255) / 256), dim3(256), 0, c->stream, skey, sval,
-                       mpar, mkind, rank_s, seg_of, seg_coll, dev_tab(c, "t_doc_off"), N, lid,
+                       cause, mpar, mkind, rank_s, seg_of, seg_coll, dev_tab(c, "t_doc_off"), N, lid,
                        lcause, lkind, lmap);
   }
   if (check_launch(c, "m_segbuild")) return -1;
@@ -5023,6 +5045,34 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
     if (weave_lists_device(c, &lb, lid + loff[s0], lcause + loff[s0], lkind + loff[s0], &lr))
       return -1;
     s0 = s1;
+  }
+  // key weaves outside the fast weave's domain -- the nil key weave with its
+  // appended orphans next to children of the root, a cause with a larger id
+  // than its node (map.cljc:40-41 folds them whatever their causes) -- by the
+  // literal fold (exact.hip), as the fused path's literal key weaves
+  {
+    HIPCHK(c, hipMemsetAsync(small, 0, 4, c->stream));
+    hipLaunchKernelGGL(k_xcount_nonempty, dim3((uint32_t)((S + 255) / 256)), dim3(256), 0, c->stream,
+                       lst, (uint32_t)S, small);
+    if (check_launch(c, "m_xcount")) return -1;
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, small, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->pin_small[0]) {
+      if (loff.empty()) {
+        loff.resize(S + 1);
+        HIPCHK(c, hipMemcpy(loff.data(), seg_off, (S + 1) * 8, hipMemcpyDeviceToHost));
+      }
+      cw_list_batch lb{};
+      lb.n_docs = S;
+      lb.doc_offsets = loff.data();
+      lb.key_bits = key_bits;
+      cw_list_result lr{};
+      lr.weave_perm = lperm;
+      lr.visible_count = lvc;
+      lr.status = lst;
+      c->x_cached = false;  // (a chunk's giant key weave left its own status there)
+      if (exact_fixup(c, &lb, lid, lcause, lkind, &lr, true)) return -1;
+    }
   }
 
   // 5. key weaves in collection-local input indices, active-node per key

@@ -47,6 +47,16 @@ __global__ __launch_bounds__(256) void k_xcount(const uint32_t *__restrict__ sta
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (uint32_t)__popcll(b));
 }
 
+// The same count for documents known to be non-empty (the key weaves of the
+// general map path: each holds its root).
+__global__ __launch_bounds__(256) void k_xcount_nonempty(const uint32_t *__restrict__ status,
+                                                         uint32_t D, uint32_t *__restrict__ count) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool take = d < D && (status[d] & X_MASK) && !(status[d] & X_SKIP);
+  const uint64_t b = __ballot(take);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (uint32_t)__popcll(b));
+}
+
 // Copy the flagged documents' nodes into one compact sub-batch (tile tables of
 // the sub-batch; src_off[f] = where sub-document f starts in the caller's arrays).
 __global__ __launch_bounds__(256) void k_xgather(

@@ -133,9 +133,11 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         if (dstart[m] <= j) lo = m; else hi = m;
       }
       const uint64_t c = cause[s0 + j];
-      const bool cid = cause_is_id[s0 + j] != 0;
+      const uint8_t cis = cause_is_id[s0 + j];
+      const bool cid = cis == 1;
       B[j] = c;
-      K8[j] = (uint8_t)((cid ? 0x80u : 0u) | (kind[s0 + j] & KIND_CLASS));
+      // 0x80: the cause is an id; 0x40: the cause is nil (cause_is_id = 2)
+      K8[j] = (uint8_t)((cid ? 0x80u : cis == 2 ? 0x40u : 0u) | (kind[s0 + j] & KIND_CLASS));
       ck[u] = id_key[s0 + j];
       oid |= ck[u];
       oca |= cid ? c : 0ull;
@@ -201,6 +203,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         if (K8[jc] & 0x80u) {  // the cause node is id-caused: the key is that id (F8c)
           key = (1ull << W) | gc;
           p = MP_CHAIN;
+        } else if (K8[jc] & 0x40u) {  // the cause node's cause is nil: the nil key, under it
+          key = 2ull << W;
+          p = (uint16_t)lo;
         } else {
           key = gc & tmask;
           if (gc > tmask) st |= CW_STATUS_MAP_KEY;
@@ -212,6 +217,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         // which the literal fold below handles; other absent causes append)
         p = c == 0 ? MP_ROOT_ID : MP_CHAIN;
       }
+    } else if (K8[j] & 0x40u) {  // a nil cause: the nil key, under its root (map.cljc:35-37)
+      key = 2ull << W;
+      p = MP_ROOT_ID;
     } else {  // a key: woven under that key's root
       key = c & tmask;
       if (c > tmask) st |= CW_STATUS_MAP_KEY;

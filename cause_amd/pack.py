@@ -240,6 +240,9 @@ def pack_maps(docs) -> PackedMaps:
             if valid_id(cause):
                 ck[j] = pk(cause)
                 ci[j] = 1
+            elif cause is None:  # the nil key (cause_is_id = 2, include/causeweave.h)
+                ck[j] = 0
+                ci[j] = 2
             else:
                 ck[j] = tok.setdefault(cause, len(tok))
                 ci[j] = 0

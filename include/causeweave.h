@@ -66,9 +66,7 @@ enum {
   CW_STATUS_DUP = 1u << 1,         /* two nodes share an id (shared.cljc:166-171)          */
   CW_STATUS_ORPHAN = 1u << 2,      /* a cause is not in the document (shared.cljc:175-178) */
   CW_STATUS_NON_LAMPORT = 1u << 3, /* a cause id is not older than its node                */
-  CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits; on the general map
-                                      path (a collection of > 2048 nodes) also a node caused by
-                                      the root id, which the fused path weaves exactly    */
+  CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits                      */
   CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
   CW_STATUS_WEFT = 1u << 6,        /* weft: a cut id is not a node of the document         */
   CW_STATUS_KEY_RANGE = 1u << 7    /* an id key >= 2^63: it does not fit the K64 layout
@@ -197,7 +195,8 @@ int cw_weave_lists_k128(cw_ctx *ctx, const cw_list_batch_k128 *batch, cw_list_re
  * and last-writer-wins per key (active-node, map.cljc:47-59).
  *
  * Each node's cause is either a packed id (cause_is_id = 1: (spec/valid? ::s/id
- * cause), map.cljc:31) or a key token (an opaque key rank, < 2^token_bits).  A
+ * cause), map.cljc:31), a key token (cause_is_id = 0: an opaque key rank,
+ * < 2^token_bits) or nil (cause_is_id = 2: the nil key, cause ignored).  A
  * key-caused node is woven under the key's virtual root [[0 "0" 0] nil nil]
  * (map.cljc:35-40), whose packed id is 0 (site "0" interns to rank 0, ts 0);
  * an id-caused node lands in the weave of its cause node's key (map.cljc:32-34).
@@ -208,17 +207,19 @@ int cw_weave_lists_k128(cw_ctx *ctx, const cw_list_batch_k128 *batch, cw_list_re
  * rendered node, blank when the root's first child is a hide.  Key weaves are
  * returned per collection in ascending seg_key order.  Ids and tokens must fit
  * 62 bits.  Collections of <= 2048 nodes are woven by one kernel per pack of
- * collections (mappack.hip), which also folds key weaves with nodes caused by
- * the root id or by a node with a larger id literally (shared.cljc:225-241;
- * CW_STATUS_NON_LAMPORT stays as information); on the general path those
- * collections are flagged (MAP_KEY / NON_LAMPORT) and their output is
- * unspecified. */
+ * collections (mappack.hip), larger ones by the general path (sorts, then every
+ * key weave as a list document through the list pipeline).  Both fold key
+ * weaves that are not a plain F5 tree -- the nil key weave holding nodes caused
+ * by the root id or by nil next to appended orphans, a cause with a larger id
+ * than its node -- literally (shared.cljc:225-241), so every collection without
+ * DUP / MAP_KEY comes out as the reference's fold; CW_STATUS_NON_LAMPORT stays
+ * as information. */
 typedef struct {
   uint64_t n_colls;
   const uint64_t *coll_offsets; /* HOST memory, [n_colls+1]                                */
   const uint64_t *id_key;       /* [N] packed ids (< 2^63)                                 */
   const uint64_t *cause;        /* [N] packed cause id, or key token                       */
-  const uint8_t *cause_is_id;   /* [N] 1 = cause is an id                                  */
+  const uint8_t *cause_is_id;   /* [N] 1 = cause is an id, 0 = a key token, 2 = nil        */
   const uint8_t *kind;          /* [N] CW_KIND_* (no root: maps have a virtual root)      */
   uint32_t key_bits;            /* significant bits of id keys (0 = find on the device)   */
   uint32_t token_bits;          /* significant bits of key tokens                         */

@@ -20,6 +20,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = None
 
 METHOD_LITERAL, METHOD_LINKED, METHOD_EFF, METHOD_GENERAL = 0, 1, 2, 3
+NIL = (1 << 64) - 1  # OR_NIL (weave_oracle.h)
 
 
 def lib():
@@ -111,6 +112,18 @@ def batch_lists(offsets, id_key, cause_key, kind, method=METHOD_LINKED, nthreads
                          _p(k, C.c_uint8), method, nthreads, _p(perm, C.c_uint32),
                          _p(vis, C.c_uint8) if vis is not None else None, _p(st, C.c_uint32))
     return perm, vis, st
+
+
+MAP_TOKEN_BIT = 1 << 63
+
+
+def map_causes(cause, cause_is_id):
+    """The ABI's map causes (packed id, key token, nil: cause_is_id 1 / 0 / 2)
+    in the form map_weave keys them by: ids as they are, tokens with bit 63 set
+    (a keyword is never a vector), nil as OR_NIL."""
+    c = np.asarray(cause, np.uint64)
+    ci = np.asarray(cause_is_id)
+    return np.where(ci == 1, c, np.where(ci == 2, np.uint64(NIL), c | np.uint64(MAP_TOKEN_BIT)))
 
 
 def map_weave(id_key, cause, cause_is_id, kind, root_id):

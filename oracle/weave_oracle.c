@@ -425,11 +425,15 @@ size_t or_map_fold_literal(size_t n, const uint64_t *id, const uint64_t *cause,
   for (size_t r = 0; r < n; r++) {
     uint32_t i = s[r].idx;
     uint64_t key, cin;
-    if (cause_is_id[i]) {
+    if (cause_is_id[i] == 2) {
+      /* a nil cause is not an id: key nil, woven under the root (map.cljc:31-37) */
+      key = OR_NIL;
+      cin = root_id;
+    } else if (cause_is_id[i]) {
       /* key = (first (get-in ct [::s/nodes cause])): the cause node's cause, nil
        * when absent (map.cljc:32-34); cause-in-weave = cause (map.cljc:35-36). */
       size_t c = find_id(s, n, cause[i]);
-      key = (c == n) ? OR_NIL : cause[s[c].idx];
+      key = (c == n || cause_is_id[s[c].idx] == 2) ? OR_NIL : cause[s[c].idx];
       cin = cause[i];
     } else {
       key = cause[i];      /* map.cljc:34 */

@@ -93,7 +93,8 @@ int or_batch_lists(size_t ndocs, const uint64_t *offsets, const uint64_t *id,
 
 /* ---- maps (single collection) ------------------------------------------------
  * cause[i] is either a packed id (cause_is_id[i] = 1: spec/valid? ::s/id,
- * map.cljc:31) or an opaque key token (cause_is_id[i] = 0).  Each key weave is a
+ * map.cljc:31), an opaque key token (cause_is_id[i] = 0) or nil (cause_is_id[i]
+ * = 2: the nil key, under its root).  Each key weave is a
  * list weave starting at [root-node] (map.cljc:40) whose root id is root_id.
  * Outputs, per node: node_key[i] = key token of the weave it lands in (OR_NIL
  * for a nil key), node_pos[i] = 1-based position in that weave.  Per key weave

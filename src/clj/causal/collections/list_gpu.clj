@@ -92,14 +92,17 @@
                                 (if (spec/valid? ::s/id cause)
                                   (let [[cts csite ctx] cause]
                                     (CauseWeave$Node. ts site tx 0 cts csite ctx (kind-of v false)))
-                                  (CauseWeave$Node. ts site tx 2 0 nil 0 (kind-of v false))))
+                                  (CauseWeave$Node. ts site tx (if (nil? cause) 1 2) 0 nil 0
+                                                    (kind-of v false))))
                               d))
                       docs)
         ;; one token per node, aligned with the node order (CauseWeave.weaveMaps reads
         ;; keyToken[j] for node j); id-caused nodes carry 0, which is never read
         key-tokens (mapv (fn [d]
                            (long-array (map (fn [[_ [cause]]]
-                                              (if (spec/valid? ::s/id cause) 0 (tok cause)))
+                                              (if (or (nil? cause) (spec/valid? ::s/id cause))
+                                                0
+                                                (tok cause)))
                                             d)))
                          docs)
         token-bits (max 1 (- 64 (Long/numberOfLeadingZeros (max 1 (dec (count @tokens))))))

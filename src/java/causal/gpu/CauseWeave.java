@@ -322,6 +322,9 @@ public final class CauseWeave implements AutoCloseable {
             long cs = Arrays.binarySearch(r, n.csite);
             cause.setAtIndex(JAVA_LONG, j, (n.cts << (siteBits + txBits)) | (cs << txBits) | n.ctx);
             isId.set(JAVA_BYTE, j, (byte) 1);
+          } else if (n.causeKind == 1) {  // nil: the nil key (cause_is_id = 2)
+            cause.setAtIndex(JAVA_LONG, j, 0L);
+            isId.set(JAVA_BYTE, j, (byte) 2);
           } else {
             cause.setAtIndex(JAVA_LONG, j, tok[k]);
             isId.set(JAVA_BYTE, j, (byte) 0);

@@ -5,8 +5,10 @@ pinned to the Python restatement and map_test.cljc in test_oracle.py).
 Compared per collection and key: the key weave (node order, root first) and
 the active node (LWW, -1 = ::blank), including the reference's quirky keys
 (a key that is an id, or nil).  Collections the library flags
-(duplicate ids, nodes caused by the root id) are out of domain: the flag
-itself is checked against the host's own reading.
+(duplicate ids) are out of domain: the flag itself is checked against the
+host's own reading.  Every other collection -- nodes caused by the root id, by
+nil or by an absent id, causes with larger ids than their nodes -- must match
+the literal fold on every path.
 """
 import random
 
@@ -58,7 +60,7 @@ def oracle_maps(off, idk, ck, ci, kd):
     tok = np.uint64(1 << 63)
     for d in range(len(off) - 1):
         a, b = int(off[d]), int(off[d + 1])
-        c = np.where(ci[a:b] == 1, ck[a:b], ck[a:b] | tok)
+        c = oracle.map_causes(ck[a:b], ci[a:b])
         nk, npos, sk, sa = oracle.map_weave(idk[a:b], c, ci[a:b], kd[a:b], 0)
 
         def api(k):
@@ -84,34 +86,29 @@ def gpu_maps(res, D):
     return out
 
 
-def expected_flags(off, idk, ck, ci, fused=False):
-    """Host reading of the map domain: duplicate ids; root-id causes, which
-    the general path flags and the fused path weaves by the literal fold."""
+def expected_flags(off, idk, ck, ci):
+    """Host reading of the map domain: duplicate ids (::nodes is a map)."""
     flags = np.zeros(len(off) - 1, np.uint32)
     for d in range(len(off) - 1):
         a, b = int(off[d]), int(off[d + 1])
         if len(set(idk[a:b].tolist())) != b - a:
             flags[d] |= abi.STATUS_DUP
-        if not fused and ((ci[a:b] == 1) & (ck[a:b] == 0)).any():
-            flags[d] |= abi.STATUS_MAP_KEY
     return flags
 
 
 def check(weaver, off, idk, ck, ci, kd, token_bits, key_bits=0, flags=None):
-    """Every collection without a flag is compared with the literal map fold;
-    the fused path also weaves key weaves with non-Lamport causes exactly
-    (CW_STATUS_NON_LAMPORT stays as information), the general paths do not."""
+    """Every collection without a flag is compared with the literal map fold on
+    every path: key weaves with nodes caused by the root id, by nil or by an
+    absent id, or with non-Lamport causes, are folded literally
+    (CW_STATUS_NON_LAMPORT stays as information)."""
     res = weaver.weave_maps(off, idk, ck, ci, kd, token_bits, key_bits)
     D = len(off) - 1
-    fused = getattr(weaver, "fused", False)
     if flags is None:
-        flags = expected_flags(off, idk, ck, ci, fused)
+        flags = expected_flags(off, idk, ck, ci)
     np.testing.assert_array_equal(res.status & (abi.STATUS_MAP_KEY | abi.STATUS_DUP), flags)
     got, want = gpu_maps(res, D), oracle_maps(off, idk, ck, ci, kd)
     for d in range(D):
         if flags[d]:
-            continue
-        if res.status[d] & abi.STATUS_NON_LAMPORT and not fused:
             continue
         assert int(res.status[d]) & ~abi.STATUS_NON_LAMPORT == 0, (d, res.status[d])
         assert got[d] == want[d], f"collection {d}"
@@ -206,7 +203,7 @@ def test_absent_causes_nil_key_and_flags(weaver):
     ci[j], ck[j] = 1, 0
     res = check(weaver, off, idk, ck, ci, kd, tb)
     assert res.status[2] & abi.STATUS_DUP
-    assert bool(res.status[3] & abi.STATUS_MAP_KEY) != weaver.fused  # fused: the literal fold
+    assert res.status[3] == 0  # the literal fold of the nil key weave, on every path
     assert res.status[0] == 0 and res.status[1] == 0 and res.status[4] == 0
     nil = np.flatnonzero((res.seg_coll == 1) & (res.seg_key == np.uint64(NIL)))
     assert len(nil) == 1 and len(res.key_weave(int(nil[0]))) == 4
@@ -253,27 +250,28 @@ def test_random_small_maps_match_oracle(weaver):
           np.array(CI, np.uint8), np.array(K, np.uint8), 3)
 
 
-def test_literal_key_weaves_root_id_and_non_lamport_causes(weaver):
-    """Key weaves the reference folds with nodes that are not children of
-    their causes in id order: nodes caused by the root id [0 "0" 0] (the nil
-    key, next to nodes whose cause is absent) and undo/redo nodes whose cause
-    has a larger id.  The fused path weaves them by the literal fold and must
-    match the oracle's literal map fold exactly."""
-    rng = random.Random(23)
+def literal_histories(rng, n_colls, n_lo, n_hi, t_max=None):
+    """Map collections the reference folds with nodes that are not children of
+    their causes in id order: nodes caused by the root id [0 "0" 0] or by nil
+    (the nil key, next to nodes whose cause is absent, and children of those),
+    and undo/redo nodes whose cause has a larger id."""
     offs, I, Cs, CI, K = [0], [], [], [], []
-    for d in range(400):
-        n = rng.randint(2, 30)
+    for d in range(n_colls):
+        n = rng.randint(n_lo, n_hi)
         nodes = []
-        ids = rng.sample(range(1, 200), n)
+        ids = rng.sample(range(1, t_max or 7 * n_hi), n)
         for m, t in enumerate(ids):
             idv = (t << 2) | rng.randint(1, 3)
             r = rng.random()
             if r < 0.45:                   # a value or hide under a key
                 nodes.append([idv, rng.randint(0, 3), 0, rng.choice([0, 0, 0, 1])])
-            elif r < 0.6:                  # caused by the root id
+            elif r < 0.55:                 # caused by the root id
                 nodes.append([idv, 0, 1, rng.choice([0, 1, 2, 3])])
+            elif r < 0.6:                  # a nil cause (cause_is_id = 2)
+                nodes.append([idv, 0, 2, rng.choice([0, 0, 1])])
             elif r < 0.7:                  # an absent cause
-                nodes.append([idv, (rng.randint(200, 300) << 2) | 1, 1, rng.choice([0, 2, 3])])
+                nodes.append([idv, ((1 << 40) + rng.randint(0, 99)) << 2 | 1, 1,
+                              rng.choice([0, 2, 3])])
             else:                          # undo / redo of any node (older or newer)
                 nodes.append([idv, None, 1, rng.choice([1, 2, 3, 0])])
         for x in nodes:
@@ -285,10 +283,28 @@ def test_literal_key_weaves_root_id_and_non_lamport_causes(weaver):
         for x in nodes:
             I.append(x[0]); Cs.append(x[1]); CI.append(x[2]); K.append(x[3])
         offs.append(len(I))
-    res = check(weaver, np.array(offs, np.uint64), np.array(I, np.uint64), np.array(Cs, np.uint64),
-                np.array(CI, np.uint8), np.array(K, np.uint8), 2)
-    if weaver.fused:
-        assert (res.status & abi.STATUS_NON_LAMPORT).any()
+    return (np.array(offs, np.uint64), np.array(I, np.uint64), np.array(Cs, np.uint64),
+            np.array(CI, np.uint8), np.array(K, np.uint8))
+
+
+def test_literal_key_weaves_root_id_nil_and_non_lamport_causes(weaver):
+    """Small collections of literal_histories: the fused path folds those key
+    weaves literally in LDS, the general paths through exact.hip; all must
+    match the oracle's literal map fold exactly."""
+    off, idk, ck, ci, kd = literal_histories(random.Random(23), 400, 2, 30, t_max=200)
+    res = check(weaver, off, idk, ck, ci, kd, 2)
+    assert (res.status & abi.STATUS_NON_LAMPORT).any()
+
+
+@pytest.mark.parametrize("n_lo,n_hi,colls", [(3000, 6000, 4), (15000, 20000, 2)])
+def test_large_literal_collections(weaver, n_lo, n_hi, colls):
+    """Collections past the fused path's pack (> 2048 nodes: the general path
+    on every weaver) with root-id, nil, absent and non-Lamport causes."""
+    off, idk, ck, ci, kd = literal_histories(random.Random(n_lo), colls, n_lo, n_hi)
+    res = check(weaver, off, idk, ck, ci, kd, 2)
+    assert (res.status & abi.STATUS_NON_LAMPORT).any()
+    nil = res.seg_key == np.uint64(NIL)
+    assert nil.sum() == colls  # one nil key weave per collection (absent, root-id, nil causes)
 
 
 def test_repeat_calls_identical(weaver):

@@ -237,6 +237,54 @@ def test_map_batch_matches_python_restatement():
             {k: str(v) for k, v in R.causal_map_to_edn(p).items()}
 
 
+@pytest.mark.parametrize("colls,n_lo,n_hi", [(40, 2, 40), (2, 2500, 3500)])
+def test_map_nil_root_absent_and_younger_causes_match_python_restatement(colls, n_lo, n_hi):
+    """Maps the reference folds whatever the causes: nil causes and the root id
+    (the nil key, under its root), absent ids (the nil key, appended), children
+    of those, and undo/redo of a younger node.  Small maps take the fused
+    kernel, the 2,500+-node ones the general path; both vs causal_ref on real
+    Clojure-shaped values."""
+    rng = random.Random(7 + n_lo)
+    sites = [C.new_site_id(rng) for _ in range(3)]
+    conv = lambda v, M: {"HIDE": M.HIDE, "H_HIDE": M.H_HIDE, "H_SHOW": M.H_SHOW}.get(v, v)
+    cts, py = [], []
+    for _ in range(colls):
+        n = rng.randint(n_lo, n_hi)
+        ts = rng.sample(range(1, 4 * n), n)
+        nodes = []
+        for m, t in enumerate(ts):
+            nid = (t, rng.choice(sites), 0)
+            r = rng.random()
+            if r < 0.5 or not nodes:
+                nd = [nid, f"k{rng.randint(0, 3)}", rng.choice([f"v{m}", f"v{m}", "HIDE"])]
+            elif r < 0.58:
+                nd = [nid, None, rng.choice([f"n{m}", "HIDE"])]
+            elif r < 0.66:
+                nd = [nid, R.ROOT_ID, rng.choice([f"r{m}", "HIDE", "H_SHOW"])]
+            elif r < 0.74:
+                nd = [nid, (10 ** 9 + m, sites[0], 0), rng.choice([f"a{m}", "H_HIDE"])]
+            else:
+                nd = [nid, "LATER", rng.choice(["HIDE", "H_HIDE", "H_SHOW", f"w{m}"])]
+            nodes.append(nd)
+        for nd in nodes:
+            if nd[1] == "LATER":  # any other node: older, or younger (non-Lamport)
+                nd[1] = rng.choice([x for x in nodes if x is not nd])[0]
+        ct = C.new_map_ct()
+        ct["nodes"] = {nd[0]: (nd[1], conv(nd[2], C)) for nd in nodes}
+        cts.append(ct)
+        p = R.new_map_ct()
+        p["nodes"] = {nd[0]: (nd[1], conv(nd[2], R)) for nd in nodes}
+        py.append(R.map_weave(p))
+    got = C.weave_maps(cts)
+    for g, p in zip(got, py):
+        want = {k: [(n[0], n[1], str(n[2])) for n in w] for k, w in p["weave"].items()}
+        have = {k: [(n[0], n[1], str(n[2])) for n in w] for k, w in g["weave"].items()}
+        assert have == want
+        assert None in have
+        assert {k: str(v) for k, v in C.causal_map_to_edn(g).items()} == \
+            {k: str(v) for k, v in R.causal_map_to_edn(p).items()}
+
+
 def test_map_exotic_site_ids_sort_before_zero():
     """Map nodes from site-ids that sort before "0" in String.compareTo order
     (" a ", " f ", " z ", as list_test.cljc:85-96 uses): the GPU map weave

@@ -339,39 +339,76 @@ def _map_nodes(rng, n, nkeys=6, nsites=4):
     return nodes
 
 
-def test_c_oracle_map_matches_python():
+def _exotic_map_nodes(rng, n):
+    """_map_nodes plus the causes c.map/weave folds whatever they are: nil, the
+    root id, an absent id (the nil key) and a younger node (non-Lamport)."""
+    nodes = _map_nodes(rng, n)
+    out = []
+    for nd in nodes:
+        r = rng.random()
+        if r < 0.1:
+            nd = (nd[0], None, nd[2])
+        elif r < 0.2:
+            nd = (nd[0], R.ROOT_ID, nd[2])
+        elif r < 0.3:
+            nd = (nd[0], (10 ** 6 + rng.randrange(9), nd[0][1], 0), nd[2])
+        elif r < 0.4 and len(nodes) > 1:
+            nd = (nd[0], rng.choice([x[0] for x in nodes if x[0] != nd[0]]), nd[2])
+        out.append(nd)
+    return out
+
+
+@pytest.mark.parametrize("exotic", [False, True])
+def test_c_oracle_map_matches_python(exotic):
     rng = random.Random(77)
-    for _ in range(60):
-        nodes = _map_nodes(rng, rng.randint(1, 40))
+    for _ in range(60 if not exotic else 200):
+        n = rng.randint(1, 40)
+        nodes = _exotic_map_nodes(rng, n) if exotic else _map_nodes(rng, n)
         ct = R.new_map_ct()
         ct["nodes"] = {n[0]: (n[1], n[2]) for n in nodes}
         ct = R.map_weave(ct)
         want = R.causal_map_to_edn(ct)
-        # pack: key tokens for keyword causes, ids for id causes
+        # pack: key tokens for keyword causes, ids for id causes, nil = cause_is_id 2
         lay = pack.layout_for([[(n[0], n[1] if R.valid_id(n[1]) else None, n[2]) for n in nodes]
                                + [R.ROOT_NODE]])
-        rank = pack.intern_sites([n[0] for n in nodes] + [R.ROOT_ID])
+        rank = pack.intern_sites([n[0] for n in nodes] + [n[1] for n in nodes if R.valid_id(n[1])]
+                                 + [R.ROOT_ID])
         key_tok = {}
         idk = np.array([lay.pack(n[0][0], rank[n[0][1]], n[0][2]) for n in nodes], np.uint64)
-        cause = []
+        cause, cis = [], []
         for n in nodes:
             if R.valid_id(n[1]):
                 cause.append(lay.pack(n[1][0], rank[n[1][1]], n[1][2]))
+                cis.append(1)
+            elif n[1] is None:
+                cause.append(0)
+                cis.append(2)
             else:
-                cause.append((1 << 63) | key_tok.setdefault(n[1], len(key_tok)))
-        cause = np.array(cause, np.uint64)
-        cis = np.array([R.valid_id(n[1]) for n in nodes], np.uint8)
+                cause.append(key_tok.setdefault(n[1], len(key_tok)))
+                cis.append(0)
+        cis = np.array(cis, np.uint8)
+        cause = oracle.map_causes(np.array(cause, np.uint64), cis)
         kind = np.array([pack.kind_of(n[2]) for n in nodes], np.uint8)
         root = lay.pack(0, rank["0"], 0)
         nk, npos, sk, sa = oracle.map_weave(idk, cause, cis, kind, root)
         inv = {v: k for k, v in key_tok.items()}
+        ids = {int(lay.pack(x[0], rank[x[1]], x[2])): x for x in
+               [nd[0] for nd in nodes] + [nd[1] for nd in nodes if R.valid_id(nd[1])] + [R.ROOT_ID]}
+
+        def key_of(k):
+            if k == oracle.NIL:
+                return None
+            if k & (1 << 63):
+                return inv[k & ~(1 << 63)]
+            return ids[k]  # an id key (SURVEY F8c)
+
         got = {}
         for s_key, act in zip(sk, sa):
             if act >= 0:
-                got[inv[int(s_key) & ~(1 << 63)]] = nodes[act][2]
+                got[key_of(int(s_key))] = nodes[act][2]
         assert got == want
         # per-node placement equals the Python key weaves
         for k, wk in ct["weave"].items():
             for pos, n in enumerate(wk[1:], 1):
                 j = next(x for x, m in enumerate(nodes) if m[0] == n[0])
-                assert npos[j] == pos
+                assert npos[j] == pos, (k, n)
