@@ -23,6 +23,7 @@ STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1,
 STATUS_MAP_KEY = 16
 STATUS_WEFT = 64
 STATUS_KEY_RANGE = 128
+STATUS_UNWOVEN = 256
 NIL32 = 0xFFFFFFFF
 K32_RESERVED = 0xFFFFFFF0     # K32 words from here up = the top 16 K64 values (CW_NIL, ...)
 
@@ -139,6 +140,26 @@ def build_id() -> str:
     return lib().cw_build_id().decode()
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm ships its own libamdhip64
+    (soname libamdhip64.so.7, NEEDED by torch as plain "libamdhip64.so"): when
+    this library loaded /opt/rocm's copy first, a later `import torch` loads a
+    second runtime, which then sees no GPU, and device pointers / streams could
+    not be shared.  Loading torch's copy first (without importing torch) makes
+    libcauseweave.so bind to it (same soname) and torch reuse it (same path).
+    CW_HIP_RUNTIME=system keeps /opt/rocm's runtime."""
+    if os.environ.get("CW_HIP_RUNTIME") == "system":
+        return
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    path = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
 def lib():
     """Load libcauseweave.so (raises if it was not built)."""
     global _LIB
@@ -146,6 +167,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise WeaveError(f"{LIB_PATH} is missing: build it (python -c "
                              "'import __graft_entry__ as g; g.build()' or `make`)")
+        _share_torch_hip_runtime()
         L = C.CDLL(LIB_PATH)
         L.cw_abi_version.restype = C.c_int
         L.cw_build_id.restype = C.c_char_p

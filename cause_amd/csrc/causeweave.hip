@@ -3376,6 +3376,7 @@ struct cw_ctx {
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
   bool x_cached = false;           // x_status holds the status of this call's giant document,
   uint32_t x_status = 0;           // read back with the walk's counter (exact.hip skips a sync)
+  uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
   uint32_t map_fused = 1;          // CW_MAP_FUSED: one-kernel map weave of small collections
   struct MapPacks {                // k_map_pack's pack table, cached by collection layout
     std::vector<uint64_t> off;

@@ -83,6 +83,7 @@ def main():
     for name, spec, off, idk, ck2, kd, bad in cases:
         res, ms, ks = run(w, off, idk, ck2, kd, spec.layout())
         line = {"case": name, "nodes": int(len(idk)), "ms_per_weave": ms, "kernels_ms": ks,
+                "synthetic_iterations": w.kernel_stats().get("xsyn_attach", (0,))[0] // 3,
                 "flagged_docs": int(np.count_nonzero(res.status & abi.STATUS_ORPHAN))}
         if bad is not None:
             chk = [int(d) for d in bad][:20]

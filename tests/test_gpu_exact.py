@@ -130,7 +130,7 @@ def test_device_memory_async_corrupted():
                               oracle.list_yarns(idk[a:b], lay.site_shift, mask))
 
 
-@pytest.mark.parametrize("case", ["orphan", "non_lamport", "no_root_first"])
+@pytest.mark.parametrize("case", ["orphan", "orphan_few", "non_lamport", "no_root_first"])
 def test_weave_ranked_exact(case):
     """cw_weave_ranked (the distributed giant list's last step) on a flagged
     list: the literal fold of the ranks."""
@@ -143,8 +143,9 @@ def test_weave_ranked_exact(case):
     par = par.view(np.uint32).copy()
     kd = kd.copy()
     rng = np.random.default_rng(1)
-    if case == "orphan":
-        par[rng.choice(np.arange(1, len(par)), 40, replace=False)] = 0xFFFFFFFF
+    if case in ("orphan", "orphan_few"):  # the serial fold / the synthetic list
+        k = 40 if case == "orphan" else 7
+        par[rng.choice(np.arange(1, len(par)), k, replace=False)] = 0xFFFFFFFF
     elif case == "non_lamport":
         js = rng.choice(np.arange(1, len(par) - 100), 40, replace=False)
         par[js] = js + rng.integers(1, 100, len(js))
@@ -171,3 +172,92 @@ def test_weave_ranked_exact(case):
     gvis = np.unpackbits(got["visible_bits"].cpu().numpy().view(np.uint8), bitorder="little")[:n]
     assert np.array_equal(gvis, vis)
     assert int(got["visible_count"][0]) == int(vis.sum())
+
+
+def _orphaned(spec, D, per_doc, rng, nil_every=0):
+    """Config-2-shaped documents whose per_doc[d] random nodes get an absent,
+    older cause (an id no node has) and, every nil_every-th, a nil cause: the
+    synthetic-list path (no non-Lamport cause)."""
+    off, idk, ck, kd = gen.generate(spec, 0, D, nthreads=8)
+    ck = ck.copy()
+    for d in range(D):
+        a, b = int(off[d]), int(off[d + 1])
+        ids = set(idk[a:b].tolist())
+        js = rng.choice(np.arange(a + 1, b), min(per_doc[d], b - a - 1), replace=False)
+        for q, j in enumerate(js):
+            if nil_every and q % nil_every == nil_every - 1:
+                ck[j] = np.uint64((1 << 64) - 1)
+                continue
+            x = int(idk[j]) - 1
+            while x in ids:
+                x -= 1
+            ck[j] = x
+    return off, idk, ck, kd
+
+
+def _attach_iterations(w):
+    return w.kernel_stats().get("xsyn_attach", (0, 0.0, 0.0))[0]
+
+
+def test_orphan_documents_synthetic_lists_few_iterations():
+    """Documents with 1 .. 32 orphans (and nil causes) go through the synthetic
+    lists: bit-exact against the literal fold, in at most (orphans + 1)
+    iterations (one weave each) -- 2 when every document has one orphan."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=6000, seed=31)
+    rng = np.random.default_rng(31)
+    with abi.Weaver(0) as w:
+        off, idk, ck, kd = _orphaned(spec, 24, [1] * 24, rng)
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, spec.layout())
+        w.set_profiling(False)
+        assert (res.status & abi.STATUS_ORPHAN).all()
+        assert 1 <= _attach_iterations(w) <= 2
+        per = [1, 2, 3, 5, 8, 13, 21, 32, 4, 7, 16, 30]
+        off, idk, ck, kd = _orphaned(spec, len(per), per, rng, nil_every=3)
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, spec.layout())
+        w.set_profiling(False)
+        assert 2 <= _attach_iterations(w) <= max(per) + 1
+
+
+def test_many_orphans_take_the_serial_fold_next_to_synthetic_ones():
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000, seed=32)
+    rng = np.random.default_rng(32)
+    off, idk, ck, kd = _orphaned(spec, 8, [1, 200, 3, 64, 0, 33, 2, 500], rng, nil_every=5)
+    with abi.Weaver(0) as w:
+        check_batch(w, off, idk, ck, kd, spec.layout())
+
+
+@pytest.mark.parametrize("orphans", [1, 10])
+def test_giant_list_orphans_synthetic(orphans):
+    """A one-document batch on the giant path with absent and nil causes: the
+    synthetic list is woven on the giant path too (compared with the C
+    restatement of the exact path's rule, or_list_fold_general, itself pinned
+    to the literal fold by test_oracle)."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=300_000, seed=33 + orphans)
+    rng = np.random.default_rng(orphans)
+    off, idk, ck, kd = _orphaned(spec, 1, [orphans], rng, nil_every=4)
+    with abi.Weaver(0) as w:
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_GENERAL)
+        w.set_profiling(False)
+        assert _attach_iterations(w) <= orphans + 1
+        assert "xfold" not in w.kernel_stats()  # no serial lane
+    assert res.status[0] & abi.STATUS_ORPHAN
+
+
+def test_unwoven_above_the_serial_limit():
+    """A non-Lamport cause in a document above the serial fold's limit (2^22
+    nodes) is not folded on one lane: CW_STATUS_UNWOVEN, the call returns."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 10, seed=34)
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
+    ck = ck.copy()
+    srt = np.sort(idk)
+    ck[100] = srt[-5]  # a cause with a larger id
+    with abi.Weaver(0) as w:
+        res = w.weave_lists(off, idk, ck, kd, spec.layout())
+    assert res.status[0] & abi.STATUS_NON_LAMPORT
+    assert res.status[0] & abi.STATUS_UNWOVEN
