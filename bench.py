@@ -734,6 +734,14 @@ def main():
     dt = time.perf_counter() - t0
     w.set_profiling(False)
     stats = w.kernel_stats()
+    # the same steps without the per-kernel events (information: for a
+    # one-list config the events are a visible share of a sub-ms step)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    dt_noprof = time.perf_counter() - t1
 
     dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
     total_nodes = N * world * a.steps
@@ -813,6 +821,7 @@ def main():
             "kernel_gbs": {k: round(v[2] / (v[1] / 1e3) / 1e9, 1) for k, v in stats.items()
                            if v[1] > 0},
             "kernel_sum_ms_per_step": kernel_ms_total / a.steps,
+            "ms_per_step_without_events_rank0": dt_noprof / a.steps * 1e3,
             "end_to_end_pcie": e2e,
             "gen_s": t_gen,
         }

@@ -1922,13 +1922,22 @@ __global__ __launch_bounds__(NT) void k_tree_l(
 //            = its parent's newest non-special (binary search in the keys);
 //   k_gthr   per tile: threads by pointer jumping inside the tile; a chain that
 //            leaves the tile is left to the walk (LINK_PEND: thr[x] is chased).
+// (also clears k_gsib's last-child tables and zeroes two counters at r == 0:
+// fewer launches on the one-list path, where each costs a visible share)
 __global__ __launch_bounds__(256) void k_geff(const uint32_t *__restrict__ par,
                                               const uint8_t *__restrict__ skind, uint32_t n,
-                                              uint32_t root_key, uint32_t *__restrict__ gk) {
+                                              uint32_t root_key, uint32_t *__restrict__ gk,
+                                              uint32_t *__restrict__ fcS, uint32_t *__restrict__ fcN,
+                                              uint32_t *__restrict__ zero_a,
+                                              uint32_t *__restrict__ zero_b) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
+  fcS[r] = 0;
+  fcN[r] = 0;
   if (r == 0) {
     gk[0] = root_key;  // the root has no group: it sorts last
+    if (zero_a) *zero_a = 0;
+    if (zero_b) *zero_b = 0;
     return;
   }
   const bool sp = is_special(skind[r]);
@@ -2274,8 +2283,10 @@ __global__ __launch_bounds__(256) void k_lvl_apply(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ ba,
                                                    const uint32_t *__restrict__ bb, uint32_t Wall,
                                                    uint32_t *__restrict__ oa, uint32_t *__restrict__ ob,
-                                                   uint32_t *__restrict__ order) {
+                                                   uint32_t *__restrict__ order,
+                                                   const uint32_t *__restrict__ dyn, uint32_t Wstat) {
   const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (dyn) Wall = min(Wstat + dyn[0], Wall);  // walkers in use (Wall: the capacity)
   if (x >= Wall) return;
   const uint32_t q = sup[x], va = ba[q] + pa[x], vb = bb[q] + pb[x];
   oa[x] = va;
@@ -2294,7 +2305,9 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
                                                    uint32_t n, uint32_t Weff, uint32_t *__restrict__ nb,
                                                    uint32_t *__restrict__ tb,
                                                    uint32_t *__restrict__ status,
-                                                   uint32_t *__restrict__ order = nullptr) {
+                                                   uint32_t *__restrict__ order = nullptr,
+                                                   const uint32_t *__restrict__ dyn = nullptr,
+                                                   uint32_t Wstat = 0, uint32_t Wcap = 0) {
   // the top level (<= 8192 elements) ranked by pointer jumping in LDS: suffix
   // sums of nodes and sublists along the list, element 0 (the root's) first.
   // ssub == nullptr: the elements are the sublists themselves (one each), and
@@ -2302,6 +2315,12 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
   // ranks them here directly, without the walk levels)
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];  // next, count, sublists
   constexpr uint32_t PT = 8;  // elements per thread: S2 <= 8192
+  // dyn: the walkers in use are Wstat + dyn[0] (<= Wcap), known on the device only;
+  // the elements are those walkers themselves when ssub == nullptr
+  if (dyn) {
+    Weff = min(Wstat + dyn[0], Wcap);
+    if (!ssub) S2 = Weff;
+  }
   uint32_t *nx = sm, *cn = sm + S2, *sb = sm + 2 * S2;
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
     nx[i] = snext[i];
@@ -3374,9 +3393,10 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
-  bool x_cached = false;           // x_status holds the status of this call's giant document,
-  uint32_t x_status = 0;           // read back with the walk's counter (exact.hip skips a sync)
   uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
+  uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
+  hipEvent_t ev_status = nullptr;  // ... and recorded there (exact.hip waits on it, not the stream)
+  bool x_pending = false;          // pin_status / ev_status hold this call's giant document
   uint32_t map_fused = 1;          // CW_MAP_FUSED: one-kernel map weave of small collections
   struct MapPacks {                // k_map_pack's pack table, cached by collection layout
     std::vector<uint64_t> off;
@@ -3844,14 +3864,14 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     const dim3 GN((N + 255) / 256);
     {
       Launch L(c, "geff", (double)N * (4 + 1 + 4));
-      hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk);
+      // (the walk's counter and the emit's rendered count zeroed here)
+      hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk, fcS, fcN,
+                         hbm_walk ? dyn_ctr : nullptr, out->visible_count);
     }
     if (check_launch(c, "geff")) return -1;
     uint32_t *gks, *gvs;
     if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
       return -1;
-    HIPCHK(c, hipMemsetAsync(fcS, 0, (size_t)N * 4, c->stream));
-    HIPCHK(c, hipMemsetAsync(fcN, 0, (size_t)N * 4, c->stream));
     {
       Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
       hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
@@ -3984,7 +4004,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     }
   } else {
     // 6. walk: sublists of the preorder successor list
-    HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));
+    if (!(giant && !linked)) HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));  // (k_geff did)
     {
       Launch L(c, "walk", (double)N * (4 + 4));
       hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
@@ -3998,18 +4018,13 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
 
     // 7. rank sublists (+ max lamport-ts per document)
     if (giant) {
-      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-      HIPCHK(c, hipMemcpyAsync(c->pin_small, dyn_ctr, 4, hipMemcpyDeviceToHost, c->stream));
-      // the document's status rides along: its domain bits are final by now
-      HIPCHK(c, hipMemcpyAsync(c->pin_small + 4, out->status, 4, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      c->x_cached = true;
-      c->x_status = c->pin_small[4];
-      const uint32_t W = t.doc_W[0], Weff = std::min(W + c->pin_small[0], t.Wtot);
-      if (Weff <= SUP_MAX) {  // few sublists: one LDS ranking, no walk levels
-        Launch L(c, "rank", (double)Weff * 20);
-        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)Weff * 12, c->stream, wcnt, nullptr,
-                           wnext, Weff, N, Weff, sbase, nullptr, out->status, order);
+      // the walkers the walk added (pending threads) stay on the device: the
+      // ranking kernels read W + dyn_ctr[0] themselves, no readback (sync) here
+      const uint32_t W = t.doc_W[0], Wcap = t.Wtot, Weff = Wcap;  // (Weff: an upper bound)
+      if (Wcap <= SUP_MAX) {  // few sublists: one LDS ranking, no walk levels
+        Launch L(c, "rank", (double)Wcap * 20);
+        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)Wcap * 12, c->stream, wcnt, nullptr,
+                           wnext, Wcap, N, Wcap, sbase, nullptr, out->status, order, dyn_ctr, W, Wcap);
       } else {
       // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
       const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
@@ -4032,15 +4047,15 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
           hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
                              S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
           hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
-                             sn3, S3, N, Weff, nb3, tb3, out->status);
+                             sn3, S3, N, Weff, nb3, tb3, out->status, nullptr, dyn_ctr, W, Wcap);
           hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
-                             nb3, tb3, S2, ba2, bb2, nullptr);
+                             nb3, tb3, S2, ba2, bb2, nullptr, nullptr, 0u);
         } else {
           hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
-                             sn2, S2, N, Weff, ba2, bb2, out->status);
+                             sn2, S2, N, Weff, ba2, bb2, out->status, nullptr, dyn_ctr, W, Wcap);
         }
         hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
-                           ba2, bb2, Weff, sbase, nullptr, order);
+                           ba2, bb2, Weff, sbase, nullptr, order, dyn_ctr, W);
       }
       }
       if (check_launch(c, "rank")) return -1;
@@ -4084,8 +4099,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   const dim3 B256(256);
 
   HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
-  HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
-  if (out->visible_bits && N)
+  // one giant document: k_geff zeroes the count, k_pack_bits writes every word
+  const bool giant1 = is_giant(c, D, bt->doc_offsets);
+  if (!giant1) HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
+  if (out->visible_bits && N && !giant1)
     HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
   c->x_hint = true;  // unknown unless the fused front end counts the flagged documents
 
@@ -4246,6 +4263,16 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }  // general front end
 
     // 3-9. tree, walk, rank, emit, visibility
+    // one giant document: its status (domain bits final now) goes to pinned
+    // memory behind an event, so the exact path's check waits for this point
+    // of the stream only, not for the whole weave (no sync between launches)
+    if (is_giant(c, D, bt->doc_offsets)) {
+      if (!c->pin_status) HIPCHK(c, hipHostMalloc((void **)&c->pin_status, 64, hipHostMallocDefault));
+      if (!c->ev_status) HIPCHK(c, hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
+      HIPCHK(c, hipMemcpyAsync(c->pin_status, out->status, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
+      c->x_pending = true;
+    }
     // without yarns the id-sort buffers are free once the ids are joined
     const bool spare = !want_yarns;
     if (weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
@@ -4310,7 +4337,7 @@ int weave_lists_dev_all(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id,
     t_giant += n >= c->giant_min ? 0.4e-3 + nd * 0.3e-9 : 0.1e-3 + nd * 22e-9;
   }
   bool x_hint = false;
-  c->x_cached = false;
+  c->x_pending = false;
   if (D > 1 && D <= c->giant_docs_max && nd_max >= c->giant_min && t_giant < t_tree) {
     if (dres.visible_bits)
       HIPCHK(c, hipMemsetAsync(dres.visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
@@ -5071,7 +5098,7 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
       lr.weave_perm = lperm;
       lr.visible_count = lvc;
       lr.status = lst;
-      c->x_cached = false;  // (a chunk's giant key weave left its own status there)
+      c->x_pending = false;  // (a chunk's giant key weave left its own status there)
       if (exact_fixup(c, &lb, lid, lcause, lkind, &lr, true)) return -1;
     }
   }
@@ -5429,6 +5456,8 @@ void cw_ctx_destroy(cw_ctx *c) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   if (c->pinned) (void)hipHostFree(c->pinned);
   if (c->pin_small) (void)hipHostFree(c->pin_small);
+  if (c->pin_status) (void)hipHostFree(c->pin_status);
+  if (c->ev_status) (void)hipEventDestroy(c->ev_status);
   for (auto &p : c->pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);

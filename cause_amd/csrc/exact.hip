@@ -687,10 +687,11 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
   const uint64_t *off = bt->doc_offsets;
   if (!hint || D == 0 || off[D] == 0) return 0;
   if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-  if (D == 1 && c->x_cached && bt->key_bits && bt->key_bits < 64) {
-    // one giant list: its status came back with the walk's counter (KEY_RANGE,
-    // set later, needs key_bits >= 64)
-    const uint32_t st = c->x_status;
+  if (D == 1 && c->x_pending && bt->key_bits && bt->key_bits < 64) {
+    // one giant list: its status was copied out after the front end (KEY_RANGE,
+    // set later, needs key_bits >= 64); wait for that copy, not for the stream
+    HIPCHK(c, hipEventSynchronize(c->ev_status));
+    const uint32_t st = c->pin_status[0];
     if (!(st & X_MASK) || (st & X_SKIP)) return 0;
   } else if (D <= 16) {
     // a few documents: their status words in one readback
