@@ -180,6 +180,7 @@ def lib():
         L.cw_ctx_set_stream.argtypes = [C.c_void_p, C.c_void_p]
         L.cw_ctx_set_async.argtypes = [C.c_void_p, C.c_int]
         L.cw_ctx_set_profiling.argtypes = [C.c_void_p, C.c_int]
+        L.cw_ctx_set_profile_only.argtypes = [C.c_void_p, C.c_char_p]
         L.cw_get_kernel_stats.argtypes = [C.c_void_p, C.POINTER(CwKernelStat), C.c_int]
         L.cw_reset_kernel_stats.argtypes = [C.c_void_p]
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
@@ -312,6 +313,11 @@ class Weaver:
 
     def set_profiling(self, on: bool):
         self._check(self._L.cw_ctx_set_profiling(self._h, int(on)), "set_profiling")
+
+    def set_profile_only(self, kernel: str | None):
+        """Per-kernel events for this kernel stat name only (None: every kernel)."""
+        self._check(self._L.cw_ctx_set_profile_only(self._h, kernel.encode() if kernel else None),
+                    "set_profile_only")
 
     def kernel_stats(self):
         n = self._L.cw_get_kernel_stats(self._h, None, 0)

@@ -3351,6 +3351,7 @@ struct cw_ctx {
   hipStream_t stream = nullptr;
   bool async = false;
   bool prof = false;
+  std::string prof_only;           // cw_ctx_set_profile_only: time this kernel stat only
   std::string err;
   std::map<std::string, DevBuf> bufs;
   void *pinned = nullptr;
@@ -3468,7 +3469,7 @@ struct Launch {
   double bytes;
   hipEvent_t a = nullptr;
   Launch(cw_ctx *c_, const char *n, double by) : c(c_), name(n), bytes(by) {
-    if (c->prof) {
+    if (c->prof && (c->prof_only.empty() || c->prof_only == n)) {
       a = get_event(c);
       (void)hipEventRecord(a, c->stream);
     }
@@ -5487,6 +5488,12 @@ int cw_ctx_set_profiling(cw_ctx *c, int on) {
   if (!c) return -1;
   if (collect_prof(c, true)) return -1;
   c->prof = on != 0;
+  return 0;
+}
+
+int cw_ctx_set_profile_only(cw_ctx *c, const char *kernel) {
+  if (!c) return -1;
+  c->prof_only = kernel ? kernel : "";
   return 0;
 }
 

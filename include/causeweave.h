@@ -102,6 +102,10 @@ int cw_ctx_set_async(cw_ctx *ctx, int async);
 /* Per-kernel timing with HIP events on the launch stream (event pairs are read
  * back when the stats are asked for; asynchronous calls stay asynchronous). */
 int cw_ctx_set_profiling(cw_ctx *ctx, int on);
+/* Restrict the per-kernel events to one kernel stat name (NULL or "" = every
+ * kernel): a sub-millisecond call is then timed with two events instead of
+ * two per launch. */
+int cw_ctx_set_profile_only(cw_ctx *ctx, const char *kernel);
 
 typedef struct {
   char name[48];
