@@ -639,6 +639,140 @@ __global__ __launch_bounds__(1024) void k_join(
   if (threadIdx.x == 0 && bst) atomicOr(&status[d], bst);
 }
 
+// --- one giant document: the id order and the join by a global rank directory ----
+// (config 5)  Lamport ids are dense over [0, 2^key_bits): a bitmap
+// over that range with a running popcount ranks every id and every cause
+// directly, so the giant path's radix sort of the ids, its bucket index and
+// its searching join (a random 8-byte gather of each cause by input index)
+// become one pass that sets bits (atomicOr: a bit already set is a repeated
+// id), a scan, and one pass in INPUT order: two directory lines read per node
+// (its id's, its cause's) and par / kind / input index scattered by rank.
+// Entry e covers keys [480 e, 480 e + 480): word 0 = ones before the entry,
+// words 1..15 = the bits -- one 64-byte line answers "present?" and "rank".
+constexpr uint32_t GD_KEYS = 480, GD_WORDS = 16;
+constexpr uint32_t GD_MAX_BITS = 35;  // key range of the directory (<= 4.6 GB)
+
+__device__ __forceinline__ void gd_split(uint64_t x, uint64_t &e, uint32_t &b) {
+  e = x / GD_KEYS;
+  b = (uint32_t)(x - e * GD_KEYS);
+}
+
+// rank of key x (the number of set keys below it) and whether x is set
+__device__ __forceinline__ uint32_t gd_rank(const uint4 *__restrict__ dir, uint64_t x, bool &present) {
+  uint64_t e;
+  uint32_t b;
+  gd_split(x, e, b);
+  const uint4 *q = dir + e * (GD_WORDS / 4);
+  const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  const uint32_t w[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                          q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+  const uint32_t wi = b >> 5, bit = b & 31;
+  uint32_t r = w[0], hit = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 15; k++) {  // (masks, no run-time index: stays in VGPRs)
+    const uint32_t word = w[k + 1];
+    const uint32_t m = k < wi ? 0xFFFFFFFFu : (k == wi ? (1u << bit) - 1u : 0u);
+    r += __popc(word & m);
+    hit |= k == wi ? (word >> bit) & 1u : 0u;
+  }
+  present = hit != 0;
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_gd_set(const uint64_t *__restrict__ id, uint32_t n,
+                                                uint64_t E, uint32_t *__restrict__ dir,
+                                                unsigned long long *__restrict__ maxid,
+                                                uint32_t *__restrict__ status) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint64_t x = 0;
+  bool dup = false, out = false;
+  if (j < n) {
+    x = id[j];
+    uint64_t e;
+    uint32_t b;
+    gd_split(x, e, b);
+    const uint32_t bit = 1u << (b & 31);
+    if (e < E) dup = (atomicOr(&dir[e * GD_WORDS + 1 + (b >> 5)], bit) & bit) != 0;
+    else out = true;  // an id beyond key_bits: the caller's layout is wrong
+  }
+  if (__ballot(out) && (threadIdx.x & 63) == 0) atomicOr(status, (uint32_t)CW_STATUS_INTERNAL);
+  unsigned long long m = out ? 0ull : x;
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
+  const uint64_t anydup = __ballot(dup);
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(maxid, m);
+    if (anydup) atomicOr(status, (uint32_t)CW_STATUS_DUP);
+  }
+}
+
+// per 1024 entries: ones of each entry -> exclusive prefix inside the block
+// (word 0) and the block's total
+__global__ __launch_bounds__(1024) void k_gd_count(uint32_t *__restrict__ dir, uint64_t E,
+                                                   uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wtot[16];
+  const uint64_t e = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  uint32_t v = 0;
+  uint4 *q = reinterpret_cast<uint4 *>(dir) + e * (GD_WORDS / 4);
+  if (e < E) {
+    const uint4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+    v = __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) + __popc(q1.z) +
+        __popc(q1.w) + __popc(q2.x) + __popc(q2.y) + __popc(q2.z) + __popc(q2.w) + __popc(q3.x) +
+        __popc(q3.y) + __popc(q3.z) + __popc(q3.w);
+  }
+  uint32_t tot;
+  const uint32_t ex = block_exscan<1024>(v, wtot, &tot);
+  if (e < E) dir[e * GD_WORDS] = ex;
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_gd_add(uint32_t *__restrict__ dir, uint64_t E,
+                                                 const uint32_t *__restrict__ sums) {
+  const uint64_t e = (uint64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (e < E) dir[e * GD_WORDS] += sums[blockIdx.x];
+}
+
+// In input order: rank of the id and of the cause, the domain checks of
+// k_join, and par / kind / input index (/ the id for the yarns) by rank.
+__global__ __launch_bounds__(256) void k_gd_place(
+    const uint64_t *__restrict__ id, const uint64_t *__restrict__ cause,
+    const uint8_t *__restrict__ kind, uint32_t n, const uint4 *__restrict__ dir,
+    const unsigned long long *__restrict__ maxid, uint32_t ts_shift, uint64_t *__restrict__ max_ts,
+    uint32_t *__restrict__ par, uint8_t *__restrict__ skind, uint32_t *__restrict__ sval,
+    uint64_t *__restrict__ skey, uint32_t *__restrict__ status) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t st = 0;
+  if (j < n) {
+    const uint64_t kmax = *maxid;
+    const uint64_t x = min((unsigned long long)id[j], kmax), c = cause[j];  // (min: see k_gd_set)
+    const uint8_t kd = kind[j];
+    bool pres;
+    const uint32_t r = gd_rank(dir, x, pres);
+    uint32_t p = 0;
+    if (r == 0) {
+      if (!(kd & KIND_ROOT)) st |= CW_STATUS_ROOT;
+    } else {
+      if (kd & KIND_ROOT) st |= CW_STATUS_ROOT;
+      bool cp = false;
+      const uint32_t rc = c <= kmax ? gd_rank(dir, c, cp) : 0u;
+      if (!cp) st |= CW_STATUS_ORPHAN;
+      else if (rc >= r) st |= CW_STATUS_NON_LAMPORT;
+      else p = rc;
+    }
+    if (r < n) {  // (a repeated id ranks two nodes alike: the document is flagged DUP)
+      par[r] = p;
+      skind[r] = kd;
+      sval[r] = j;
+      if (skey) skey[r] = x;
+    }
+    if (j == 0 && max_ts) *max_ts = kmax >> ts_shift;
+  }
+  const uint64_t any = __ballot(st != 0);
+  if (any) {
+    for (int o = 32; o > 0; o >>= 1) st |= __shfl_xor(st, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicOr(status, st);
+  }
+}
+
 // --- front end by rank directory: id order and cause join without a sort ---------
 // Lamport ids are dense: a document of n nodes from s sites has ids inside a
 // range of about (max ts) * 2^site_bits keys.  A bitmap over [kmin, kmax]
@@ -3384,6 +3518,7 @@ struct cw_ctx {
   uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
   uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
   uint32_t tl_mode = 0;            // CW_TL_MODE: k_tree_l variant bits (A/B)
+  uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
@@ -4181,6 +4316,43 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         sval = nullptr;
         skey = nullptr;
         kbm = nullptr;
+      }
+    }
+    // one giant document whose ids fit a global rank directory:
+    // no id sort, no bucket index, no searching join
+    // (a directory larger than the caches makes k_gd_set's atomics HBM round
+    // trips: 6.7e7 nodes over 2^31 keys took 12.8 ms against 8.3 for sort +
+    // join, so the directory is taken only while it stays small)
+    if (!front_done && c->gdir && is_giant(c, D, bt->doc_offsets) && key_bits <= GD_MAX_BITS &&
+        (1ull << key_bits) / GD_KEYS * GD_WORDS * 4 <= (uint64_t)c->gdir * (1ull << 20)) {
+      const uint64_t E = ((1ull << key_bits) + GD_KEYS - 1) / GD_KEYS;
+      const uint32_t nb = (uint32_t)((E + 1023) / 1024);
+      uint32_t *dir = scratch_t<uint32_t>(c, "gd_dir", E * GD_WORDS);
+      uint32_t *sums = scratch_t<uint32_t>(c, "gd_sums", nb + 1);
+      unsigned long long *maxid = scratch_t<unsigned long long>(c, "gd_max", 1);
+      if (dir && sums && maxid) {
+        HIPCHK(c, hipMemsetAsync(dir, 0, E * GD_WORDS * 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(maxid, 0, 8, c->stream));
+        const dim3 GN((N + 255) / 256);
+        {
+          Launch L(c, "gdir", (double)N * 8 + (double)E * GD_WORDS * 4 * 2);
+          hipLaunchKernelGGL(k_gd_set, GN, dim3(256), 0, c->stream, id_key, N, E, dir, maxid,
+                             out->status);
+          hipLaunchKernelGGL(k_gd_count, dim3(nb), dim3(1024), 0, c->stream, dir, E, sums);
+          hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, c->stream, sums, nb, sums + nb);
+          hipLaunchKernelGGL(k_gd_add, dim3(nb), dim3(1024), 0, c->stream, dir, E, sums);
+        }
+        if (check_launch(c, "gdir")) return -1;
+        skey = want_yarns ? skA : nullptr;
+        sval = svA;
+        {
+          Launch L(c, "gplace", (double)N * (8 + 8 + 1 + 4 + 1 + 4 + (skey ? 8 : 0)) + (double)N * 2 * 64);
+          hipLaunchKernelGGL(k_gd_place, GN, dim3(256), 0, c->stream, id_key, cause_key, kind, N,
+                             reinterpret_cast<const uint4 *>(dir), maxid, bt->ts_shift, out->max_ts,
+                             par, skind, sval, skey, out->status);
+        }
+        if (check_launch(c, "gplace")) return -1;
+        front_done = true;
       }
     }
     if (!front_done && c->front && N >= (uint64_t)c->front_min_avg * D && t.nmax <= 64 * TILE) {
@@ -5433,6 +5605,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_pad = knob("CW_TREE_PAD", 0);
   c->tree_l = knob("CW_TREE_L", 2048);
   c->tl_mode = knob("CW_TL_MODE", 0);
+  c->gdir = knob("CW_GDIR", 32);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
