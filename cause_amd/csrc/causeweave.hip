@@ -731,6 +731,119 @@ __global__ __launch_bounds__(1024) void k_gd_add(uint32_t *__restrict__ dir, uin
   if (e < E) dir[e * GD_WORDS] += sums[blockIdx.x];
 }
 
+// The same directory from the SORTED ids (the giant path after its id sort):
+// neighbouring lanes set bits of the same or the next words, so the atomics
+// stay in L2; a repeated id shows as two equal neighbours.
+__global__ __launch_bounds__(256) void k_gd_set_sorted(const uint64_t *__restrict__ skey, uint32_t n,
+                                                       uint64_t E, uint32_t *__restrict__ dir,
+                                                       uint32_t *__restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  bool dup = false, out = false;
+  uint64_t w = ~0ull;  // word index (the ids are sorted: equal words are neighbouring lanes)
+  uint32_t v = 0;
+  if (i < n) {
+    const uint64_t x = skey[i];
+    dup = i > 0 && skey[i - 1] == x;
+    uint64_t e;
+    uint32_t b;
+    gd_split(x, e, b);
+    if (e < E) {
+      w = e * GD_WORDS + 1 + (b >> 5);
+      v = 1u << (b & 31);
+    } else {
+      out = true;
+    }
+  }
+  // OR of each run of lanes with the same word; the run's first lane writes it
+  // (a plain store; atomically only for runs that may continue in the
+  // neighbouring waves)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_down(v, o, 64);
+    const uint64_t wy = __shfl_down(w, o, 64);
+    if (lane + o < 64 && wy == w) v |= y;
+  }
+  const uint64_t wp = __shfl_up(w, 1, 64);
+  const uint64_t wlast = __shfl(w, 63, 64);
+  if (w != ~0ull && (lane == 0 || wp != w)) {
+    if (lane == 0 || w == wlast) atomicOr(&dir[w], v);
+    else dir[w] = v;
+  }
+  const uint64_t d = __ballot(dup), o = __ballot(out);
+  if ((threadIdx.x & 63) == 0 && (d | o))
+    atomicOr(status, (d ? (uint32_t)CW_STATUS_DUP : 0u) | (o ? (uint32_t)CW_STATUS_INTERNAL : 0u));
+}
+
+// Word 0 of each directory entry from the sorted ids, no scan: the ones before
+// entry e are the rank of the first id at or above its range (like k_index_flat's
+// buckets, 480 keys wide); the entries a thread starts are zeroed for
+// k_gd_set_sorted.  Entries past the largest id are never read.
+__global__ __launch_bounds__(256) void k_gd_first(const uint64_t *__restrict__ skey, uint32_t n,
+                                                  uint64_t E, uint32_t *__restrict__ dir) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t e = min(skey[i] / GD_KEYS, E - 1);
+  const uint64_t e0 = i > 0 ? min(skey[i - 1] / GD_KEYS, E - 1) + 1 : 0;
+  for (uint64_t x = e0; x <= e; x++) {
+    uint4 *q = reinterpret_cast<uint4 *>(dir + x * GD_WORDS);
+    q[0] = make_uint4(i, 0, 0, 0);
+    q[1] = q[2] = q[3] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// k_join for one giant document with the directory: each rank's cause and kind
+// gathered by input index (as k_join), the cause's rank from one directory
+// line instead of the bucket index and a search.
+constexpr int GJOIN_ITEMS = 4;
+__global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey,
+                                               const uint32_t *__restrict__ sval,
+                                               const uint64_t *__restrict__ cause_key,
+                                               const uint8_t *__restrict__ kind, uint32_t n,
+                                               const uint4 *__restrict__ dir,
+                                               uint32_t *__restrict__ par, uint8_t *__restrict__ skind,
+                                               uint32_t *__restrict__ status) {
+  const uint32_t i0 = blockIdx.x * (256 * GJOIN_ITEMS) + threadIdx.x;
+  const uint64_t kmax = skey[n - 1];
+  uint32_t gi[GJOIN_ITEMS];
+  uint64_t ck[GJOIN_ITEMS];
+  uint8_t kd[GJOIN_ITEMS];
+#pragma unroll
+  for (int k = 0; k < GJOIN_ITEMS; k++) {
+    const uint32_t i = i0 + k * 256;
+    gi[k] = i < n ? sval[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < GJOIN_ITEMS; k++) {
+    const uint32_t i = i0 + k * 256;
+    ck[k] = i < n ? cause_key[gi[k]] : 0ull;
+    kd[k] = i < n ? kind[gi[k]] : 0;
+  }
+  uint32_t st = 0;
+#pragma unroll
+  for (int k = 0; k < GJOIN_ITEMS; k++) {
+    const uint32_t r = i0 + k * 256;
+    if (r >= n) continue;
+    uint32_t p = 0;
+    if (r == 0) {
+      if (!(kd[k] & KIND_ROOT)) st |= CW_STATUS_ROOT;
+    } else {
+      if (kd[k] & KIND_ROOT) st |= CW_STATUS_ROOT;
+      bool cp = false;
+      const uint32_t rc = ck[k] <= kmax ? gd_rank(dir, ck[k], cp) : 0u;
+      if (!cp) st |= CW_STATUS_ORPHAN;
+      else if (rc >= r) st |= CW_STATUS_NON_LAMPORT;
+      else p = rc;
+    }
+    par[r] = p;
+    skind[r] = kd[k];
+  }
+  const uint64_t any = __ballot(st != 0);
+  if (any) {
+    for (int o = 32; o > 0; o >>= 1) st |= __shfl_xor(st, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicOr(status, st);
+  }
+}
+
 // In input order: rank of the id and of the cause, the domain checks of
 // k_join, and par / kind / input index (/ the id for the yarns) by rank.
 __global__ __launch_bounds__(256) void k_gd_place(
@@ -3519,6 +3632,7 @@ struct cw_ctx {
   uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
   uint32_t tl_mode = 0;            // CW_TL_MODE: k_tree_l variant bits (A/B)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
+  uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
@@ -4414,6 +4528,29 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       return -1;
 
     // 2. join
+    // one giant document: a rank directory built from the sorted ids answers
+    // each cause with one line (no bucket index, no search)
+    const uint64_t E = ((1ull << std::min(key_bits, 63u)) + GD_KEYS - 1) / GD_KEYS;
+    uint32_t *gdir = nullptr;
+    if (is_giant(c, D, bt->doc_offsets) && c->gjoin && key_bits <= GD_MAX_BITS) {
+      gdir = scratch_t<uint32_t>(c, "gd_dir", E * GD_WORDS);
+    }
+    if (gdir) {
+      {
+        Launch L(c, "index", (double)N * 8 * 2 + (double)N / 15 * 64);
+        hipLaunchKernelGGL(k_gd_first, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir);
+        hipLaunchKernelGGL(k_gd_set_sorted, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir,
+                           out->status);
+      }
+      if (check_launch(c, "index")) return -1;
+      {
+        Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1) + (double)N * 64);
+        hipLaunchKernelGGL(k_gjoin, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
+                           c->stream, skey, sval, cause_key, kind, N,
+                           reinterpret_cast<const uint4 *>(gdir), par, skind, out->status);
+      }
+      if (check_launch(c, "join")) return -1;
+    } else {
     uint32_t *bkt = scratch_t<uint32_t>(c, "bkt", t.Btot);
     if (!bkt) return fail(c, "out of device memory (bucket index)");
     {
@@ -4433,6 +4570,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                          out->status);
     }
     if (check_launch(c, "join")) return -1;
+    }  // bucket index
     }  // general front end
 
     // 3-9. tree, walk, rank, emit, visibility
@@ -5606,6 +5744,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_l = knob("CW_TREE_L", 2048);
   c->tl_mode = knob("CW_TL_MODE", 0);
   c->gdir = knob("CW_GDIR", 32);
+  c->gjoin = knob("CW_GJOIN", 1);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
