@@ -1207,7 +1207,7 @@ __global__ __launch_bounds__(NT) void k_front(
     uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t eff) {
+    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t doc0 = 0) {
   extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -1221,7 +1221,7 @@ __global__ __launch_bounds__(NT) void k_front(
   __shared__ uint64_t rmax[NT / 64];
   __shared__ uint32_t wtot[NT / 64];
   __shared__ uint32_t bst;
-  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, nw = (n + 31) / 32;
   const uint64_t *const idD = id_key + base, *const causeD = cause_key + base;
   const uint8_t *const kindD = kind + base;
@@ -1770,7 +1770,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
     uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
     unsigned long long *__restrict__ tprof,
-    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first) {
+    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first, uint32_t doc0 = 0) {
   constexpr uint32_t IT = TILE_T / NT;
   unsigned long long tacc[16] = {}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -1796,7 +1796,7 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   __shared__ uint32_t run[64];
   __shared__ uint32_t n_osp;
   extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
-  const uint32_t d = blockIdx.x, tid = threadIdx.x;
+  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   // this document's slices (wave-uniform bases, lane offsets: lane_at)
   const uint32_t *const parD = par + base;
@@ -2731,7 +2731,8 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
                                              uint32_t *__restrict__ perm, uint32_t *__restrict__ vbits,
                                              uint32_t *__restrict__ vcount,
                                              uint32_t *__restrict__ status, uint32_t *loc,
-                                             unsigned long long *__restrict__ tprof) {
+                                             unsigned long long *__restrict__ tprof,
+                                             uint32_t doc0 = 0) {
   constexpr uint32_t SPT = 8;  // sublists per thread in the jumping rounds: S <= SPT * NT
   extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   __shared__ uint32_t wtot[NT / 64];
@@ -2745,7 +2746,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
     }
   };
   stamp(-1);
-  const uint32_t d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   const uint32_t *const linkD = link + base;
   uint32_t *const locD = loc + base, *const permD = perm + base;
@@ -3716,17 +3717,19 @@ struct Launch {
   cw_ctx *c;
   const char *name;
   double bytes;
+  hipStream_t s;
   hipEvent_t a = nullptr;
-  Launch(cw_ctx *c_, const char *n, double by) : c(c_), name(n), bytes(by) {
+  Launch(cw_ctx *c_, const char *n, double by, hipStream_t st = nullptr)
+      : c(c_), name(n), bytes(by), s(st ? st : c_->stream) {
     if (c->prof && (c->prof_only.empty() || c->prof_only == n)) {
       a = get_event(c);
-      (void)hipEventRecord(a, c->stream);
+      (void)hipEventRecord(a, s);
     }
   }
   ~Launch() {
     if (c->prof && a) {
       hipEvent_t b = get_event(c);
-      (void)hipEventRecord(b, c->stream);
+      (void)hipEventRecord(b, s);
       c->pending.push_back({name, a, b, bytes});
     }
   }
@@ -4158,7 +4161,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     auto tree_l_kernel = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(TL_NT), (size_t)tl_dyn, c->stream, par, skind,
                          doc_off, doc_log2k, kbits, (t.nmax + 31) / 32, nsc, fcS,
-                         (uint32_t *)link, thr, tprof, kbm, dev_tab(c, "t_tile_first"));
+                         (uint32_t *)link, thr, tprof, kbm, dev_tab(c, "t_tile_first"), 0u);
     };
     auto tree_l_mode = [&](auto prof, auto mode) {
       constexpr bool P = decltype(prof)::value;
