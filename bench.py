@@ -59,6 +59,14 @@ def parse():
     ap.add_argument("--no-prestaged", action="store_true",
                     help="--config 3: skip the pass with the inputs pre-staged in host memory")
     ap.add_argument("--giant", type=int, default=1 << 26, help="--config 5: nodes in the list")
+    ap.add_argument("--ranking", default="auto", choices=["auto", "ruling", "root"],
+                    help="--config 5 --dist with the tree by rank: list ranking by a ruling set "
+                         "where the list lies (ruling) or on rank 0 (root); auto = ruling for N > 1")
+    ap.add_argument("--out", default="root", choices=["root", "sharded"],
+                    help="--config 5 --dist --ranking ruling: the weave on rank 0, or spread "
+                         "over the ranks by weave position")
+    ap.add_argument("--ruler-k", type=int, default=16,
+                    help="--config 5 --ranking ruling: one ruler per ~K nodes")
     ap.add_argument("--colls", type=int, default=1_000_000, help="--config 4: collections per GPU")
     ap.add_argument("--dist", action="store_true",
                     help="--config 5 on one GPU through the distributed path (sample sort, "
@@ -277,6 +285,40 @@ def cpu_baseline_maps(spec, budget_s):
                       f"literal map weave + active-node (map.cljc:21-59) in C, {t_total:.1f} s"}
 
 
+def check_giant_dist(res, idk, ck, kd, world, rank, dist, N, sharded):
+    """--check for --config 5 --dist: the weave (on rank 0, or its slices
+    gathered there) against the oracle's weave of the whole list (rank r holds
+    nodes r, r + world, ... of the generation order)."""
+    import oracle
+
+    parts = None
+    if sharded:
+        parts = [None] * world
+        dist.all_gather_object(parts, (res.pos_base, res.weave_perm.cpu().numpy(),
+                                       res.visible_bits.cpu().numpy()))
+    if rank != 0:
+        return
+    if parts is not None:
+        parts.sort(key=lambda p: p[0])
+        wp = np.concatenate([p[1] for p in parts]).view(np.uint32)
+        vis = np.concatenate([np.unpackbits(p[2].view(np.uint8), bitorder="little")[:len(p[1])]
+                              for p in parts])
+    else:
+        wp = res.weave_perm.cpu().numpy().view(np.uint32)
+        vis = np.unpackbits(res.visible_bits.cpu().numpy().view(np.uint8), bitorder="little")[:N]
+    # global input index: rank r's local i is node r + i * world
+    counts = [len(range(r, N, world)) for r in range(world)]
+    start = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    r_of = np.repeat(np.arange(world), counts)
+    node = r_of + (np.arange(N) - start[r_of]) * world
+    perm, want_vis, st = oracle.batch_lists(np.array([0, N], np.uint64), idk, ck, kd,
+                                            method=oracle.METHOD_EFF)
+    ok = bool(np.array_equal(node[wp], perm)) and bool(np.array_equal(vis, want_vis))
+    print(json.dumps({"check": "config5 dist", "nodes": N, "ok": ok}), flush=True)
+    if not ok:
+        raise SystemExit("config 5 --check: the weave differs from the oracle")
+
+
 def main_giant_dist(a, world, rank, local, dist, torch, dev):
     """--config 5 on N GPUs: ONE list of --giant nodes whose nodes are spread
     over the ranks (rank r holds every N-th node of the generation order).
@@ -292,6 +334,8 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
 
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.giant)
     lay = spec.layout()
+    tree_dist = a.tree == "dist" or (a.tree == "auto" and world > 1)
+    ruling = tree_dist and (a.ranking == "ruling" or (a.ranking == "auto" and world > 1))
     t0 = time.time()
     with heartbeat("generating the input"):
         off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
@@ -301,8 +345,9 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     g_id = torch.from_numpy(np.ascontiguousarray(idk[sel]).view(np.int64)).to(dev)
     g_ca = torch.from_numpy(np.ascontiguousarray(ck[sel]).view(np.int64)).to(dev)
     g_kd = torch.from_numpy(np.ascontiguousarray(kd[sel])).to(dev)
-    if rank != 0 or a.no_cpu:
+    if rank != 0 or (a.no_cpu and not a.check):
         del idk, ck, kd
+        idk = ck = kd = None
     torch.cuda.synchronize()
     group = None
     if world == 1:  # one rank: a private gloo group only for the (empty) exchange bookkeeping
@@ -319,14 +364,17 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
 
     def step():
         return giant.weave_distributed(ops, g_id, g_ca, g_kd, lay.key_bits, ts_shift=lay.ts_shift,
-                                       group=group, tree=a.tree)
+                                       group=group, tree=a.tree, ranking=a.ranking, out=a.out,
+                                       ruler_k=a.ruler_k)
 
     res = None
     for _ in range(a.warmup):
         res = step()
     torch.cuda.synchronize()
-    if rank == 0 and res is not None and res.status != 0:
+    if res is not None and res.status not in (None, 0):
         raise SystemExit(f"status {res.status}")
+    if a.check and res is not None:
+        check_giant_dist(res, idk, ck, kd, world, rank, dist, N, ruling and a.out == "sharded")
     w.reset_kernel_stats()
     w.set_profiling(True)
     dist.barrier()
@@ -357,8 +405,10 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
             "scaling": "strong", "vs_baseline": None, "dtype": "u64", "data": "synthetic",
             "config": {"workload": (f"config5: one CausalList of {N:,} nodes spread over "
                                     f"{world} rank(s), distributed sample sort + "
-                                    f"{'tree by rank' if a.tree == 'dist' or (a.tree == 'auto' and world > 1) else 'tree on rank 0'}"),
-                       "tree": a.tree,
+                                    + (f"tree by rank + {'ruling-set ranking (K=%d, weave %s)' % (a.ruler_k, 'on rank 0' if a.out == 'root' else 'sharded by position') if ruling else 'list ranking on rank 0'}"
+                                       if tree_dist else "tree on rank 0")),
+                       "tree": a.tree, "ranking": a.ranking if tree_dist else None,
+                       "out": a.out if tree_dist and ruling else "root",
                        "nodes_total": N, "sites": spec.n_sites, "p_hide": spec.p_hide,
                        "key_bits": lay.key_bits,
                        "parallelism": f"sample sort x{world} ({dist.get_backend()})"},

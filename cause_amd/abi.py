@@ -114,6 +114,8 @@ _DIST_ARGS = {
     "pending": "P U64 P P", "gkey": "P P U64 P", "runs": "P P U64 U32 P P P P",
     "rkey": "P U64 P", "link": "P P U64 P U32 U64 P P P", "put": "P P U64 U32 U64 P",
     "thr": "P U64 U32 P", "succ": "P P P U64 U32 P",
+    "rs_rulers": "P P U64 U32 U32 U32 P P P", "rs_walk": "P U64 P U32 P P U64 U32 P P P P P P",
+    "rs_top": "P U64 U64 P P", "rs_pos": "P P P P U64 P P", "rs_emit": "P U64 U32 U64 P P P P",
 }
 
 

@@ -5969,6 +5969,32 @@ int cw_dist_succ(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const uint
                  uint64_t n, uint32_t base, uint32_t *out) {
   CW_DIST_ENTRY(dist_succ_impl(c, kind, fcS, fcN, n, base, out))
 }
+int cw_dist_rs_rulers(cw_ctx *c, const uint32_t *succ, const uint32_t *thr, uint64_t n,
+                      uint32_t base, uint32_t k, uint32_t seed, uint32_t *word, uint32_t *rlist,
+                      uint32_t *count) {
+  CW_DIST_ENTRY(dist_rs_rulers_impl(c, succ, thr, n, base, k, seed, word, rlist, count))
+}
+int cw_dist_rs_walk(cw_ctx *c, const uint32_t *walkers, uint64_t m, const uint32_t *rlist,
+                    uint32_t rbase, const uint32_t *word, const uint32_t *thr, uint64_t n,
+                    uint32_t base, uint32_t *own, uint32_t *links, uint32_t *nlinks, uint32_t *out,
+                    uint64_t *key, uint32_t *status) {
+  CW_DIST_ENTRY(dist_rs_walk_impl(c, walkers, m, rlist, rbase, word, thr, n, base, own, links,
+                                  nlinks, out, key, status))
+}
+int cw_dist_rs_top(cw_ctx *c, const uint32_t *links, uint64_t m, uint64_t total, uint32_t *pos,
+                   uint32_t *status) {
+  CW_DIST_ENTRY(dist_rs_top_impl(c, links, m, total, pos, status))
+}
+int cw_dist_rs_pos(cw_ctx *c, const uint32_t *own, const uint32_t *pos_base, const uint32_t *succ,
+                   const uint32_t *val, uint64_t n, uint32_t *rec, uint64_t *key) {
+  CW_DIST_ENTRY(dist_rs_pos_impl(c, own, pos_base, succ, val, n, rec, key))
+}
+int cw_dist_rs_emit(cw_ctx *c, const uint32_t *rec, uint64_t m, uint32_t p0, uint64_t len,
+                    uint32_t *weave_perm, uint32_t *visible_bits, uint32_t *visible_count,
+                    uint32_t *status) {
+  CW_DIST_ENTRY(dist_rs_emit_impl(c, rec, m, p0, len, weave_perm, visible_bits, visible_count,
+                                  status))
+}
 #undef CW_DIST_ENTRY
 
 int cw_weave_linked(cw_ctx *c, const cw_linked_list *l, cw_list_result *r) {

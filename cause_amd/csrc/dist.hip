@@ -292,6 +292,218 @@ __global__ __launch_bounds__(256) void k_linked_words(const uint32_t *__restrict
   thr[r] = (t & THRW_PEND) ? t : (t < n ? t : SUCCW_END);
 }
 
+// ---- Ruling-set list ranking over the ranks ------------------
+// The preorder list crosses ranks at ~42% of its steps (W = 8), so it is
+// ranked where it lies: rulers (global rank 0, and every node whose hash falls
+// under 2^32 / K) start one walker each; a walker numbers the nodes it visits
+// (own = {ruler, offset}) until it reaches the next ruler or the list's end
+// (a link {ruler, next ruler, length}), and hops to another rank as a message
+// {ruler, count, target} whenever the list does.  The links -- one per ruler
+// -- are ranked on one GPU (k_rs_jump), and every node's weave position is
+// its ruler's position + its offset.
+constexpr uint32_t RS_CHASE = 0x80000000u;  // next word / target: follow this node's thread
+constexpr uint32_t RS_NONE = 0xFFFFFFFFu;   // word.y of a non-ruler; link: the list ends
+
+__device__ __forceinline__ bool rs_is_ruler(uint32_t g, uint32_t k, uint32_t seed) {
+  return g == 0 || (uint64_t)mix32(seed, g) * k < (1ull << 32);
+}
+
+// Pass 1 of the ruler numbering: in-block exclusive count (parked in word.y)
+// and the block's total.
+__global__ __launch_bounds__(1024) void k_rs_flag(uint32_t n, uint32_t base, uint32_t k,
+                                                  uint32_t seed, uint2 *__restrict__ word,
+                                                  uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wtot[16];
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t f = i < n && rs_is_ruler(base + i, k, seed) ? 1u : 0u;
+  uint32_t tot;
+  const uint32_t ex = block_exscan<1024>(f, wtot, &tot);
+  if (i < n) word[i].y = ex;
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// Pass 2: word = {next, ruler index or RS_NONE}; next = the successor, the
+// resolved thread, RS_CHASE | the ancestor whose thread it is, or SUCCW_END.
+__global__ __launch_bounds__(1024) void k_rs_index(const uint32_t *__restrict__ succ,
+                                                   const uint32_t *__restrict__ thr, uint32_t n,
+                                                   uint32_t base, uint32_t k, uint32_t seed,
+                                                   const uint32_t *__restrict__ sums,
+                                                   uint2 *__restrict__ word,
+                                                   uint32_t *__restrict__ rlist) {
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  if (i >= n) return;
+  uint32_t nx = succ[i] & ~LINK_VIS;
+  if (nx == DIST_FROM_THR) {
+    const uint32_t t = thr[i];
+    nx = (t & THRW_PEND) ? (RS_CHASE | (t & ~THRW_PEND)) : t;
+  }
+  uint32_t r = RS_NONE;
+  if (rs_is_ruler(base + i, k, seed)) {
+    r = word[i].y + sums[blockIdx.x];
+    rlist[r] = i;
+  }
+  word[i] = make_uint2(nx, r);
+}
+
+// One launch per exchange round: walker i (walkers == NULL: the run's ruler
+// i, starting) walks while its list stays on this rank.  Messages: out[i] =
+// {ruler, count, target, 0} with key[i] = the target's global rank (for the
+// partition by owner), UINT64_MAX when walker i stopped here.
+__global__ __launch_bounds__(256) void k_rs_walk(const uint4 *__restrict__ wk, uint32_t m,
+                                                 const uint32_t *__restrict__ rlist, uint32_t rbase,
+                                                 const uint2 *__restrict__ word,
+                                                 const uint32_t *__restrict__ thr, uint32_t n,
+                                                 uint32_t base, uint2 *__restrict__ own,
+                                                 uint4 *__restrict__ links,
+                                                 uint32_t *__restrict__ nlinks,
+                                                 uint4 *__restrict__ out,
+                                                 uint64_t *__restrict__ key,
+                                                 uint32_t *__restrict__ status) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= m) return;
+  uint32_t R, cnt, tgt;
+  if (wk) {
+    const uint4 w = wk[i];
+    R = w.x;
+    cnt = w.y;
+    tgt = w.z;
+  } else {
+    R = rbase + i;
+    cnt = 0;
+    tgt = base + rlist[i];
+  }
+  uint64_t kk = ~0ull;
+  bool link = false, bad = false;
+  uint32_t lnext = RS_NONE;
+  // every step numbers a node of the run or climbs to an older ancestor
+  // (threads point to lower ranks): 2n + 2 steps bound a valid walk
+  for (uint32_t hop = 0;; hop++) {
+    if (hop > 2 * n + 2) {
+      bad = true;
+      break;
+    }
+    const uint32_t a = tgt & ~RS_CHASE;
+    if (a - base >= n) {  // another rank's node (a < base wraps)
+      kk = a;
+      break;
+    }
+    uint32_t nx;
+    if (tgt & RS_CHASE) {
+      const uint32_t t = thr[a - base];
+      nx = (t & THRW_PEND) ? (RS_CHASE | (t & ~THRW_PEND)) : t;
+    } else {
+      const uint2 wd = word[a - base];
+      if (wd.y != RS_NONE && cnt > 0) {  // the next ruler: this sublist ends
+        link = true;
+        lnext = rbase + wd.y;
+        break;
+      }
+      own[a - base] = make_uint2(R, cnt);
+      cnt++;
+      nx = wd.x;
+    }
+    if (nx == SUCCW_END) {
+      link = true;
+      break;
+    }
+    tgt = nx;
+  }
+  key[i] = kk;
+  out[i] = make_uint4(R, cnt, tgt, 0u);
+  if (bad) atomicOr(status, CW_STATUS_INTERNAL);
+  // links appended with one atomic per wave
+  const uint64_t b = __ballot(link);
+  if (b) {
+    const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__ffsll((long long)b) - 1;
+    uint32_t s0 = 0;
+    if (lane == lead) s0 = atomicAdd(nlinks, (uint32_t)__popcll(b));
+    s0 = __shfl(s0, lead, 64);
+    if (link) links[s0 + lanes_below(b)] = make_uint4(R, lnext, cnt, 0u);
+  }
+}
+
+// The ruler list on one GPU: A[r] = {next ruler, length} from the links.
+__global__ __launch_bounds__(256) void k_rs_links(const uint4 *__restrict__ links, uint32_t m,
+                                                  uint2 *__restrict__ A) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint4 l = links[j];
+  if (l.x < m) A[l.x] = make_uint2(l.y, l.z);
+}
+
+// One pointer-jumping round: {next, nodes from here to the end}.
+__global__ __launch_bounds__(256) void k_rs_jump(const uint2 *__restrict__ A, uint32_t m,
+                                                 uint2 *__restrict__ B) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint2 v = A[j];
+  if (v.x < m) {
+    const uint2 w = A[v.x];
+    B[j] = make_uint2(w.x, v.y + w.y);
+  } else {
+    B[j] = make_uint2(RS_NONE, v.y);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rs_base(const uint2 *__restrict__ A, uint32_t m,
+                                                 uint32_t total, uint32_t *__restrict__ pos,
+                                                 uint32_t *__restrict__ status) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint2 v = A[j];
+  pos[j] = total - v.y;
+  // one list from ruler 0 over every node, and every walk ran to the end
+  if (j == 0 && (v.y != total || v.x != RS_NONE)) atomicOr(status, CW_STATUS_INTERNAL);
+}
+
+// Weave position of each node of the run and its emit record {position,
+// val | render << 31}; key = the position (for an emit spread by position).
+__global__ __launch_bounds__(256) void k_rs_pos(const uint2 *__restrict__ own,
+                                                const uint32_t *__restrict__ pbase,
+                                                const uint32_t *__restrict__ succ,
+                                                const uint32_t *__restrict__ val, uint32_t n,
+                                                uint2 *__restrict__ rec,
+                                                uint64_t *__restrict__ key) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint2 o = own[i];
+  const uint32_t p = pbase[o.x] + o.y;
+  rec[i] = make_uint2(p, (val[i] & 0x7FFFFFFFu) | (succ[i] & LINK_VIS));
+  if (key) key[i] = p;
+}
+
+// At the owner of positions [p0, p0 + len): weave_perm and the render bytes;
+// one count atomic per block (grid-stride over a fixed grid).
+__global__ __launch_bounds__(256) void k_rs_emit(const uint2 *__restrict__ rec, uint32_t m,
+                                                 uint32_t p0, uint32_t len,
+                                                 uint32_t *__restrict__ perm,
+                                                 uint8_t *__restrict__ vis8,
+                                                 uint32_t *__restrict__ count,
+                                                 uint32_t *__restrict__ status) {
+  __shared__ uint32_t wsum[4];
+  uint32_t c = 0;
+  bool bad = false;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < m; j += gridDim.x * blockDim.x) {
+    const uint2 r = rec[j];
+    const uint32_t p = r.x - p0;
+    if (p >= len) {
+      bad = true;
+      continue;
+    }
+    perm[p] = r.y & 0x7FFFFFFFu;
+    vis8[p] = (uint8_t)(r.y >> 31);
+    c += r.y >> 31;
+  }
+  if (bad) atomicOr(status, CW_STATUS_INTERNAL);
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (t) atomicAdd(count, t);
+  }
+}
+
 int dist_launch_ok(cw_ctx *c, const char *nm) { return check_launch(c, nm); }
 
 #define DIST_GRID(m) dim3((uint32_t)(((m) + 255) / 256)), dim3(256), 0, c->stream
@@ -378,6 +590,90 @@ int dist_succ_impl(cw_ctx *c, const uint8_t *kind, const uint32_t *fcS, const ui
   Launch L(c, "dist_succ", (double)n * (1 + 4 + 4 + 4));
   hipLaunchKernelGGL(k_dist_succ, DIST_GRID(n), kind, fcS, fcN, (uint32_t)n, base, out);
   return dist_launch_ok(c, "dist_succ");
+}
+
+int dist_rs_rulers_impl(cw_ctx *c, const uint32_t *succ, const uint32_t *thr, uint64_t n,
+                        uint32_t base, uint32_t k, uint32_t seed, uint32_t *word, uint32_t *rlist,
+                        uint32_t *count) {
+  if (k == 0) return fail(c, "rs_rulers: k >= 1");
+  if (!n) {
+    HIPCHK(c, hipMemsetAsync(count, 0, 4, c->stream));
+    return 0;
+  }
+  const uint32_t nb = (uint32_t)((n + 1023) / 1024);
+  uint32_t *sums = scratch_t<uint32_t>(c, "rs_sums", (size_t)nb + 1);
+  if (!sums) return fail(c, "out of device memory (rs_rulers)");
+  uint2 *w2 = reinterpret_cast<uint2 *>(word);
+  Launch L(c, "rs_rulers", (double)n * (4 + 4 + 8 + 8 + 4.0 / k));
+  hipLaunchKernelGGL(k_rs_flag, dim3(nb), dim3(1024), 0, c->stream, (uint32_t)n, base, k, seed, w2,
+                     sums);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, c->stream, sums, nb, sums + nb);
+  hipLaunchKernelGGL(k_rs_index, dim3(nb), dim3(1024), 0, c->stream, succ, thr, (uint32_t)n, base,
+                     k, seed, sums, w2, rlist);
+  HIPCHK(c, hipMemcpyAsync(count, sums + nb, 4, hipMemcpyDeviceToDevice, c->stream));
+  return dist_launch_ok(c, "rs_rulers");
+}
+
+int dist_rs_walk_impl(cw_ctx *c, const uint32_t *walkers, uint64_t m, const uint32_t *rlist,
+                      uint32_t rbase, const uint32_t *word, const uint32_t *thr, uint64_t n,
+                      uint32_t base, uint32_t *own, uint32_t *links, uint32_t *nlinks,
+                      uint32_t *out, uint64_t *key, uint32_t *status) {
+  if (!m) return 0;
+  if (!walkers && !rlist) return fail(c, "rs_walk: walkers or rlist");
+  Launch L(c, "rs_walk", (double)m * (16 + 16 + 8) + (double)n * (8 + 8));
+  hipLaunchKernelGGL(k_rs_walk, DIST_GRID(m), reinterpret_cast<const uint4 *>(walkers), (uint32_t)m,
+                     rlist, rbase, reinterpret_cast<const uint2 *>(word), thr, (uint32_t)n, base,
+                     reinterpret_cast<uint2 *>(own), reinterpret_cast<uint4 *>(links), nlinks,
+                     reinterpret_cast<uint4 *>(out), key, status);
+  return dist_launch_ok(c, "rs_walk");
+}
+
+int dist_rs_top_impl(cw_ctx *c, const uint32_t *links, uint64_t m, uint64_t total, uint32_t *pos,
+                     uint32_t *status) {
+  if (!m) return 0;
+  if (m >= RS_NONE || total >= SUCCW_END) return fail(c, "rs_top: sizes");
+  uint2 *A = scratch_t<uint2>(c, "rs_a", m), *B = scratch_t<uint2>(c, "rs_b", m);
+  if (!A || !B) return fail(c, "out of device memory (rs_top, m=%llu)", (unsigned long long)m);
+  // a ruler without a link (a broken walk) points past the end with no length
+  HIPCHK(c, hipMemsetAsync(A, 0xFF, m * sizeof(uint2), c->stream));
+  uint32_t rounds = 0;
+  while ((1ull << rounds) < m) rounds++;
+  Launch L(c, "rs_top", (double)m * (16 + 8) + (double)rounds * m * (8 + 8 + 8) + (double)m * 12);
+  hipLaunchKernelGGL(k_rs_links, DIST_GRID(m), reinterpret_cast<const uint4 *>(links), (uint32_t)m,
+                     A);
+  for (uint32_t r = 0; r < rounds; r++) {
+    hipLaunchKernelGGL(k_rs_jump, DIST_GRID(m), A, (uint32_t)m, B);
+    std::swap(A, B);
+  }
+  hipLaunchKernelGGL(k_rs_base, DIST_GRID(m), A, (uint32_t)m, (uint32_t)total, pos, status);
+  return dist_launch_ok(c, "rs_top");
+}
+
+int dist_rs_pos_impl(cw_ctx *c, const uint32_t *own, const uint32_t *pbase, const uint32_t *succ,
+                     const uint32_t *val, uint64_t n, uint32_t *rec, uint64_t *key) {
+  if (!n) return 0;
+  Launch L(c, "rs_pos", (double)n * (8 + 4 + 4 + 4 + 8 + (key ? 8 : 0)));
+  hipLaunchKernelGGL(k_rs_pos, DIST_GRID(n), reinterpret_cast<const uint2 *>(own), pbase, succ, val,
+                     (uint32_t)n, reinterpret_cast<uint2 *>(rec), key);
+  return dist_launch_ok(c, "rs_pos");
+}
+
+int dist_rs_emit_impl(cw_ctx *c, const uint32_t *rec, uint64_t m, uint32_t p0, uint64_t len,
+                      uint32_t *perm, uint32_t *bits, uint32_t *count, uint32_t *status) {
+  HIPCHK(c, hipMemsetAsync(count, 0, 4, c->stream));
+  if (!len) return 0;
+  uint8_t *vis8 = scratch_t<uint8_t>(c, "rs_vis", (size_t)len + 32);
+  if (!vis8) return fail(c, "out of device memory (rs_emit)");
+  Launch L(c, "rs_emit", (double)m * (8 + 4 + 1) + (double)len * (1 + 0.125));
+  if (m) {
+    const uint32_t nb = (uint32_t)std::min<uint64_t>((m + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_rs_emit, dim3(nb), dim3(256), 0, c->stream,
+                       reinterpret_cast<const uint2 *>(rec), (uint32_t)m, p0, (uint32_t)len, perm,
+                       vis8, count, status);
+  }
+  hipLaunchKernelGGL(k_pack_bits, dim3((uint32_t)((len + 31) / 32 + 255) / 256), dim3(256), 0,
+                     c->stream, vis8, (uint32_t)len, bits);
+  return dist_launch_ok(c, "rs_emit");
 }
 
 // The walk, ranking and emit of one list given every node's successor.

@@ -34,6 +34,9 @@ import torch
 import torch.distributed as dist
 
 NOT_FOUND = 0xFFFFFFFF
+STATUS_INTERNAL = 1 << 5   # CW_STATUS_INTERNAL
+RULER_K = 16               # one ruler per ~16 nodes (DESIGN.md §6 study)
+RULER_SEED = 0x2545F491
 
 
 def _on_stream(f):
@@ -216,6 +219,54 @@ class HipOps:
                     self._p(out))
         return out
 
+    # --- the ruling-set list ranking (dist.hip) ------------------
+    @_on_stream
+    def rs_rulers(self, succ, thr, base, k, seed):
+        """(node words int32 [n, 2], ruler list int32 [n], number of rulers)."""
+        n = succ.numel()
+        word, rlist = self._e(2 * n, torch.int32).view(n, 2), self._e(n, torch.int32)
+        cnt = torch.zeros(1, dtype=torch.int32, device=self.dev)
+        self.w.dist("rs_rulers", self._p(succ), self._p(thr), n, base, k, seed, self._p(word),
+                    self._p(rlist), cnt.data_ptr())
+        return word, rlist, int(cnt.item())
+
+    @_on_stream
+    def rs_walk(self, walkers, m, rlist, rbase, word, thr, base, own, links, nlinks, status):
+        """One exchange round: (messages int32 [m, 4], their partition keys)."""
+        out, key = self._e(m * 4, torch.int32).view(m, 4), self._e(m, torch.int64)
+        self.w.dist("rs_walk", self._p(walkers), m, self._p(rlist), rbase, self._p(word),
+                    self._p(thr), word.shape[0], base, self._p(own), self._p(links),
+                    nlinks.data_ptr(), self._p(out), self._p(key), status.data_ptr())
+        return out, key
+
+    @_on_stream
+    def rs_top(self, links, total, status):
+        """Weave position of every ruler (int32 [m]) from all m links."""
+        m = links.shape[0]
+        pos = self._e(m, torch.int32)
+        self.w.dist("rs_top", self._p(links), m, total, self._p(pos), status.data_ptr())
+        return pos
+
+    @_on_stream
+    def rs_pos(self, own, pos_base, succ, val, keys=False):
+        n = succ.numel()
+        rec = self._e(2 * n, torch.int32).view(n, 2)
+        key = self._e(n, torch.int64) if keys else None
+        self.w.dist("rs_pos", self._p(own), self._p(pos_base), self._p(succ), self._p(val), n,
+                    self._p(rec), self._p(key))
+        return rec, key
+
+    @_on_stream
+    def rs_emit(self, rec, p0, length, status):
+        """(weave_perm [length], visible_bits, visible_count [1]) of positions
+        [p0, p0 + length) from the emit records."""
+        perm = self._e(length, torch.int32)
+        bits = self._e((length + 31) // 32, torch.int32)
+        cnt = self._e(1, torch.int32)
+        self.w.dist("rs_emit", self._p(rec), rec.shape[0], p0, length, self._p(perm),
+                    self._p(bits), cnt.data_ptr(), status.data_ptr())
+        return perm, bits, cnt
+
     @_on_stream
     def gather_rows(self, rec, idx):
         """rec[idx] for 16-byte rows (int32 [n, 4])."""
@@ -261,6 +312,7 @@ class GiantResult:
     n_total: int
     n_owned: int        # ids this rank owned after the sample sort
     max_ts: int
+    pos_base: int = 0   # out="sharded": weave position of this rank's weave_perm[0]
 
 
 def _a2a(t, send, recv, group):
@@ -310,22 +362,35 @@ def choose_splitters(samples, weights, W):
 
 
 def weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift=0, group=None,
-                      root=0, samples=256, tree="auto") -> GiantResult:
+                      root=0, samples=256, tree="auto", ranking="auto", out="root",
+                      ruler_k=RULER_K) -> GiantResult:
     """Weave one list whose nodes are spread over the ranks of `group`.
 
     id_key / cause_key: int64 tensors holding the packed u64 keys (< 2^63);
     kind: uint8.  Every rank calls this; rank `root` receives the weave.
     tree: "dist" builds the tree rank by rank (_tree_distributed), "root" on
     the root alone (cw_weave_ranked), "auto" = dist for W > 1.  Lists outside
-    the fast path's domain always take "root" (its exact path)."""
+    the fast path's domain always take "root" (its exact path).
+    ranking (tree "dist" only): "ruling" ranks the list where it lies
+    (_rank_ruling, a ruler every ~ruler_k nodes), "root" gathers the
+    successors on the root (cw_weave_linked); "auto" = ruling for W > 1.
+    out (ranking "ruling" only): "root" -- the whole weave on the root;
+    "sharded" -- rank j holds weave positions [pos_base, pos_base + len) (a
+    contiguous 1/W of them, 32-aligned), visible_count is the list's total."""
     if key_bits > 63:
         raise ValueError("keys must be < 2^63 (int64 order)")
     if tree not in ("auto", "dist", "root"):
         raise ValueError("tree: auto, dist or root")
+    if ranking not in ("auto", "ruling", "root"):
+        raise ValueError("ranking: auto, ruling or root")
+    if out not in ("root", "sharded"):
+        raise ValueError("out: root or sharded")
+    if ruler_k < 1:
+        raise ValueError("ruler_k >= 1")
     ctx = getattr(ops, "stream_context", contextlib.nullcontext)
     with ctx():
         return _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root,
-                                  samples, tree)
+                                  samples, tree, ranking, out, ruler_k)
 
 
 def _any(v, group, dev):
@@ -376,8 +441,104 @@ def _tree_distributed(ops, par, kind, base, owns, group, dev):
     return ops.dist_succ(kind, fcS, fcN, base), ops.dist_thr(nsc, base)
 
 
+def _bcast(t, src, group):
+    """Broadcast from group rank src (gloo works on host tensors)."""
+    if dist.get_world_size(group) == 1:
+        return t
+    g = dist.get_global_rank(group, src) if group is not None else src
+    if dist.get_backend(group) == "gloo" and t.is_cuda:
+        c = t.cpu()
+        dist.broadcast(c, g, group=group)
+        t.copy_(c)
+    else:
+        dist.broadcast(t, g, group=group)
+    return t
+
+
+def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_own, max_ts):
+    """The list ranking where the list lies (dist.hip k_rs_*):
+    rulers (global rank 0 and ~1/k of the nodes, by hash) walk their sublists
+    (cw_dist_rs_walk), a walker crossing ranks travels as a 16-byte message in
+    an all-to-all round; the links (one per ruler) are ranked on the root
+    (cw_dist_rs_top), the rulers' positions broadcast, and every node's
+    position = its ruler's + its offset (cw_dist_rs_pos).  The emit records
+    {position, origin | render} go to the root (out="root") or to the owner of
+    the position (out="sharded")."""
+    W, r = dist.get_world_size(group), dist.get_rank(group)
+    n, N = succ.numel(), sum(owns)
+    starts = [sum(owns[:j]) for j in range(1, W)] + [N]
+    split_t = torch.as_tensor(np.array(starts, np.int64), device=dev)
+    word, rlist, nr = ops.rs_rulers(succ, thr, base, k, RULER_SEED)
+    rc = [v[0] for v in _all_gather_ints([nr], group, dev)]
+    rbase, M = sum(rc[:r]), sum(rc)
+    own = ops.zeros32(2 * n)
+    links = ops.zeros32(4 * M).view(M, 4)   # any walk may end on this rank
+    nlinks, status = ops.zeros32(1), ops.zeros32(1)
+    walkers, m, rounds = None, nr, 0
+    while True:
+        msg, key = ops.rs_walk(walkers, m, rlist, rbase, word, thr, base, own, links, nlinks,
+                               status)
+        rounds += 1
+        if W == 1:
+            break
+        perm, counts = ops.partition(key, split_t)   # W + 1 buckets: the last stopped here
+        send = counts[:W]
+        mat = _all_gather_ints(send, group, dev)
+        if not any(any(row) for row in mat):
+            break
+        if rounds > 2 * N + 4:
+            raise RuntimeError("ruling set: the walks did not end")
+        recv = [mat[j][r] for j in range(W)]
+        idx = perm[:sum(send)]
+        walkers = _a2a(ops.gather_rows(msg, idx).reshape(-1), [4 * x for x in send],
+                       [4 * x for x in recv], group).view(-1, 4)
+        m = walkers.shape[0]
+    del word, rlist, walkers
+    nl = int(nlinks[0])
+    agg = _all_gather_ints([nl, int(status[0])], group, dev)
+    bad = sum(v[0] for v in agg) != M or any(v[1] for v in agg)
+    gsend = [4 * nl if j == root else 0 for j in range(W)]
+    grecv = [4 * agg[j][0] if r == root else 0 for j in range(W)]
+    all_links = _a2a(links[:nl].reshape(-1), gsend, grecv, group)
+    del links
+    pos_base = ops.zeros32(M)
+    tstat = ops.zeros32(1)
+    if r == root and not bad:
+        pos_base = ops.rs_top(all_links.view(-1, 4), N, tstat)
+    del all_links
+    _bcast(pos_base, root, group)
+    rec, key = ops.rs_pos(own, pos_base, succ, org, keys=(out == "sharded"))
+    del own, pos_base
+    estat = ops.zeros32(1)
+    if out == "root":
+        gsend = [2 * n if j == root else 0 for j in range(W)]
+        grecv = [2 * owns[j] if r == root else 0 for j in range(W)]
+        allrec = _a2a(rec.reshape(-1), gsend, grecv, group).view(-1, 2)
+        if r != root:
+            return GiantResult(None, None, None, None, N, n_own, max_ts)
+        wp, bits, cnt = ops.rs_emit(allrec, 0, N, estat)
+        st = int(tstat[0]) | int(estat[0]) | (STATUS_INTERNAL if bad else 0)
+        return GiantResult(wp, bits, int(cnt[0]), st, N, n_own, max_ts)
+    # sharded: rank j owns positions [j * chunk, (j + 1) * chunk)
+    chunk = ((N + W - 1) // W + 31) // 32 * 32
+    ps = torch.as_tensor(np.array([min(j * chunk, N) for j in range(1, W)] + [N], np.int64),
+                         device=dev)
+    perm, counts = ops.partition(key, ps)
+    send = counts[:W]
+    recv = _exchange_counts(send, group, dev)
+    rows = ops.gather(rec.reshape(-1).view(torch.int64), perm[:sum(send)])
+    mine = _a2a(rows, send, recv, group).view(torch.int32).view(-1, 2)
+    p0 = min(r * chunk, N)
+    wp, bits, cnt = ops.rs_emit(mine, p0, min(p0 + chunk, N) - p0, estat)
+    tot = _all_gather_ints([int(cnt[0]), int(tstat[0]) | int(estat[0])], group, dev)
+    st = (STATUS_INTERNAL if bad else 0)
+    for v in tot:
+        st |= v[1]
+    return GiantResult(wp, bits, sum(v[0] for v in tot), st, N, n_own, max_ts, pos_base=p0)
+
+
 def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples,
-                       tree="auto"):
+                       tree="auto", ranking="auto", out="root", ruler_k=RULER_K):
     W, r = dist.get_world_size(group), dist.get_rank(group)
     dev = id_key.device
     n = id_key.numel()
@@ -451,6 +612,9 @@ def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, 
             st |= v[0]
         if not st and not dups:
             succ, thr = _tree_distributed(ops, par, okd, own_base, owns, group, dev)
+            if ranking == "ruling" or (ranking == "auto" and W > 1):
+                return _rank_ruling(ops, succ, thr, oorg, own_base, owns, group, dev, root, out,
+                                    ruler_k, n_own, max_ts)
             gsend = [n_own if j == root else 0 for j in range(W)]
             grecv = [owns[j] if r == root else 0 for j in range(W)]
             g_succ = _a2a(succ, gsend, grecv, group)

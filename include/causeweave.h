@@ -422,6 +422,49 @@ int cw_dist_thr(cw_ctx *ctx, const uint32_t *nsc, uint64_t n, uint32_t base, uin
 int cw_dist_succ(cw_ctx *ctx, const uint8_t *kind, const uint32_t *fcS, const uint32_t *fcN,
                  uint64_t n, uint32_t base, uint32_t *out);
 
+/* Ruling-set list ranking of the distributed list: the list
+ * is ranked where it lies instead of on one GPU.  Rulers: global rank 0 and
+ * every rank g with mix32(seed, g) * k < 2^32; each walks its sublist.
+ * Replaces the rank-0 walk of cw_weave_linked for W > 1 (cause_amd/giant.py).
+ *
+ * cw_dist_rs_rulers: word[2i..2i+1] = {next, ruler index} of base + i (next =
+ * successor, resolved thread, CW_RS_CHASE | the ancestor whose thread it is,
+ * or 0x7FFFFFFF at the end; ruler index among this run's rulers, or
+ * CW_RS_NONE); rlist[j] = local index of ruler j; *count (device) = rulers.
+ * cw_dist_rs_walk: one exchange round.  walkers: m records {ruler, count,
+ * target, 0} received from other ranks, or NULL for the run's own rulers
+ * (ruler index rbase + j, j < m).  Each walker numbers the nodes it visits
+ * (own[2x..2x+1] = {ruler, offset}) until its list reaches another ruler or
+ * the end (a record {ruler, next ruler or CW_RS_NONE, length, 0} appended at
+ * links[4 * (*nlinks)]) or leaves the run: out[4i..] = {ruler, count, target,
+ * 0}, key[i] = the target's global rank (UINT64_MAX for a walker that
+ * stopped), for cw_partition_keys by owner.  status |= CW_STATUS_INTERNAL on
+ * a walk past its step bound.
+ * cw_dist_rs_top (one GPU, all m = number of rulers links): pos[r] = weave
+ * position of ruler r; status |= CW_STATUS_INTERNAL unless the links form
+ * one list from ruler 0 over `total` nodes.
+ * cw_dist_rs_pos: rec[2i..] = {position, val[i] | render bit << 31} of base
+ * + i; key[i] = the position (key may be NULL).
+ * cw_dist_rs_emit: at the owner of positions [p0, p0 + len): weave_perm,
+ * visible_bits (from position p0, a multiple of 32) and *visible_count from m
+ * records. */
+#define CW_RS_CHASE 0x80000000u
+#define CW_RS_NONE 0xFFFFFFFFu
+int cw_dist_rs_rulers(cw_ctx *ctx, const uint32_t *succ, const uint32_t *thr, uint64_t n,
+                      uint32_t base, uint32_t k, uint32_t seed, uint32_t *word, uint32_t *rlist,
+                      uint32_t *count);
+int cw_dist_rs_walk(cw_ctx *ctx, const uint32_t *walkers, uint64_t m, const uint32_t *rlist,
+                    uint32_t rbase, const uint32_t *word, const uint32_t *thr, uint64_t n,
+                    uint32_t base, uint32_t *own, uint32_t *links, uint32_t *nlinks, uint32_t *out,
+                    uint64_t *key, uint32_t *status);
+int cw_dist_rs_top(cw_ctx *ctx, const uint32_t *links, uint64_t m, uint64_t total, uint32_t *pos,
+                   uint32_t *status);
+int cw_dist_rs_pos(cw_ctx *ctx, const uint32_t *own, const uint32_t *pos_base, const uint32_t *succ,
+                   const uint32_t *val, uint64_t n, uint32_t *rec, uint64_t *key);
+int cw_dist_rs_emit(cw_ctx *ctx, const uint32_t *rec, uint64_t m, uint32_t p0, uint64_t len,
+                    uint32_t *weave_perm, uint32_t *visible_bits, uint32_t *visible_count,
+                    uint32_t *status);
+
 /* One list given every node's successor word (cw_dist_succ) and thread word
  * (cw_dist_thr), in rank order; the walk chases pending threads.  val as
  * cw_ranked_list. */

@@ -238,6 +238,121 @@ class CpuOps:
             out[i] = succ | (0x80000000 if vis else 0)
         return self._t32(out)
 
+    # --- the ruling-set ranking (numpy restatement of dist.hip k_rs_*) ---------
+    CHASE = 0x80000000
+    RS_NONE = 0xFFFFFFFF
+
+    @staticmethod
+    def _mix32(a, b):
+        m = np.uint64(0xFFFFFFFF)
+        h = (np.uint64(a) * np.uint64(0x9E3779B1) + np.asarray(b, np.uint64)) & m
+        h ^= h >> np.uint64(16)
+        h = (h * np.uint64(0x85EBCA6B)) & m
+        h ^= h >> np.uint64(13)
+        h = (h * np.uint64(0xC2B2AE35)) & m
+        h ^= h >> np.uint64(16)
+        return h
+
+    def _ruler(self, g, k, seed):
+        g = np.asarray(g, np.uint64)
+        return (g == 0) | (self._mix32(seed, g) * np.uint64(k) < np.uint64(1 << 32))
+
+    def rs_rulers(self, succ, thr, base, k, seed):
+        s, t = self._u32(succ), self._u32(thr)
+        n = len(s)
+        nx = s & np.uint32(0x7FFFFFFF)
+        ft = nx == 0x7FFFFFFE
+        tv = np.where(t & self.PEND, self.CHASE | (t & np.uint32(0x7FFFFFFF)), t)
+        nx = np.where(ft, tv, nx).astype(np.uint32)
+        f = self._ruler(base + np.arange(n, dtype=np.uint64), k, seed)
+        ridx = np.full(n, self.RS_NONE, np.uint32)
+        ridx[f] = np.arange(int(f.sum()), dtype=np.uint32)
+        word = np.stack([nx, ridx], 1)
+        rlist = np.zeros(n, np.uint32)
+        rlist[:int(f.sum())] = np.flatnonzero(f)
+        return self._t32(word), self._t32(rlist), int(f.sum())
+
+    def rs_walk(self, walkers, m, rlist, rbase, word, thr, base, own, links, nlinks, status):
+        wd = word.numpy().view(np.uint32)
+        th, rl = self._u32(thr), self._u32(rlist)
+        ow, lk = own.numpy().view(np.uint32), links.numpy().view(np.uint32)
+        nl = nlinks.numpy().view(np.uint32)
+        n = wd.shape[0]
+        out = np.zeros((m, 4), np.uint32)
+        key = np.full(m, 2**64 - 1, np.uint64)
+        wk = walkers.numpy().view(np.uint32) if walkers is not None else None
+        for i in range(m):
+            if wk is not None:
+                R, cnt, tgt = int(wk[i, 0]), int(wk[i, 1]), int(wk[i, 2])
+            else:
+                R, cnt, tgt = rbase + i, 0, base + int(rl[i])
+            link, lnext = False, self.RS_NONE
+            while True:
+                a = tgt & 0x7FFFFFFF
+                if not base <= a < base + n:
+                    key[i] = a
+                    break
+                if tgt & self.CHASE:
+                    t = int(th[a - base])
+                    nx = self.CHASE | (t & 0x7FFFFFFF) if t & self.PEND else t
+                else:
+                    x, r = int(wd[a - base, 0]), int(wd[a - base, 1])
+                    if r != self.RS_NONE and cnt > 0:
+                        link, lnext = True, rbase + r
+                        break
+                    ow[2 * (a - base)], ow[2 * (a - base) + 1] = R, cnt
+                    cnt += 1
+                    nx = x
+                if nx == self.END:
+                    link = True
+                    break
+                tgt = nx
+            out[i] = (R, cnt, tgt, 0)
+            if link:
+                lk[int(nl[0])] = (R, lnext, cnt, 0)
+                nl[0] += 1
+        return self._t32(out), torch.from_numpy(key.view(np.int64))
+
+    def rs_top(self, links, total, status):
+        lk = links.numpy().view(np.uint32)
+        m = lk.shape[0]
+        nxt = np.full(m, self.RS_NONE, np.int64)
+        ln = np.zeros(m, np.int64)
+        nxt[lk[:, 0]] = lk[:, 1]
+        ln[lk[:, 0]] = lk[:, 2]
+        pos = np.zeros(m, np.uint32)
+        r, p, seen = 0, 0, 0
+        while r != self.RS_NONE and seen <= m:
+            pos[r] = p
+            p += int(ln[r])
+            r = int(nxt[r])
+            seen += 1
+        if p != total or seen != m:
+            status.numpy()[0] |= 32
+        return self._t32(pos)
+
+    def rs_pos(self, own, pos_base, succ, val, keys=False):
+        ow = own.numpy().view(np.uint32).reshape(-1, 2)
+        pb, s, v = self._u32(pos_base), self._u32(succ), self._u32(val)
+        p = pb[ow[:, 0]].astype(np.uint64) + ow[:, 1] if len(ow) else np.zeros(0, np.uint64)
+        rec = np.stack([p.astype(np.uint32), (v & np.uint32(0x7FFFFFFF)) | (s & np.uint32(0x80000000))], 1)
+        return self._t32(rec.reshape(-1, 2)), (torch.from_numpy(p.astype(np.int64)) if keys else None)
+
+    def rs_emit(self, rec, p0, length, status):
+        r = rec.numpy().view(np.uint32).reshape(-1, 2)
+        perm = np.zeros(length, np.uint32)
+        vis = np.zeros(length, np.uint8)
+        p = r[:, 0].astype(np.int64) - p0
+        if ((p < 0) | (p >= length)).any():
+            status.numpy()[0] |= 32
+        ok = (p >= 0) & (p < length)
+        perm[p[ok]] = r[ok, 1] & 0x7FFFFFFF
+        vis[p[ok]] = r[ok, 1] >> 31
+        bits = np.packbits(vis, bitorder="little")
+        bits = np.pad(bits, (0, (-len(bits)) % 4)).view(np.int32)
+        return (self._t32(perm), torch.from_numpy(bits.copy()),
+                torch.tensor([int(vis.sum())], dtype=torch.int32))
+
     def gather_rows(self, rec, idx):
         return rec[idx.long()]
 

@@ -11,7 +11,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def main(outdir):
+def main(outdir, ranking="auto", out="root"):
     import torch
     import torch.distributed as dist
 
@@ -30,8 +30,27 @@ def main(outdir):
         with abi.Weaver(0) as w:
             ops = giant.HipOps(w, "cuda:0")
             res = giant.weave_distributed(ops, t(idk[sh].view(np.int64)), t(ck[sh].view(np.int64)),
-                                          t(kd[sh]), lay.key_bits, ts_shift=lay.ts_shift)
+                                          t(kd[sh]), lay.key_bits, ts_shift=lay.ts_shift,
+                                          ranking=ranking, out=out)
             torch.cuda.synchronize()
+        if out == "sharded":
+            # the slices meet on rank 0 (gloo: host tensors)
+            parts = [None] * world
+            dist.all_gather_object(parts, (res.pos_base, res.weave_perm.cpu().numpy(),
+                                           res.visible_bits.cpu().numpy(), res.status))
+            if rank == 0:
+                perm, vis, st = oracle.batch_lists(np.array([0, len(idk)], np.uint64), idk, ck, kd,
+                                                   method=oracle.METHOD_EFF)
+                allsh = np.concatenate(shares(len(idk), world, 31))
+                parts.sort(key=lambda p: p[0])
+                wp = np.concatenate([p[1] for p in parts]).view(np.uint32)
+                bits = np.concatenate([np.unpackbits(p[2].view(np.uint8), bitorder="little")[:len(p[1])]
+                                       for p in parts])
+                ok = (all(p[3] == 0 for p in parts) and bool(np.array_equal(allsh[wp], perm))
+                      and bool(np.array_equal(bits, vis)) and res.visible_count == int(vis.sum()))
+                json.dump({"ok": ok, "status": [p[3] for p in parts], "n": res.n_total},
+                          open(os.path.join(outdir, "rank0.json"), "w"))
+            return
         if rank == 0:
             perm, vis, st = oracle.batch_lists(np.array([0, len(idk)], np.uint64), idk, ck, kd,
                                                method=oracle.METHOD_EFF)
@@ -46,4 +65,4 @@ def main(outdir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(*sys.argv[1:])

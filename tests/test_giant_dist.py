@@ -40,7 +40,7 @@ def shares(N, W, seed, empty_rank=None):
     return [rng.permutation(np.flatnonzero(owner == r)) for r in range(W)]
 
 
-def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q):
+def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q, opts=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,8 +53,13 @@ def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q):
         lay = spec.layout()
         res = giant.weave_distributed(CpuOps(), t(idk[sh]), t(ck[sh]),
                                       torch.from_numpy(kd[sh].copy()), lay.key_bits,
-                                      ts_shift=lay.ts_shift, samples=samples, tree=tree)
-        if rank == 0:
+                                      ts_shift=lay.ts_shift, samples=samples, tree=tree,
+                                      **(opts or {}))
+        if (opts or {}).get("out") == "sharded":
+            q.put(("part", rank, res.pos_base, res.weave_perm.numpy().copy(),
+                   res.visible_bits.numpy().copy(), res.visible_count, res.status, res.n_total,
+                   res.max_ts))
+        elif rank == 0:
             q.put((res.weave_perm.numpy().copy(), res.visible_count, res.status, res.n_total,
                    res.max_ts))
         q.put(("own", rank, res.n_owned))
@@ -62,21 +67,41 @@ def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q):
         dist.destroy_process_group()
 
 
-def run(world, n, seed, samples=64, empty_rank=None, tree="auto"):
+def run(world, n, seed, samples=64, empty_rank=None, tree="auto", **opts):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, n, seed, samples, empty_rank, tree, q))
+    ps = [ctx.Process(target=_worker,
+                      args=(r, world, port, n, seed, samples, empty_rank, tree, q, opts))
           for r in range(world)]
     for p in ps:
         p.start()
-    got, owned = None, {}
-    for _ in range(world + 1):
+    sharded = opts.get("out") == "sharded"
+    got, owned, parts = None, {}, []
+    for _ in range(2 * world if sharded else world + 1):
         m = q.get(timeout=120)
-        if isinstance(m[0], str):
+        if isinstance(m[0], str) and m[0] == "part":
+            parts.append(m)
+        elif isinstance(m[0], str):
             owned[m[1]] = m[2]
         else:
             got = m
+    if sharded:
+        # the slices in position order: weave_perm and render bits of the whole list
+        parts.sort(key=lambda m: m[2])
+        N = parts[0][7]
+        pos = 0
+        for m in parts:
+            assert m[2] == pos and (m[2] % 32 == 0)
+            pos += len(m[3])
+        assert pos == N and len({m[5] for m in parts}) == 1
+        st = 0
+        for m in parts:
+            st |= m[6]
+        wp = np.concatenate([m[3] for m in parts])
+        bits = np.concatenate([np.unpackbits(m[4].view(np.uint8), bitorder="little")[:len(m[3])]
+                               for m in parts])
+        got = (wp, parts[0][5], st, N, parts[0][8], bits)
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
@@ -102,6 +127,30 @@ def test_distributed_weave_matches_oracle(world, n, seed, empty, tree):
     assert max_ts == int(idk.max()) >> spec.layout().ts_shift
     # the sample sort balances the owners
     assert max(owned.values()) < 2.0 * N / world
+
+
+@pytest.mark.parametrize("world,n,seed,empty,k,out", [
+    (1, 3000, 21, None, 16, "root"), (2, 4000, 22, None, 16, "root"),
+    (3, 5000, 23, None, 4, "sharded"), (4, 3000, 24, 1, 16, "sharded"),
+    (2, 2500, 25, None, 1, "root"), (2, 2500, 26, None, 1000, "sharded")])
+def test_ruling_set_ranking_matches_oracle(world, n, seed, empty, k, out):
+    """The list ranked where it lies (giant._rank_ruling, dist.hip k_rs_*'s numpy
+    double): rulers every ~k nodes walk their sublists, walkers crossing ranks
+    travel as all-to-all messages, the ruler links are ranked on rank 0, and the
+    weave lands on rank 0 or spread by position.  k = 1 (every node a ruler)
+    and k = 1000 (a few long walks) bound the density."""
+    got, owned = run(world, n, seed, empty_rank=empty, tree="dist", ranking="ruling",
+                     out=out, ruler_k=k)
+    wp, vcount, status, N = got[:4]
+    spec, idk, ck, kd = make_list(n, seed)
+    perm, vis, st = oracle.batch_lists(np.array([0, N], np.uint64), idk, ck, kd,
+                                       method=oracle.METHOD_EFF)
+    sh = np.concatenate(shares(N, world, seed, empty))
+    assert status == 0 and not st.any()
+    assert np.array_equal(sh[wp.view(np.uint32)], perm)
+    assert vcount == int(vis.sum())
+    if out == "sharded":
+        assert np.array_equal(got[5], vis)
 
 
 def _dup_worker(rank, world, port, q):

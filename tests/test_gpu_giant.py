@@ -263,8 +263,83 @@ def test_weave_linked_equals_weave_ranked(ops, n, seed):
     assert _same(got["visible_bits"][:nb], want["visible_bits"][:nb])
 
 
-@pytest.mark.parametrize("tree", ["root", "dist"])
-def test_distributed_one_rank_in_process(ops, tree):
+def _one_rank_tree(ops, par, kd):
+    """(succ, thr) of the one-rank distributed tree on the GPU."""
+    n = len(par)
+    eff = ops.dist_eff(_t(par), _t(kd), 0)
+    sk, si = ops.sort_keys32(ops.dist_gkey(eff, _t(kd)), 32)
+    nsc, okey, rec = ops.dist_runs(sk, si, 0, _t(kd))
+    heads = okey.cpu().numpy() != -1
+    rs = _t(rec.cpu().numpy()[heads])
+    rk, ri = ops.sort_keys32(ops.dist_rkey(rs), 32)
+    fs, fn = ops.zeros32(n), ops.zeros32(n)
+    reply = ops.dist_link(rk, ri, rs, 0, n, fs, fn)
+    ops.dist_put(rs, reply, 0, nsc)
+    return ops.dist_succ(_t(kd), fs, fn, 0), ops.dist_thr(nsc, 0)
+
+
+def _rows_sorted(t):
+    a = t.cpu().numpy().view(np.uint32)
+    return a[np.lexsort(a.T[::-1])] if len(a) else a
+
+
+@pytest.mark.parametrize("n,seed,k,lo,hi", [(20_000, 3, 16, 0, None), (20_000, 5, 4, 7_000, 15_000),
+                                            (300_000, 4, 16, 100_000, 250_000),
+                                            (50, 2, 1, 0, None), (5_000, 6, 5000, 1_000, 4_000)])
+def test_ruling_set_ops_match_the_double(ops, n, seed, k, lo, hi):
+    """The ruling-set kernels (dist.hip k_rs_*) against their numpy restatement
+    (tests/giant_cpu_ops.py) on a whole list and on one rank's run of it: node
+    words, ruler list, one walk round (every node's {ruler, offset}, the links
+    and the messages of walkers leaving the run), the ruler ranking, positions
+    and the emit -- which must be cw_weave_linked's weave."""
+    import torch
+
+    cpu = CpuOps()
+    T = torch.from_numpy
+    par, kd, val = ranked_case(n, seed)
+    N = len(par)
+    hi = N if hi is None else hi
+    succ, thr = _one_rank_tree(ops, par, kd)
+    cs, ct = succ.cpu(), thr.cpu()
+    seed32 = giant.RULER_SEED
+    # one run [lo, hi) of the list (base lo); the rest of the list is "remote"
+    word, rlist, nr = ops.rs_rulers(_t(cs.numpy()[lo:hi]), _t(ct.numpy()[lo:hi]), lo, k, seed32)
+    cw, crl, cnr = cpu.rs_rulers(cs[lo:hi], ct[lo:hi], lo, k, seed32)
+    assert nr == cnr and _same(word, cw) and _same(rlist.cpu()[:nr], crl[:nr])
+    m = hi - lo
+    own, links = ops.zeros32(2 * m), ops.zeros32(4 * max(nr, 1)).view(-1, 4)
+    nl, st = ops.zeros32(1), ops.zeros32(1)
+    out, key = ops.rs_walk(None, nr, rlist, 7, word, _t(ct.numpy()[lo:hi]), lo, own, links, nl, st)
+    cown, clinks = cpu.zeros32(2 * m), cpu.zeros32(4 * max(cnr, 1)).view(-1, 4)
+    cnl, cst = cpu.zeros32(1), cpu.zeros32(1)
+    cout, ckey = cpu.rs_walk(None, cnr, crl, 7, cw, ct[lo:hi], lo, cown, clinks, cnl, cst)
+    assert int(st[0]) == 0 == int(cst[0]) and int(nl[0]) == int(cnl[0])
+    assert _same(own, cown) and _same(key, ckey)
+    moved = ckey.numpy() != -1
+    assert _same(out.cpu()[torch.from_numpy(moved)], cout[torch.from_numpy(moved)])
+    assert np.array_equal(_rows_sorted(links[:int(nl[0])]), _rows_sorted(clinks[:int(cnl[0])]))
+    if lo or hi != N:
+        return
+    # the whole list: one round ranks it
+    assert not moved.any() and int(nl[0]) == nr
+    pb = ops.rs_top(links[:nr], N, st)
+    cpb = cpu.rs_top(clinks[:nr], N, cst)
+    assert int(st[0]) == 0 == int(cst[0]) and _same(pb, cpb)
+    rec, pk = ops.rs_pos(own, pb, succ, _t(val), keys=True)
+    crec, cpk = cpu.rs_pos(cown, cpb, cs, T(val), keys=True)
+    assert _same(rec, crec) and _same(pk, cpk)
+    wp, bits, cnt = ops.rs_emit(rec, 0, N, st)
+    want = ops.weave_linked(succ, thr, _t(val))
+    assert int(st[0]) == 0
+    assert _same(wp, want["weave_perm"]) and int(cnt[0]) == int(want["visible_count"][0])
+    nb = (N + 31) // 32
+    assert _same(bits[:nb], want["visible_bits"][:nb])
+
+
+@pytest.mark.parametrize("tree,ranking,out", [("root", "auto", "root"), ("dist", "root", "root"),
+                                              ("dist", "ruling", "root"),
+                                              ("dist", "ruling", "sharded")])
+def test_distributed_one_rank_in_process(ops, tree, ranking, out):
     import torch
     import torch.distributed as dist
 
@@ -278,7 +353,8 @@ def test_distributed_one_rank_in_process(ops, tree):
     try:
         lay = spec.layout()
         res = giant.weave_distributed(ops, _t(_i64(idk[sh])), _t(_i64(ck[sh])), _t(kd[sh]),
-                                      lay.key_bits, ts_shift=lay.ts_shift, tree=tree)
+                                      lay.key_bits, ts_shift=lay.ts_shift, tree=tree,
+                                      ranking=ranking, out=out)
     finally:
         dist.destroy_process_group()
     perm, vis, st = oracle.batch_lists(np.array([0, len(idk)], np.uint64), idk, ck, kd,
@@ -288,17 +364,20 @@ def test_distributed_one_rank_in_process(ops, tree):
     assert res.visible_count == int(vis.sum())
 
 
-def test_distributed_two_ranks_share_the_gpu(tmp_path):
+@pytest.mark.parametrize("ranking,out", [("auto", "root"), ("root", "root"), ("ruling", "sharded")])
+def test_distributed_two_ranks_share_the_gpu(tmp_path, ranking, out):
     """Two worker processes on cuda:0 (gloo: the exchange is staged on the host;
-    with the nccl backend on distinct GPUs it runs over RCCL)."""
+    with the nccl backend on distinct GPUs it runs over RCCL).  ranking auto =
+    the ruling set at W = 2; "root" = the successors gathered on rank 0;
+    out="sharded": each rank holds its 1/W of the weave positions."""
     port = _free_port()
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
     procs = []
     for r in range(2):
         e = dict(env, RANK=str(r))
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(ROOT, "tests", "giant_worker.py"),
-                                       str(tmp_path)], env=e, cwd=ROOT))
+                                       str(tmp_path), ranking, out], env=e, cwd=ROOT))
     for p in procs:
         assert p.wait(timeout=300) == 0
-    out = json.load(open(tmp_path / "rank0.json"))
-    assert out["ok"], out
+    res = json.load(open(tmp_path / "rank0.json"))
+    assert res["ok"], res
