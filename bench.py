@@ -421,7 +421,7 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
             "kernels_ms_per_step_rank0": {k: round(v[1] / a.steps, 4) for k, v in
                                           sorted(stats.items(), key=lambda kv: -kv[1][1])},
             "kernel_sum_ms_per_step_rank0": sum(v[1] for v in stats.values()) / a.steps,
-            "nodes_owned_rank0": res.n_owned, "gen_s": t_gen,
+            "nodes_owned_rank0": res.n_owned, "gen_s": t_gen, "ruling_set": res.ranking,
         }
         print(json.dumps(line), flush=True)
     w.close()

@@ -445,6 +445,91 @@ __global__ __launch_bounds__(256) void k_rs_jump(const uint2 *__restrict__ A, ui
   }
 }
 
+// Large ruler lists rank in two levels: sub-rulers (ruler 0 and ~1/16 of the
+// rest, by hash) walk their stretch of the ruler list summing lengths, the
+// sub-ruler list is pointer-jumped, and each ruler's position is its
+// sub-ruler's plus its offset.  R4[r] = {next, length, sub-ruler index or
+// RS_NONE, 0}.
+constexpr uint32_t RS_TOP_DIRECT = 1u << 21;  // rulers ranked by pointer jumping alone
+constexpr uint32_t RS_SUB_K = 16;
+constexpr uint32_t RS_SUB_SEED = 0x68E31DA4u;
+
+__global__ __launch_bounds__(256) void k_rs_links4(const uint4 *__restrict__ links, uint32_t m,
+                                                   uint4 *__restrict__ R4) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  const uint4 l = links[j];
+  if (l.x < m) R4[l.x] = make_uint4(l.y, l.z, 0u, 0u);
+}
+
+__global__ __launch_bounds__(1024) void k_rs_tflag(uint32_t m, uint4 *__restrict__ R4,
+                                                   uint32_t *__restrict__ sums) {
+  __shared__ uint32_t wtot[16];
+  const uint32_t r = blockIdx.x * 1024 + threadIdx.x;
+  const uint32_t f = r < m && rs_is_ruler(r, RS_SUB_K, RS_SUB_SEED) ? 1u : 0u;
+  uint32_t tot;
+  const uint32_t ex = block_exscan<1024>(f, wtot, &tot);
+  if (r < m) R4[r].z = ex;
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(1024) void k_rs_tindex(uint32_t m, const uint32_t *__restrict__ sums,
+                                                    uint4 *__restrict__ R4,
+                                                    uint32_t *__restrict__ slist) {
+  const uint32_t r = blockIdx.x * 1024 + threadIdx.x;
+  if (r >= m) return;
+  uint32_t s = RS_NONE;
+  if (rs_is_ruler(r, RS_SUB_K, RS_SUB_SEED)) {
+    s = R4[r].z + sums[blockIdx.x];
+    slist[s] = r;
+  }
+  R4[r].z = s;
+}
+
+// Sub-ruler j walks the ruler list to the next sub-ruler: own2[r] = {j,
+// nodes before r in the stretch}; A2[j] = {next sub-ruler, nodes}.
+__global__ __launch_bounds__(256) void k_rs_twalk(const uint32_t *__restrict__ slist, uint32_t m2,
+                                                  const uint4 *__restrict__ R4, uint32_t m,
+                                                  uint2 *__restrict__ own2,
+                                                  uint2 *__restrict__ A2,
+                                                  uint32_t *__restrict__ status) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= m2) return;
+  uint32_t r = slist[j], sum = 0, nx2 = RS_NONE;
+  for (uint32_t hop = 0;; hop++) {
+    const uint4 v = R4[r];
+    if (hop > 0 && v.z != RS_NONE) {
+      nx2 = v.z;
+      break;
+    }
+    if (hop > m) {
+      atomicOr(status, CW_STATUS_INTERNAL);
+      break;
+    }
+    own2[r] = make_uint2(j, sum);
+    sum += v.y;
+    if (v.x >= m) break;
+    r = v.x;
+  }
+  A2[j] = make_uint2(nx2, sum);
+}
+
+__global__ __launch_bounds__(256) void k_rs_tpos(const uint2 *__restrict__ own2, uint32_t m,
+                                                 const uint2 *__restrict__ A2, uint32_t m2,
+                                                 uint32_t total, uint32_t *__restrict__ pos,
+                                                 uint32_t *__restrict__ status) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  const uint2 o = own2[r];
+  if (o.x >= m2) {  // a ruler no sub-ruler reached (a broken list)
+    pos[r] = 0;
+    atomicOr(status, CW_STATUS_INTERNAL);
+    return;
+  }
+  pos[r] = total - A2[o.x].y + o.y;
+  if (r == 0 && (A2[0].y != total || A2[0].x != RS_NONE)) atomicOr(status, CW_STATUS_INTERNAL);
+}
+
 __global__ __launch_bounds__(256) void k_rs_base(const uint2 *__restrict__ A, uint32_t m,
                                                  uint32_t total, uint32_t *__restrict__ pos,
                                                  uint32_t *__restrict__ status) {
@@ -632,20 +717,54 @@ int dist_rs_top_impl(cw_ctx *c, const uint32_t *links, uint64_t m, uint64_t tota
                      uint32_t *status) {
   if (!m) return 0;
   if (m >= RS_NONE || total >= SUCCW_END) return fail(c, "rs_top: sizes");
-  uint2 *A = scratch_t<uint2>(c, "rs_a", m), *B = scratch_t<uint2>(c, "rs_b", m);
-  if (!A || !B) return fail(c, "out of device memory (rs_top, m=%llu)", (unsigned long long)m);
-  // a ruler without a link (a broken walk) points past the end with no length
-  HIPCHK(c, hipMemsetAsync(A, 0xFF, m * sizeof(uint2), c->stream));
+  if (m <= RS_TOP_DIRECT) {
+    uint2 *A = scratch_t<uint2>(c, "rs_a", m), *B = scratch_t<uint2>(c, "rs_b", m);
+    if (!A || !B) return fail(c, "out of device memory (rs_top, m=%llu)", (unsigned long long)m);
+    // a ruler without a link (a broken walk) points past the end with no length
+    HIPCHK(c, hipMemsetAsync(A, 0xFF, m * sizeof(uint2), c->stream));
+    uint32_t rounds = 0;
+    while ((1ull << rounds) < m) rounds++;
+    Launch L(c, "rs_top", (double)m * (16 + 8) + (double)rounds * m * (8 + 8 + 8) + (double)m * 12);
+    hipLaunchKernelGGL(k_rs_links, DIST_GRID(m), reinterpret_cast<const uint4 *>(links),
+                       (uint32_t)m, A);
+    for (uint32_t r = 0; r < rounds; r++) {
+      hipLaunchKernelGGL(k_rs_jump, DIST_GRID(m), A, (uint32_t)m, B);
+      std::swap(A, B);
+    }
+    hipLaunchKernelGGL(k_rs_base, DIST_GRID(m), A, (uint32_t)m, (uint32_t)total, pos, status);
+    return dist_launch_ok(c, "rs_top");
+  }
+  // two levels: sub-rulers walk the ruler list, the sub-ruler list is jumped
+  const uint32_t nb = (uint32_t)((m + 1023) / 1024);
+  uint4 *R4 = scratch_t<uint4>(c, "rs_r4", m);
+  uint2 *own2 = scratch_t<uint2>(c, "rs_own2", m);
+  uint32_t *sums = scratch_t<uint32_t>(c, "rs_sums", (size_t)nb + 1);
+  uint32_t *slist = scratch_t<uint32_t>(c, "rs_slist", m);
+  if (!R4 || !own2 || !sums || !slist)
+    return fail(c, "out of device memory (rs_top, m=%llu)", (unsigned long long)m);
+  HIPCHK(c, hipMemsetAsync(R4, 0xFF, m * sizeof(uint4), c->stream));
+  HIPCHK(c, hipMemsetAsync(own2, 0xFF, m * sizeof(uint2), c->stream));
+  hipLaunchKernelGGL(k_rs_links4, DIST_GRID(m), reinterpret_cast<const uint4 *>(links),
+                     (uint32_t)m, R4);
+  hipLaunchKernelGGL(k_rs_tflag, dim3(nb), dim3(1024), 0, c->stream, (uint32_t)m, R4, sums);
+  hipLaunchKernelGGL(k_scan_sums, dim3(1), dim3(1024), 0, c->stream, sums, nb, sums + nb);
+  hipLaunchKernelGGL(k_rs_tindex, dim3(nb), dim3(1024), 0, c->stream, (uint32_t)m, sums, R4, slist);
+  uint32_t m2 = 0;
+  HIPCHK(c, hipMemcpyAsync(&m2, sums + nb, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m2 == 0 || m2 > m) return fail(c, "rs_top: %u sub-rulers", m2);
+  uint2 *A = scratch_t<uint2>(c, "rs_a", m2), *B = scratch_t<uint2>(c, "rs_b", m2);
+  if (!A || !B) return fail(c, "out of device memory (rs_top, m2=%u)", m2);
   uint32_t rounds = 0;
-  while ((1ull << rounds) < m) rounds++;
-  Launch L(c, "rs_top", (double)m * (16 + 8) + (double)rounds * m * (8 + 8 + 8) + (double)m * 12);
-  hipLaunchKernelGGL(k_rs_links, DIST_GRID(m), reinterpret_cast<const uint4 *>(links), (uint32_t)m,
-                     A);
+  while ((1ull << rounds) < m2) rounds++;
+  Launch L(c, "rs_top", (double)m * (16 + 16 + 16 + 8 + 8 + 12) + (double)rounds * m2 * 24);
+  hipLaunchKernelGGL(k_rs_twalk, DIST_GRID(m2), slist, m2, R4, (uint32_t)m, own2, A, status);
   for (uint32_t r = 0; r < rounds; r++) {
-    hipLaunchKernelGGL(k_rs_jump, DIST_GRID(m), A, (uint32_t)m, B);
+    hipLaunchKernelGGL(k_rs_jump, DIST_GRID(m2), A, m2, B);
     std::swap(A, B);
   }
-  hipLaunchKernelGGL(k_rs_base, DIST_GRID(m), A, (uint32_t)m, (uint32_t)total, pos, status);
+  hipLaunchKernelGGL(k_rs_tpos, DIST_GRID(m), own2, (uint32_t)m, A, m2, (uint32_t)total, pos,
+                     status);
   return dist_launch_ok(c, "rs_top");
 }
 

@@ -14,9 +14,13 @@ arbitrary share of the node bag and the weave runs as
   4. cause join (shared.cljc:175-178): cause ids travel to the rank owning
      them (cw_partition_keys + all_to_all), are looked up there
      (cw_lookup_keys) and the global ranks travel back (all_to_all);
-  5. the rank-ordered (parent rank, kind, origin) arrays -- 9 bytes a node --
-     gather on one rank, which runs the tree and the Euler tour for the whole
-     list (cw_weave_ranked: the giant-document path of causeweave.hip).
+  5. the tree rank by rank (_tree_distributed: all-to-all rounds between the
+     dist.hip kernels) and the list ranking where the list lies
+     (_rank_ruling: a ruling set whose walkers hop ranks as messages); the
+     weave lands on one rank or spread by weave position.  Lists outside the
+     fast path's domain (and tree="root") instead gather the rank-ordered
+     (parent rank, kind, origin) arrays -- 9 bytes a node -- on one rank, which
+     weaves the whole list there (cw_weave_ranked, with its exact path).
 
 Every step that touches node data is a HIP kernel of libcauseweave behind the
 C ABI; torch provides device memory, the collectives and tiny host-side
@@ -313,6 +317,7 @@ class GiantResult:
     n_owned: int        # ids this rank owned after the sample sort
     max_ts: int
     pos_base: int = 0   # out="sharded": weave position of this rank's weave_perm[0]
+    ranking: dict | None = None   # ruling set: rulers, exchange rounds, messages sent
 
 
 def _a2a(t, send, recv, group):
@@ -474,7 +479,7 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
     own = ops.zeros32(2 * n)
     links = ops.zeros32(4 * M).view(M, 4)   # any walk may end on this rank
     nlinks, status = ops.zeros32(1), ops.zeros32(1)
-    walkers, m, rounds = None, nr, 0
+    walkers, m, rounds, sent = None, nr, 0, 0
     while True:
         msg, key = ops.rs_walk(walkers, m, rlist, rbase, word, thr, base, own, links, nlinks,
                                status)
@@ -489,11 +494,13 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
         if rounds > 2 * N + 4:
             raise RuntimeError("ruling set: the walks did not end")
         recv = [mat[j][r] for j in range(W)]
+        sent += sum(sum(row) for row in mat)
         idx = perm[:sum(send)]
         walkers = _a2a(ops.gather_rows(msg, idx).reshape(-1), [4 * x for x in send],
                        [4 * x for x in recv], group).view(-1, 4)
         m = walkers.shape[0]
     del word, rlist, walkers
+    info = {"rulers": M, "ruler_k": k, "rounds": rounds, "messages": sent}
     nl = int(nlinks[0])
     agg = _all_gather_ints([nl, int(status[0])], group, dev)
     bad = sum(v[0] for v in agg) != M or any(v[1] for v in agg)
@@ -515,10 +522,10 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
         grecv = [2 * owns[j] if r == root else 0 for j in range(W)]
         allrec = _a2a(rec.reshape(-1), gsend, grecv, group).view(-1, 2)
         if r != root:
-            return GiantResult(None, None, None, None, N, n_own, max_ts)
+            return GiantResult(None, None, None, None, N, n_own, max_ts, ranking=info)
         wp, bits, cnt = ops.rs_emit(allrec, 0, N, estat)
         st = int(tstat[0]) | int(estat[0]) | (STATUS_INTERNAL if bad else 0)
-        return GiantResult(wp, bits, int(cnt[0]), st, N, n_own, max_ts)
+        return GiantResult(wp, bits, int(cnt[0]), st, N, n_own, max_ts, ranking=info)
     # sharded: rank j owns positions [j * chunk, (j + 1) * chunk)
     chunk = ((N + W - 1) // W + 31) // 32 * 32
     ps = torch.as_tensor(np.array([min(j * chunk, N) for j in range(1, W)] + [N], np.int64),
@@ -534,7 +541,8 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
     st = (STATUS_INTERNAL if bad else 0)
     for v in tot:
         st |= v[1]
-    return GiantResult(wp, bits, sum(v[0] for v in tot), st, N, n_own, max_ts, pos_base=p0)
+    return GiantResult(wp, bits, sum(v[0] for v in tot), st, N, n_own, max_ts, pos_base=p0,
+                       ranking=info)
 
 
 def _weave_distributed(ops, id_key, cause_key, kind, key_bits, ts_shift, group, root, samples,

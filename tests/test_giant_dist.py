@@ -63,6 +63,8 @@ def _worker(rank, world, port, n, seed, samples, empty_rank, tree, q, opts=None)
             q.put((res.weave_perm.numpy().copy(), res.visible_count, res.status, res.n_total,
                    res.max_ts))
         q.put(("own", rank, res.n_owned))
+        if rank == 0:
+            q.put(("rk", res.ranking))
     finally:
         dist.destroy_process_group()
 
@@ -78,10 +80,12 @@ def run(world, n, seed, samples=64, empty_rank=None, tree="auto", **opts):
         p.start()
     sharded = opts.get("out") == "sharded"
     got, owned, parts = None, {}, []
-    for _ in range(2 * world if sharded else world + 1):
+    for _ in range(2 * world + 1 if sharded else world + 2):
         m = q.get(timeout=120)
         if isinstance(m[0], str) and m[0] == "part":
             parts.append(m)
+        elif isinstance(m[0], str) and m[0] == "rk":
+            run.ranking = m[1]
         elif isinstance(m[0], str):
             owned[m[1]] = m[2]
         else:
@@ -151,6 +155,25 @@ def test_ruling_set_ranking_matches_oracle(world, n, seed, empty, k, out):
     assert vcount == int(vis.sum())
     if out == "sharded":
         assert np.array_equal(got[5], vis)
+
+
+def test_ruling_set_rounds_and_messages_at_w8():
+    """A config-5 list over 8 ranks (DESIGN.md §6 study): every crossing step
+    of the list is one walker message -- ~0.4 per node at W = 8 -- and the
+    rounds are the most crossings of any sublist (K = 16: ~50-120 at this
+    size), with the weave still the oracle's."""
+    n, seed = 20_000, 27
+    got, owned = run(8, n, seed, tree="dist", ranking="ruling")
+    wp, vcount, status, N = got[:4]
+    spec, idk, ck, kd = make_list(n, seed)
+    perm, vis, st = oracle.batch_lists(np.array([0, N], np.uint64), idk, ck, kd,
+                                       method=oracle.METHOD_EFF)
+    sh = np.concatenate(shares(N, 8, seed))
+    assert status == 0 and np.array_equal(sh[wp.view(np.uint32)], perm)
+    info = run.ranking
+    assert info["ruler_k"] == 16 and 0.04 < info["rulers"] / N < 0.09, info
+    assert 0.3 < info["messages"] / N < 0.5, info
+    assert 20 < info["rounds"] < 200, info
 
 
 def _dup_worker(rank, world, port, q):

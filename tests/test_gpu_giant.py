@@ -307,12 +307,13 @@ def test_ruling_set_ops_match_the_double(ops, n, seed, k, lo, hi):
     cw, crl, cnr = cpu.rs_rulers(cs[lo:hi], ct[lo:hi], lo, k, seed32)
     assert nr == cnr and _same(word, cw) and _same(rlist.cpu()[:nr], crl[:nr])
     m = hi - lo
+    rb = 0 if (lo == 0 and hi == N) else 7   # ruler indices of a later rank start higher
     own, links = ops.zeros32(2 * m), ops.zeros32(4 * max(nr, 1)).view(-1, 4)
     nl, st = ops.zeros32(1), ops.zeros32(1)
-    out, key = ops.rs_walk(None, nr, rlist, 7, word, _t(ct.numpy()[lo:hi]), lo, own, links, nl, st)
+    out, key = ops.rs_walk(None, nr, rlist, rb, word, _t(ct.numpy()[lo:hi]), lo, own, links, nl, st)
     cown, clinks = cpu.zeros32(2 * m), cpu.zeros32(4 * max(cnr, 1)).view(-1, 4)
     cnl, cst = cpu.zeros32(1), cpu.zeros32(1)
-    cout, ckey = cpu.rs_walk(None, cnr, crl, 7, cw, ct[lo:hi], lo, cown, clinks, cnl, cst)
+    cout, ckey = cpu.rs_walk(None, cnr, crl, rb, cw, ct[lo:hi], lo, cown, clinks, cnl, cst)
     assert int(st[0]) == 0 == int(cst[0]) and int(nl[0]) == int(cnl[0])
     assert _same(own, cown) and _same(key, ckey)
     moved = ckey.numpy() != -1
@@ -334,6 +335,36 @@ def test_ruling_set_ops_match_the_double(ops, n, seed, k, lo, hi):
     assert _same(wp, want["weave_perm"]) and int(cnt[0]) == int(want["visible_count"][0])
     nb = (N + 31) // 32
     assert _same(bits[:nb], want["visible_bits"][:nb])
+
+
+@pytest.mark.parametrize("m", [1, 2, 1000, (1 << 21) + 5, 3_000_000])
+def test_ruling_set_top_level(ops, m):
+    """cw_dist_rs_top on m ruler links in random list order (ruler 0 first),
+    directly by pointer jumping (m <= 2^21) or in two levels (sub-rulers walk
+    the ruler list): every ruler's position = the lengths before it."""
+    import torch
+
+    rng = np.random.default_rng(m)
+    order = np.concatenate([[0], rng.permutation(np.arange(1, m))]).astype(np.uint32)
+    ln = rng.integers(1, 40, m).astype(np.uint32)
+    nxt = np.full(m, 0xFFFFFFFF, np.uint32)
+    nxt[order[:-1]] = order[1:]
+    links = np.stack([np.arange(m, dtype=np.uint32), nxt, ln, np.zeros(m, np.uint32)], 1)
+    links = links[rng.permutation(m)]          # records arrive in any order
+    want = np.zeros(m, np.uint64)
+    want[order] = np.concatenate([[0], np.cumsum(ln[order].astype(np.uint64))[:-1]])
+    total = int(ln.sum())
+    st = ops.zeros32(1)
+    pos = ops.rs_top(_t(np.ascontiguousarray(links)), total, st)
+    assert int(st[0]) == 0
+    assert np.array_equal(pos.cpu().numpy().view(np.uint32), want.astype(np.uint32))
+    # a broken list (one link lost) is flagged, not ranked silently
+    if m > 2:
+        bad = links.copy()
+        bad[bad[:, 0] == order[m // 2], 1] = 0xFFFFFFFF
+        st = ops.zeros32(1)
+        ops.rs_top(_t(np.ascontiguousarray(bad)), total, st)
+        assert int(st[0]) & 32
 
 
 @pytest.mark.parametrize("tree,ranking,out", [("root", "auto", "root"), ("dist", "root", "root"),
