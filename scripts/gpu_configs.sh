@@ -1,7 +1,7 @@
 #!/bin/bash
 # The non-default BASELINE configurations on the GPU box (via gpurun), each
 # step under its own time limit; the first failure ends the script.
-#   scripts/gpu_configs.sh [c1|c4|c4prof|c5|c5full|c3 ...] -> gpurun_out/cfg/
+#   scripts/gpu_configs.sh [c1|c4|c4prof|c5|c5full|c5dist|c5dist4|c5dist4s|c3 ...] -> gpurun_out/cfg/
 set -e
 R="${GRAFT_REPO_ROOT:-$PWD}"
 cd "$R"
@@ -18,6 +18,12 @@ for s in ${*:-c1 c4 c4prof c5}; do
     c5) timeout -k 10 300 python bench.py --config 5 > $O/c5.json 2> $O/c5.err ;;
     c5full) timeout -k 10 900 python bench.py --config 5 --giant 2000000001 --steps 2 --warmup 1 \
               > $O/c5full.json 2> $O/c5full.err ;;
+    c5dist) timeout -k 10 300 python bench.py --config 5 --dist --tree dist --ranking ruling \
+              > $O/c5dist.json 2> $O/c5dist.err ;;
+    c5dist4) timeout -k 10 600 python bench.py --gpus 4 --config 5 --giant 4194304 --ranking ruling \
+               --check --steps 2 --warmup 1 > $O/c5dist4.json 2> $O/c5dist4.err ;;
+    c5dist4s) timeout -k 10 600 python bench.py --gpus 4 --config 5 --giant 4194304 --ranking ruling \
+                --out sharded --check --steps 2 --warmup 1 > $O/c5dist4s.json 2> $O/c5dist4s.err ;;
     c3) timeout -k 10 900 python bench.py --config 3 > $O/c3.json 2> $O/c3.err ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
