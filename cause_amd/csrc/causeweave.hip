@@ -1199,16 +1199,19 @@ __host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) 
   return sg * 16 + 4 * ((nmax + 1) / 2) + 8 * ((nmax + 31) / 32);
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_front(
+// one document d (the whole workgroup); lds: the dynamic LDS.  Returns false
+// when the document's ids leave the directory (big[0] counts it).  PT / VT:
+// the width of par / sval (u16 inside k_weave_doc: n < 2^16); skind may be
+// null (the tree reads the class bitmaps).
+template <int NT, typename PT = uint32_t, typename VT = uint32_t>
+__device__ __forceinline__ bool front_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
-    const uint32_t *__restrict__ tile_first, uint32_t sg, uint32_t *__restrict__ par,
-    uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
+    const uint32_t *__restrict__ tile_first, uint32_t sg, PT *__restrict__ par,
+    uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t doc0 = 0) {
-  extern __shared__ __attribute__((aligned(16))) uint4 sdir[];
+    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t d, uint4 *sdir) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (tprof) {
@@ -1221,14 +1224,15 @@ __global__ __launch_bounds__(NT) void k_front(
   __shared__ uint64_t rmax[NT / 64];
   __shared__ uint32_t wtot[NT / 64];
   __shared__ uint32_t bst;
-  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, nw = (n + 31) / 32;
   const uint64_t *const idD = id_key + base, *const causeD = cause_key + base;
   const uint8_t *const kindD = kind + base;
   uint16_t *const rankD = rank16 + base;
-  uint32_t *const parD = par + base, *const svalD = sval + base;
-  uint8_t *const skindD = skind + base;
-  if (n == 0) return;
+  PT *const parD = par + base;
+  VT *const svalD = sval + base;
+  uint8_t *const skindD = skind ? skind + base : nullptr;
+  if (n == 0) return true;
   uint32_t *sw = reinterpret_cast<uint32_t *>(sdir);
   uint16_t *p16 = reinterpret_cast<uint16_t *>(sdir + sg);  // par, then sval, by rank
   uint32_t *clsA = reinterpret_cast<uint32_t *>(p16) + (n + 1) / 2, *clsB = clsA + nw;
@@ -1273,7 +1277,7 @@ __global__ __launch_bounds__(NT) void k_front(
   if (tid == 0 && max_ts) max_ts[d] = mx >> ts_shift;
   if (any_far) {
     if (tid == 0) atomicAdd(&big[0], 1u);
-    return;
+    return false;
   }
   stamp(0);
   const uint32_t G = (uint32_t)(mx / FR_GROUP_BITS) + 1;
@@ -1364,9 +1368,9 @@ __global__ __launch_bounds__(NT) void k_front(
           p = pp < p ? pp : 0u;
         }
     }
-    lane_at(parD, r) = p;
+    lane_at(parD, r) = (PT)p;
     const uint32_t a = (clsA[r >> 5] >> (r & 31)) & 1u, b = (clsB[r >> 5] >> (r & 31)) & 1u;
-    lane_at(skindD, r) = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
+    if (skindD) lane_at(skindD, r) = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
   }
   uint32_t *kb = kbm + (size_t)tile_first[d] * KBM_WORDS;
   for (uint32_t w = tid; w < nw; w += NT) {  // word w of the document = word w & 127 of tile w >> 7
@@ -1398,12 +1402,27 @@ __global__ __launch_bounds__(NT) void k_front(
   stamp(3);
   for (uint32_t r = tid; r < n; r += NT) {
     const uint32_t v = p16[r];
-    lane_at(svalD, r) = v;
+    lane_at(svalD, r) = (VT)v;
     if (skey) skey[base + r] = lane_at(idD, (v < n ? v : 0u));  // ids in rank order (yarns)
   }
   stamp(4);
   if (tprof && tid == 0)
     for (int ph = 0; ph < 6; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+  return true;
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_front(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ tile_first, uint32_t sg, uint32_t *__restrict__ par,
+    uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
+    uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
+    uint32_t *__restrict__ status, uint32_t *__restrict__ big,
+    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t doc0 = 0) {
+  extern __shared__ __attribute__((aligned(16))) uint4 lds_fr[];
+  front_doc<NT>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey, rank16,
+                max_ts, ts_shift, status, big, tprof, eff, doc0 + blockIdx.x, lds_fr);
 }
 
 // dst bits [off, off + nbits) |= src bits [0, nbits) (dst zeroed beforehand).
@@ -1754,8 +1773,15 @@ __global__ __launch_bounds__(NT) void k_tree(
 constexpr uint32_t TL_END = 0xFFFFu;
 
 
+// LDS of k_tree_l: the tile tables (hash / sort buffer, member lists, digit
+// counters: tree_l_tile_bytes, at the front of the dynamic buffer) and the
+// document tables (two bitmaps + the u16 table: tree_l_lds_bytes).  (A
+// static array would add to the other phases' LDS in the fused kernel.)
+__host__ __device__ constexpr uint32_t tree_l_tile_bytes(uint32_t nt, uint32_t tile) {
+  return 4 * tile * 4 + (nt / 64) * SUB_BINS * 4 + tile * 2;
+}
 __host__ __device__ constexpr uint32_t tree_l_static_bytes(uint32_t nt, uint32_t tile) {
-  return 4 * tile * 4 + tile * 2 + (nt / 64) * SUB_BINS * 4 + 64 * 4 + 4;
+  return tree_l_tile_bytes(nt, tile) + 64 * 4 + 4;
 }
 __host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
   return ((nmax + 31) / 32) * 8 + ((nmax + 1) / 2) * 4;  // two bitmaps + u16 table
@@ -1763,14 +1789,16 @@ __host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
 
 // MODE (A/B knob CW_TL_MODE): bit 0 = one CAS per insert (else CAS + exchange),
 // bit 1 = the special-table reads and the next parents go out before the keys
-template <int NT, int TILE_T, bool PROF, int MODE>
-__global__ __launch_bounds__(NT) void k_tree_l(
-    const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
+// one document d (the whole workgroup); lds: the dynamic LDS (16-byte aligned)
+template <int NT, int TILE_T, bool PROF, int MODE, typename PT = uint32_t>
+__device__ __forceinline__ void tree_l_doc(
+    const PT *__restrict__ par, const uint8_t *__restrict__ skind,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ doc_log2k, uint32_t kbits,
     uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
     unsigned long long *__restrict__ tprof,
-    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first, uint32_t doc0 = 0) {
+    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first, uint32_t d,
+    uint32_t *lds) {
   constexpr uint32_t IT = TILE_T / NT;
   unsigned long long tacc[16] = {}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -1787,19 +1815,20 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   // fallback sort's tkey/trank/tns and sweep 2's T live in the same buffer.
   constexpr uint32_t HS = 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
   static_assert(TILE_T <= (1u << HB) && 17 + HB <= 32, "slot word layout");
-  __shared__ uint32_t hbuf[3 * TILE_T > 2 * HS ? 3 * TILE_T : 2 * HS];
-  __shared__ uint16_t nxt[TILE_T];
+  static_assert(3 * TILE_T <= 2 * HS, "the sort buffer fits the hash");
+  uint32_t *const hbuf = lds;  // 2 HS words
+  uint32_t(*const wcnt)[SUB_BINS] = reinterpret_cast<uint32_t(*)[SUB_BINS]>(lds + 2 * HS);
+  uint16_t *const nxt = reinterpret_cast<uint16_t *>(lds + 2 * HS + (NT / 64) * SUB_BINS);
+  uint32_t *const bm = lds + tree_l_tile_bytes(NT, TILE_T) / 4;
   uint32_t *const hw = hbuf, *const hk = hbuf, *const hh = hbuf + HS;  // MODE 1 / MODE 0
   uint32_t *const tkey = hbuf, *const trank = hbuf + TILE_T, *const tns = hbuf + 2 * TILE_T;
   uint32_t *const ptab = tns;
-  __shared__ uint32_t wcnt[NT / 64][SUB_BINS];
   __shared__ uint32_t run[64];
   __shared__ uint32_t n_osp;
-  extern __shared__ __attribute__((aligned(16))) uint32_t bm[];
-  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   // this document's slices (wave-uniform bases, lane offsets: lane_at)
-  const uint32_t *const parD = par + base;
+  const PT *const parD = par + base;
   uint32_t *const fcSD = fcS + base, *const nscD = nsc + base;
   uint32_t *const linkD = link + base, *const ospD = osp + base;
   uint32_t *const spec_bm = bm, *const hide_bm = bm + bm_words;
@@ -2156,6 +2185,19 @@ __global__ __launch_bounds__(NT) void k_tree_l(
   }
   if (PROF && tid == 0)
     for (int ph = 0; ph < 16; ph++) tprof[(size_t)d * 16 + ph] = tacc[ph];
+}
+
+template <int NT, int TILE_T, bool PROF, int MODE>
+__global__ __launch_bounds__(NT) void k_tree_l(
+    const uint32_t *__restrict__ par, const uint8_t *__restrict__ skind,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ doc_log2k, uint32_t kbits,
+    uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+    uint32_t *__restrict__ link, uint32_t *__restrict__ osp,
+    unsigned long long *__restrict__ tprof,
+    const uint32_t *__restrict__ kbm, const uint32_t *__restrict__ tile_first, uint32_t doc0 = 0) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_tl[];
+  tree_l_doc<NT, TILE_T, PROF, MODE>(par, skind, doc_off, doc_log2k, kbits, bm_words, nsc, fcS, link,
+                                     osp, tprof, kbm, tile_first, doc0 + blockIdx.x, lds_tl);
 }
 
 // --- tree for one giant document (all tiles in parallel) -------------------------
@@ -2721,9 +2763,9 @@ __host__ __device__ inline uint32_t tour_lds_bytes(uint32_t nmax, uint32_t log2k
   return 4 * ((nmax + 1) / 2 + 2 * ((nmax + 31) / 32) + S);
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
-                                             const uint32_t *__restrict__ sval,
+template <int NT, typename VT = uint32_t>
+__device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
+                                             const VT *__restrict__ sval,
                                              const uint32_t *__restrict__ doc_off,
                                              const uint32_t *__restrict__ doc_log2k,
                                              const uint64_t *__restrict__ skey, uint32_t ts_shift,
@@ -2732,9 +2774,8 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
                                              uint32_t *__restrict__ vcount,
                                              uint32_t *__restrict__ status, uint32_t *loc,
                                              unsigned long long *__restrict__ tprof,
-                                             uint32_t doc0 = 0) {
+                                             uint32_t d, uint32_t *sm) {
   constexpr uint32_t SPT = 8;  // sublists per thread in the jumping rounds: S <= SPT * NT
-  extern __shared__ __attribute__((aligned(16))) uint32_t sm[];
   __shared__ uint32_t wtot[NT / 64];
   __shared__ uint32_t bad_s, next_j;
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
@@ -2746,7 +2787,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
     }
   };
   stamp(-1);
-  const uint32_t d = doc0 + blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base, log2k = doc_log2k[d];
   const uint32_t *const linkD = link + base;
   uint32_t *const locD = loc + base, *const permD = perm + base;
@@ -2915,6 +2956,56 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
   stamp(4);
   if (tprof && tid == 0)
     for (int ph = 0; ph < 6; ph++) tprof[(size_t)d * 8 + ph] = tacc[ph];
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
+                                             const uint32_t *__restrict__ sval,
+                                             const uint32_t *__restrict__ doc_off,
+                                             const uint32_t *__restrict__ doc_log2k,
+                                             const uint64_t *__restrict__ skey, uint32_t ts_shift,
+                                             uint64_t *__restrict__ max_ts,
+                                             uint32_t *__restrict__ perm, uint32_t *__restrict__ vbits,
+                                             uint32_t *__restrict__ vcount,
+                                             uint32_t *__restrict__ status, uint32_t *loc,
+                                             unsigned long long *__restrict__ tprof,
+                                             uint32_t doc0 = 0) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_t[];
+  tour_doc<NT>(link, sval, doc_off, doc_log2k, skey, ts_shift, max_ts, perm, vbits, vcount, status, loc, tprof, doc0 + blockIdx.x, lds_t);
+}
+
+// --- the whole weave of one document in ONE workgroup (CW_FUSED, round 3) -------
+// front end, tree and tour of document blockIdx.x back to back: the three
+// phases reuse the same LDS, the handoffs (par, class bitmaps, sval; nsc, fcS;
+// link) go through memory written by this workgroup a moment earlier (its
+// L2 slice has them), the CUs of the chip are at different phases at any time
+// (the front end streams HBM while the tree and the tour wait on LDS), and
+// there is one tail instead of three.  A document whose ids leave the front
+// end's directory counts itself in big[0] and stops: the host then weaves the
+// batch with the separate kernels.
+template <int NT, int TILE_T, typename VT>
+__global__ __launch_bounds__(NT) void k_weave_doc(
+    const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
+    const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
+    const uint32_t *__restrict__ tile_first, uint32_t sg, uint16_t *__restrict__ par,
+    uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
+    uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
+    uint32_t *__restrict__ status, uint32_t *__restrict__ big, const uint32_t *__restrict__ doc_log2k,
+    uint32_t kbits, uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+    uint32_t *__restrict__ link, uint32_t *__restrict__ osp, uint32_t *__restrict__ perm,
+    uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
+  const uint32_t d = blockIdx.x;
+  if (!front_doc<NT, uint16_t, VT>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
+                     rank16, max_ts, ts_shift, status, big, nullptr, 0u, d,
+                     reinterpret_cast<uint4 *>(lds_w)))
+    return;
+  __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
+  tree_l_doc<NT, TILE_T, false, 0, uint16_t>(par, skind, doc_off, doc_log2k, kbits, bm_words, nsc, fcS, link,
+                                   osp, nullptr, kbm, tile_first, d, lds_w);
+  __syncthreads();
+  tour_doc<NT, VT>(link, sval, doc_off, doc_log2k, nullptr, 0u, nullptr, perm, vbits, vcount, status,
+                   loc, nullptr, d, lds_w);
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
@@ -3643,6 +3734,7 @@ struct cw_ctx {
                                    // go through the giant path document by document
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
+  uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
   uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
@@ -3802,10 +3894,11 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
   t.tour = false;
   t.tour_log2k = c->tour_log2k;
   if (c->tour && !giant && nmax <= TOUR_END) {
-    while (t.tour_log2k < 8 && (tour_lds_bytes((uint32_t)nmax, t.tour_log2k) > std::min(TOUR_LDS_MAX, c->lds_max - 1024) ||
+    auto lds = [&](uint32_t l2k) { return tour_lds_bytes((uint32_t)nmax, l2k); };
+    while (t.tour_log2k < 8 && (lds(t.tour_log2k) > std::min(TOUR_LDS_MAX, c->lds_max - 1024) ||
                                 ((nmax + (1u << t.tour_log2k) - 1) >> t.tour_log2k) > 8 * 1024))
       t.tour_log2k++;
-    t.tour = tour_lds_bytes((uint32_t)nmax, t.tour_log2k) <= std::min(TOUR_LDS_MAX, c->lds_max - 1024);
+    t.tour = lds(t.tour_log2k) <= std::min(TOUR_LDS_MAX, c->lds_max - 1024);
   }
   for (uint64_t d = 0; d < D; d++) {
     const uint32_t b = (uint32_t)off[d], n = (uint32_t)(off[d + 1] - off[d]);
@@ -4159,7 +4252,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     Launch L(c, "tree", tree_l ? (double)N * (4 + 1 + 4 + 4 + 8 + 4)
                                : (double)N * (4 + 1 + 4 + 8 + 4 + 8 + 4 + 4));
     auto tree_l_kernel = [&](auto kern) {
-      hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(TL_NT), (size_t)tl_dyn, c->stream, par, skind,
+      hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(TL_NT),
+                         (size_t)tl_dyn + tree_l_tile_bytes(TL_NT, tree_l), c->stream, par, skind,
                          doc_off, doc_log2k, kbits, (t.nmax + 31) / 32, nsc, fcS,
                          (uint32_t *)link, thr, tprof, kbm, dev_tab(c, "t_tile_first"), 0u);
     };
@@ -4386,7 +4480,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     uint32_t *sval = nullptr;
     const bool want_yarns = out->yarn_perm && bt->site_bits;
     // 1-2 (dense ids). id order and join through per-document rank directories
-    bool front_done = false;
+    bool front_done = false, fused_done = false;
     uint32_t *kbm = nullptr;  // special / hide bitmaps per tile (front end -> tree)
     // fused front end: documents of < 2^16 nodes whose ids fit a 40 KiB directory
     if (c->front && c->front_fused && N >= (uint64_t)c->front_min_avg * D &&
@@ -4404,15 +4498,52 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         tprof_f = scratch_t<unsigned long long>(c, "tprof3", (size_t)D * 8);
         HIPCHK(c, hipMemsetAsync(tprof_f, 0, (size_t)D * 64, c->stream));
       }
-      {
+      // the whole weave in one kernel when every phase fits: k_tree_l's
+      // 2,048-rank tiles and the fused tour (CW_FUSED)
+      const uint32_t fr_lds = front_lds_bytes(t.nmax, FRONT_FUSED_SG);
+      const uint32_t tl_lds = tree_l_lds_bytes(t.nmax) + tree_l_tile_bytes(1024, 2048);
+      const uint32_t to_lds = tour_lds_bytes(t.nmax, t.tour_log2k);
+      const uint32_t wd_lds = std::max(fr_lds, std::max(tl_lds, to_lds));
+      fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 && !c->tree_pad && !c->tree_prof &&
+                   !c->front_eff && tl_lds + 64 * 4 + 4 <= c->lds_max && wd_lds + 1024 <= c->lds_max &&
+                   to_lds <= TOUR_LDS_MAX;
+      if (fused_done) {
+        uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *thr = scratch_t<uint32_t>(c, "thr", N);
+        uint32_t *loc = scratch_t<uint32_t>(c, "tour_loc", N);
+        if (!fcS || !thr || !loc)
+          return fail(c, "out of device memory (fused weave)");
+        const uint32_t kbits_t = ceil_log2((uint64_t)t.nmax + 1) + 1;
+        // par and (without yarns, which sort by it) sval as u16, no skind
+        uint16_t *par16 = scratch_t<uint16_t>(c, "par16", N);
+        uint16_t *sval16 = want_yarns ? nullptr : scratch_t<uint16_t>(c, "sval16", N);
+        if (!par16 || (!want_yarns && !sval16)) return fail(c, "out of device memory (fused weave)");
+        // algorithmic bytes: front end (ids twice, causes, kinds, the rank scratch
+        // out and back, par 2, sval 2 or 4, class bitmaps), tree (par 2, kind bits;
+        // fcS clear 4, nsc 4; fcS + nsc back 8, link 4), tour (link 4, sval, the
+        // (sublist, index) records out and back 8, weave_perm 4, bits)
+        const double sv = want_yarns ? 4 : 2;
+        Launch L(c, "weave", (double)N * (8 + 8 + 8 + 1 + 2 + 2 + 2 + sv + (skey ? 16 : 0) + 0.25) +
+                                 (double)N * (2 + 0.25 + 4 + 4 + 8 + 4) +
+                                 (double)N * (4 + sv + 8 + 4 + 0.125));
+        auto launch = [&](auto kern, auto *sv_ptr) {
+          hipLaunchKernelGGL(kern, dim3((uint32_t)D), dim3(1024), (size_t)wd_lds, c->stream, id_key,
+                             cause_key, kind, doc_off, dev_tab(c, "t_tile_first"), FRONT_FUSED_SG, par16,
+                             nullptr, sv_ptr, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status,
+                             big, dev_tab(c, "t_doc_log2k"), kbits_t, (t.nmax + 31) / 32, nsc, fcS,
+                             (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
+                             out->visible_count, loc);
+        };
+        if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t>, sval);
+        else launch(k_weave_doc<1024, 2048, uint16_t>, sval16);
+      } else {
         Launch L(c, "front", (double)N * (8 + 8 + 1 + 2 + 4 + 1 + 2 + 4 + (skey ? 16 : 0)) + (double)N * 8);
         hipLaunchKernelGGL(k_front<1024>, dim3((uint32_t)D), dim3(1024),
-                           (size_t)front_lds_bytes(t.nmax, FRONT_FUSED_SG), c->stream, id_key,
+                           (size_t)fr_lds, c->stream, id_key,
                            cause_key, kind, doc_off, dev_tab(c, "t_tile_first"), FRONT_FUSED_SG, par,
                            skind, sval, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status, big,
                            tprof_f, c->front_eff);
       }
-      if (check_launch(c, "front")) return -1;
+      if (check_launch(c, fused_done ? "weave" : "front")) return -1;
       if (tprof_f) {
         std::vector<unsigned long long> h((size_t)D * 8);
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4430,6 +4561,12 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         c->x_hint = c->pin_small[1] != 0;  // flagged documents, for the exact path
       } else {  // a document's ids leave the small directory: the three-kernel front end
         HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
+        if (fused_done) {  // (and the separate tree and tour: the fused kernel stopped early)
+          fused_done = false;
+          HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
+          if (out->visible_bits)
+            HIPCHK(c, hipMemsetAsync(out->visible_bits, 0, ((size_t)N + 31) / 32 * 4, c->stream));
+        }
         sval = nullptr;
         skey = nullptr;
         kbm = nullptr;
@@ -4589,7 +4726,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }
     // without yarns the id-sort buffers are free once the ids are joined
     const bool spare = !want_yarns;
-    if (weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
+    if (!fused_done &&
+        weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
                    front_done ? nullptr : skey, bt->ts_shift, out, spare ? skA : nullptr,
                    spare ? skB : nullptr))
       return -1;
@@ -5758,6 +5896,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->giant_docs_max = knob("CW_GIANT_DOCS", 32);
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
+  c->fused = knob("CW_FUSED", 1);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

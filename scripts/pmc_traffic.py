@@ -20,7 +20,8 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ALIAS = {"pack_bits": "packbits", "tree_l": "tree"}  # k_tree_l is the library's "tree" stat
+# k_tree_l is the library's "tree" stat, k_weave_doc its "weave"
+ALIAS = {"pack_bits": "packbits", "tree_l": "tree", "weave_doc": "weave"}
 
 
 def stat_name(sym):

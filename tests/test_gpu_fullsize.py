@@ -24,8 +24,8 @@ def mixed():
     return F.config2_mixed(12, 12)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"CW_TOUR": "0"}, {"CW_FRONT": "0"}],
-                         ids=["default", "hbm-walk", "radix"])
+@pytest.mark.parametrize("knobs", [{}, {"CW_FUSED": "0"}, {"CW_TOUR": "0"}, {"CW_FRONT": "0"}],
+                         ids=["default", "separate", "hbm-walk", "radix"])
 def test_config2_full_documents_vs_literal(mixed, knobs, monkeypatch):
     off, idk, ck, kd, dirty, lay = mixed
     assert len(dirty) == 24 and dirty.sum() == 12

@@ -20,10 +20,12 @@ pytestmark = pytest.mark.gpu
 
 
 # Front ends: "front" = rank directories for every document (CW_FRONT_MIN_AVG=0
-# also sends tiny documents through it; the fused k_front where it applies),
-# "front3" = the three-kernel directory front end, "radix" = segmented radix
-# sort + join.
+# also sends tiny documents through it; the whole weave of a document in one
+# kernel, k_weave_doc, where it applies), "separate" = k_front, k_tree_l and
+# k_tour as three kernels, "front3" = the three-kernel directory front end,
+# "radix" = segmented radix sort + join.
 FRONTS = {"front": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0"},
+          "separate": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0", "CW_FUSED": "0"},
           "front3": {"CW_FRONT": "1", "CW_FRONT_MIN_AVG": "0", "CW_FRONT_FUSED": "0"},
           "radix": {"CW_FRONT": "0"},
           "radix-global": {"CW_FRONT": "0", "CW_PACK_SORT": "0"},  # no LDS pack sorts
@@ -333,7 +335,8 @@ def test_config2_documents_any_geometry(knobs, monkeypatch):
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"CW_TOUR": "0"}], ids=["default", "hbm-walk"])
+@pytest.mark.parametrize("knobs", [{}, {"CW_FUSED": "0"}, {"CW_TOUR": "0"}],
+                         ids=["default", "separate", "hbm-walk"])
 def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
     """The whole bench workload (10,000 config-2 documents, 5e8 nodes) against
     the oracle, every document, plus permutation validity."""
