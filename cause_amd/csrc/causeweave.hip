@@ -3735,6 +3735,8 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
+  uint32_t map_flags = 1;          // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
+                                   // CW_MAP_RELAXED (bit 2)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
   uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
@@ -5897,6 +5899,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->fused = knob("CW_FUSED", 1);
+  c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |
+                 (knob("CW_MAP_RELAXED", 0) ? 4u : 0u);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

@@ -76,7 +76,11 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     uint64_t *__restrict__ seg_offsets, uint32_t *__restrict__ seg_coll,
     uint64_t *__restrict__ seg_key, int64_t *__restrict__ seg_active,
     uint32_t *__restrict__ seg_perm, uint32_t *__restrict__ status, uint32_t *ctl,
-    unsigned long long *__restrict__ tprof) {
+    unsigned long long *__restrict__ tprof, uint32_t mflags) {
+  // mflags (A/B knobs CW_MAP_DIR, CW_MAP_LBW, CW_MAP_RELAXED): bit 0 = sort 1
+  // through the id directory where it fits, bit 1 = four look-back windows a
+  // round trip, bit 2 = relaxed look-back atomics (the 64-bit word is the
+  // whole message: flag and count; no acquire / release fences around it)
   constexpr uint32_t IT = PK / NT;
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -94,7 +98,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // order -> input), P16 (id order: cause position or MP_*), Q (id order -> key
   // order), LQ / KQ (key order: collection-local input index, kind).
   __shared__ uint64_t A[PK], B[PK];
-  __shared__ uint16_t VS[PK], I2J[PK], P16[PK], Q[PK], LQ[PK];
+  __shared__ __attribute__((aligned(16))) uint16_t U16[5 * PK];  // VS I2J P16 Q LQ (one block: sort 1's directory)
+  uint16_t *const VS = U16, *const I2J = U16 + PK, *const P16 = U16 + 2 * PK, *const Q = U16 + 3 * PK,
+                  *const LQ = U16 + 4 * PK;
   __shared__ uint8_t K8[PK], KQ[PK];
   __shared__ uint32_t dstart[PK + 1], dstat[PK];
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS], run[64], wtot[NT / 64];
@@ -165,7 +171,64 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   const uint64_t imask = (1ull << min(kbits, 63u)) - 1;
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) ck[u] = fits ? (((uint64_t)dl0[u] << kbits) | ck[u]) : 0ull;
-  mp_sort<NT, IT>(ck, val, len, fits ? kbits + dbits : 1, A, VS, wcnt, run);
+  // Lamport ids are dense: when every collection's id range fits a slice of a
+  // pack-wide bitmap (P16 | Q | LQ, 1.5 PK words), an id's sorted position is
+  // the number of set bits before it -- one atomicOr and one lookup a node
+  // instead of the radix passes.  A repeated id (DUP) takes the sort.
+  constexpr uint32_t DIRW = 3 * PK / 2;
+  const uint32_t lw = kbits > 5 ? kbits - 5 : 0;  // log2 of the words per collection
+  bool sorted = false;
+  if ((mflags & 1) && fits && ((uint64_t)nd << lw) <= DIRW) {
+    uint32_t *const dir = reinterpret_cast<uint32_t *>(P16);
+    uint16_t *const wpre = VS;  // (VS | I2J: 2 PK >= DIRW prefix counts)
+    const uint32_t nwd = nd << lw;
+    for (uint32_t w = tid; w < nwd; w += NT) dir[w] = 0;
+    __syncthreads();
+    bool dup = false;
+#pragma unroll
+    for (uint32_t u = 0; u < IT; u++) {
+      if (wb_elem<IT>(u) >= len) continue;
+      const uint32_t x = (uint32_t)(ck[u] & imask), w = (dl0[u] << lw) + (x >> 5), m = 1u << (x & 31);
+      dup |= (atomicOr(&dir[w], m) & m) != 0;
+    }
+    if (!__syncthreads_or(dup)) {
+      // exclusive prefix of the words' popcounts: contiguous words per thread
+      const uint32_t per = (nwd + NT - 1) / NT, w0 = min(nwd, tid * per), w1 = min(nwd, w0 + per);
+      uint32_t c = 0;
+      for (uint32_t w = w0; w < w1; w++) c += __popc(dir[w]);
+      uint32_t run0 = block_exscan<NT>(c, wtot, nullptr);
+      for (uint32_t w = w0; w < w1; w++) {
+        wpre[w] = (uint16_t)run0;
+        run0 += __popc(dir[w]);
+      }
+      __syncthreads();
+      uint32_t pos[IT];
+#pragma unroll
+      for (uint32_t u = 0; u < IT; u++) {
+        const uint32_t x = (uint32_t)(ck[u] & imask), w = (dl0[u] << lw) + (x >> 5);
+        pos[u] = wb_elem<IT>(u) < len ? wpre[w] + __popc(dir[w] & ((1u << (x & 31)) - 1)) : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < IT; u++)
+        if (wb_elem<IT>(u) < len) {
+          A[pos[u]] = ck[u];
+          VS[pos[u]] = (uint16_t)val[u];
+        }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < IT; u++) {
+        const uint32_t j = wb_elem<IT>(u);
+        if (j < len) {
+          ck[u] = A[j];
+          val[u] = VS[j];
+        }
+      }
+      __syncthreads();
+      sorted = true;
+    }
+  }
+  if (!sorted) mp_sort<NT, IT>(ck, val, len, fits ? kbits + dbits : 1, A, VS, wcnt, run);
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t i = wb_elem<IT>(u);
@@ -268,9 +331,11 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   stamp(2);
   // 4. publish this pack's number of key weaves (its prefix comes after the
   // weave below, so the wait for earlier packs overlaps this pack's work)
-  if (tid == 0)
-    __hip_atomic_store(lb + pk, (pk == 0 ? LB_INC : LB_AGG) | nseg, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    const unsigned long long w = (pk == 0 ? LB_INC : LB_AGG) | nseg;
+    if (mflags & 4) __hip_atomic_store(lb + pk, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else __hip_atomic_store(lb + pk, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // 5. each key weave's list weave: member 0 the root, members 1..m in id order
   uint32_t mst[IT], mm[IT], mr[IT], me[IT];
@@ -513,32 +578,54 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   }
   stamp(4);
   // 7. this pack's first key weave number: decoupled look-back over the packs,
-  // one wave reading 64 predecessors at a time (earlier packs are dispatched
-  // first and publish their counts before weaving, so the wait always ends)
+  // one wave reading LBW windows of 64 predecessors per round trip (earlier
+  // packs are dispatched first and publish their counts before weaving, so the
+  // wait always ends).  The resident packs reach their look-backs together, so
+  // the nearest inclusive prefix is typically a whole residency (~500 packs)
+  // back: one window per round trip cost ~8 L2 round trips (20k clocks).
   if (tid < 64) {
+    constexpr uint32_t LBW = 4;
+    const uint32_t lbw = (mflags & 2) ? LBW : 1;
     const uint32_t lane = tid;
     uint32_t base = 0;
     if (pk > 0) {
-      for (int64_t q0 = (int64_t)pk - 1; q0 >= 0;) {
-        const int64_t q = q0 - lane;  // lane 0 = the nearest predecessor
-        const unsigned long long v =
-            q >= 0 ? __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : LB_INC;
-        const uint64_t inc = __ballot((v >> 62) == 2), none = __ballot((v >> 62) == 0);
-        const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive
-        const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-        if (none & need) {  // a pack in the window has not counted its key weaves yet
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        uint32_t x = lane <= first ? (uint32_t)v : 0u;
+      for (int64_t q0 = (int64_t)pk - 1;;) {
+        unsigned long long v[LBW];
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        base += x;
-        if (first < 64) break;
-        q0 -= 64;
+        for (uint32_t k = 0; k < LBW; k++) {
+          const int64_t q = q0 - 64 * (int64_t)k - lane;  // lane 0 of window 0 = the nearest
+          v[k] = !(q >= 0 && k < lbw) ? (k < lbw ? LB_INC : 0ull)
+                 : (mflags & 4) ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bool done = false, retry = false;  // (wave-uniform: ballots)
+#pragma unroll
+        for (uint32_t k = 0; k < LBW; k++) {
+          if (done || retry || k >= lbw) continue;
+          const uint64_t inc = __ballot((v[k] >> 62) == 2), none = __ballot((v[k] >> 62) == 0);
+          const uint32_t first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // nearest inclusive
+          const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+          if (none & need) {  // a pack in this window has not counted its key weaves yet
+            retry = true;
+            continue;
+          }
+          uint32_t x = lane <= first ? (uint32_t)v[k] : 0u;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+          base += x;
+          if (first < 64) done = true;
+          else q0 -= 64;
+        }
+        if (done) break;
+        if (retry) __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0)
-        __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      {
+        if (mflags & 4)
+          __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+          __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     if (lane == 0) {
       s_base = base;
@@ -653,7 +740,7 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
   hipLaunchKernelGGL((k_map_pack<PK_, NT_>), dim3(P), dim3(NT_), 0, c->stream, id, cause, cis, kind, \
                      (const uint64_t *)c->bufs["mp_off"].p, (const uint32_t *)c->bufs["mp_doc0"].p, \
                      P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
-                     sp, st, ctl, tprof)
+                     sp, st, ctl, tprof, c->map_flags)
     if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
     else if (c->map_pack == 2) CW_MAP_PACK_LAUNCH(2048, 1024);
     else CW_MAP_PACK_LAUNCH(2048, 512);
