@@ -1788,7 +1788,10 @@ __host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
 }
 
 // MODE (A/B knob CW_TL_MODE): bit 0 = one CAS per insert (else CAS + exchange),
-// bit 1 = the special-table reads and the next parents go out before the keys
+// bit 1 = the special-table reads and the next parents go out before the keys,
+// bit 2 = a group whose parent lies in the tile (69% of config-2 nodes) keeps
+// its list head in a direct table indexed by (class, parent - tile start): one
+// exchange instead of a claiming CAS + exchange (with bit 0 clear)
 // one document d (the whole workgroup); lds: the dynamic LDS (16-byte aligned)
 template <int NT, int TILE_T, bool PROF, int MODE, typename PT = uint32_t>
 __device__ __forceinline__ void tree_l_doc(
@@ -1813,12 +1816,13 @@ __device__ __forceinline__ void tree_l_doc(
   // the head of the slot's member list (a tile index; MODE bit 0 packs both
   // into hw[slot] = key << HB | head); nxt: next member, TL_END ends.  The
   // fallback sort's tkey/trank/tns and sweep 2's T live in the same buffer.
-  constexpr uint32_t HS = 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
+  constexpr bool DH = (MODE & 4) && !(MODE & 1);
+  constexpr uint32_t HS = DH ? TILE_T : 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
   static_assert(TILE_T <= (1u << HB) && 17 + HB <= 32, "slot word layout");
-  static_assert(3 * TILE_T <= 2 * HS, "the sort buffer fits the hash");
-  uint32_t *const hbuf = lds;  // 2 HS words
-  uint32_t(*const wcnt)[SUB_BINS] = reinterpret_cast<uint32_t(*)[SUB_BINS]>(lds + 2 * HS);
-  uint16_t *const nxt = reinterpret_cast<uint16_t *>(lds + 2 * HS + (NT / 64) * SUB_BINS);
+  static_assert(2 * HS + (DH ? 2 * TILE_T : 0) == 4 * TILE_T, "hash (+ direct heads) = 4 TILE_T words");
+  uint32_t *const hbuf = lds;  // 4 TILE_T words: hash keys, hash heads (, direct heads)
+  uint32_t(*const wcnt)[SUB_BINS] = reinterpret_cast<uint32_t(*)[SUB_BINS]>(lds + 4 * TILE_T);
+  uint16_t *const nxt = reinterpret_cast<uint16_t *>(lds + 4 * TILE_T + (NT / 64) * SUB_BINS);
   uint32_t *const bm = lds + tree_l_tile_bytes(NT, TILE_T) / 4;
   uint32_t *const hw = hbuf, *const hk = hbuf, *const hh = hbuf + HS;  // MODE 1 / MODE 0
   uint32_t *const tkey = hbuf, *const trank = hbuf + TILE_T, *const tns = hbuf + 2 * TILE_T;
@@ -1881,6 +1885,8 @@ __device__ __forceinline__ void tree_l_doc(
       hw[i] = 0;
       if (!(MODE & 1)) hh[i] = TL_END;
     }
+    if (DH)
+      for (uint32_t i = tid; i < 2 * TILE_T; i += NT) hbuf[2 * HS + i] = TL_END;
   };
   clear_hash();
   if (tid == 0) n_osp = 0;
@@ -1941,6 +1947,13 @@ __device__ __forceinline__ void tree_l_doc(
       slot[k] = 0;
       if (j < len && kk) {
         uint32_t h = (kk * 0x9E3779B1u) >> (32 - __builtin_ctz(HS)), cmp = 0u;
+        const uint32_t e = (kk >> 1) - 1;
+        if (DH && e >= r0) {  // slot = the head's word in hbuf
+          const uint32_t s = 2 * HS + (kk & 1) * TILE_T + (e - r0);
+          nxt[j] = (uint16_t)atomicExch(&hbuf[s], j);
+          slot[k] = s;
+          continue;
+        }
         if (MODE & 1) {
           for (;;) {  // one CAS for a new group; pushes onto a group's list retry
             const uint32_t old = atomicCAS(&hw[h], cmp, (kk << HB) | j);
@@ -1963,7 +1976,7 @@ __device__ __forceinline__ void tree_l_doc(
           }
           nxt[j] = (uint16_t)atomicExch(&hh[h], j);
         }
-        slot[k] = h;
+        slot[k] = DH ? HS + h : h;
       }
     }
     stamp(11);
@@ -1975,7 +1988,9 @@ __device__ __forceinline__ void tree_l_doc(
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = wb_elem<IT>(k);
-      uint32_t x = !(j < len && key[k]) ? TL_END : (MODE & 1) ? (hw[slot[k]] & ((1u << HB) - 1)) : hh[slot[k]];
+      uint32_t x = !(j < len && key[k]) ? TL_END
+                   : (MODE & 1) ? (hw[slot[k]] & ((1u << HB) - 1))
+                   : DH ? hbuf[slot[k]] : hh[slot[k]];
       uint32_t p1 = 0, steps = 0;
       bool ls = true;
 #pragma unroll 1
@@ -2065,7 +2080,10 @@ __device__ __forceinline__ void tree_l_doc(
           if (kk & 1) tab[e] = (uint16_t)r;
           else lane_at(fcSD, e) = r;
         }
-        if (kk) {
+        if (kk && DH) {
+          if (slot[k] < 2 * HS) hk[slot[k] - HS] = 0;
+          hbuf[slot[k]] = TL_END;
+        } else if (kk) {
           hw[slot[k]] = 0;
           if (!(MODE & 1)) hh[slot[k]] = TL_END;
         }
@@ -2983,7 +3001,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 // there is one tail instead of three.  A document whose ids leave the front
 // end's directory counts itself in big[0] and stops: the host then weaves the
 // batch with the separate kernels.
-template <int NT, int TILE_T, typename VT>
+template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0>
 __global__ __launch_bounds__(NT) void k_weave_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
@@ -2993,19 +3011,30 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
     uint32_t *__restrict__ status, uint32_t *__restrict__ big, const uint32_t *__restrict__ doc_log2k,
     uint32_t kbits, uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp, uint32_t *__restrict__ perm,
-    uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc) {
+    uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc,
+    unsigned long long *__restrict__ tprof) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
   const uint32_t d = blockIdx.x;
+  // (tprof, CW_TREE_PROF: the three phases' clocks per document)
+  const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   if (!front_doc<NT, uint16_t, VT>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, 0u, d,
                      reinterpret_cast<uint4 *>(lds_w)))
     return;
   __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
-  tree_l_doc<NT, TILE_T, false, 0, uint16_t>(par, skind, doc_off, doc_log2k, kbits, bm_words, nsc, fcS, link,
+  const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
+  tree_l_doc<NT, TILE_T, false, TLM, uint16_t>(par, skind, doc_off, doc_log2k, kbits, bm_words, nsc, fcS, link,
                                    osp, nullptr, kbm, tile_first, d, lds_w);
   __syncthreads();
+  const unsigned long long t2 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   tour_doc<NT, VT>(link, sval, doc_off, doc_log2k, nullptr, 0u, nullptr, perm, vbits, vcount, status,
                    loc, nullptr, d, lds_w);
+  if (PROF && threadIdx.x == 0) {
+    const unsigned long long t3 = __builtin_amdgcn_s_memtime();
+    tprof[(size_t)d * 4] = t1 - t0;
+    tprof[(size_t)d * 4 + 1] = t2 - t1;
+    tprof[(size_t)d * 4 + 2] = t3 - t2;
+  }
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
@@ -3735,8 +3764,8 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
-  uint32_t map_flags = 1;          // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
-                                   // CW_MAP_RELAXED (bit 2)
+  uint32_t map_flags = 1 | 4 | 8 | 16;  // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
+                                   // CW_MAP_RELAXED (bit 2), CW_MAP_DIRJOIN (bit 3), CW_MAP_EARLY (bit 4)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
   uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
@@ -4506,7 +4535,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t tl_lds = tree_l_lds_bytes(t.nmax) + tree_l_tile_bytes(1024, 2048);
       const uint32_t to_lds = tour_lds_bytes(t.nmax, t.tour_log2k);
       const uint32_t wd_lds = std::max(fr_lds, std::max(tl_lds, to_lds));
-      fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 && !c->tree_pad && !c->tree_prof &&
+      fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 && !c->tree_pad &&
                    !c->front_eff && tl_lds + 64 * 4 + 4 <= c->lds_max && wd_lds + 1024 <= c->lds_max &&
                    to_lds <= TOUR_LDS_MAX;
       if (fused_done) {
@@ -4533,10 +4562,18 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              nullptr, sv_ptr, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status,
                              big, dev_tab(c, "t_doc_log2k"), kbits_t, (t.nmax + 31) / 32, nsc, fcS,
                              (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
-                             out->visible_count, loc);
+                             out->visible_count, loc, tprof_f);
         };
-        if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t>, sval);
-        else launch(k_weave_doc<1024, 2048, uint16_t>, sval16);
+        if (tprof_f) {
+          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true>, sval);
+          else launch(k_weave_doc<1024, 2048, uint16_t, true>, sval16);
+        } else if (c->tl_mode == 4) {
+          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false, 4>, sval);
+          else launch(k_weave_doc<1024, 2048, uint16_t, false, 4>, sval16);
+        } else {
+          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false>, sval);
+          else launch(k_weave_doc<1024, 2048, uint16_t, false>, sval16);
+        }
       } else {
         Launch L(c, "front", (double)N * (8 + 8 + 1 + 2 + 4 + 1 + 2 + 4 + (skey ? 16 : 0)) + (double)N * 8);
         hipLaunchKernelGGL(k_front<1024>, dim3((uint32_t)D), dim3(1024),
@@ -4546,7 +4583,16 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            tprof_f, c->front_eff);
       }
       if (check_launch(c, fused_done ? "weave" : "front")) return -1;
-      if (tprof_f) {
+      if (tprof_f && fused_done) {
+        std::vector<unsigned long long> h((size_t)D * 8);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipMemcpy(h.data(), tprof_f, (size_t)D * 64, hipMemcpyDeviceToHost));
+        double a[3] = {0};
+        for (uint64_t dd = 0; dd < D; dd++)
+          for (int ph = 0; ph < 3; ph++) a[ph] += (double)h[dd * 4 + ph];
+        fprintf(stderr, "weave phases (memtime ticks per doc): front %.0f tree %.0f tour %.0f\n", a[0] / D,
+                a[1] / D, a[2] / D);
+      } else if (tprof_f) {
         std::vector<unsigned long long> h((size_t)D * 8);
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipMemcpy(h.data(), tprof_f, (size_t)D * 64, hipMemcpyDeviceToHost));
@@ -5900,7 +5946,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->fused = knob("CW_FUSED", 1);
   c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |
-                 (knob("CW_MAP_RELAXED", 0) ? 4u : 0u);
+                 (knob("CW_MAP_RELAXED", 1) ? 4u : 0u) | (knob("CW_MAP_DIRJOIN", 1) ? 8u : 0u) |
+                 (knob("CW_MAP_EARLY", 1) ? 16u : 0u);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

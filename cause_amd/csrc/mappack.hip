@@ -71,16 +71,20 @@ template <int PK, int NT>
 __global__ __launch_bounds__(NT) void k_map_pack(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause,
     const uint8_t *__restrict__ cause_is_id, const uint8_t *__restrict__ kind,
-    const uint64_t *__restrict__ coll_off, const uint32_t *__restrict__ pack_doc0, uint32_t P,
+    const uint64_t *__restrict__ coll_off, const uint32_t *__restrict__ pack_doc0,
+    const uint64_t *__restrict__ pack_s0, uint32_t P,
     uint32_t token_bits, unsigned long long *lb, uint64_t cap_segs, uint64_t n_total,
     uint64_t *__restrict__ seg_offsets, uint32_t *__restrict__ seg_coll,
     uint64_t *__restrict__ seg_key, int64_t *__restrict__ seg_active,
     uint32_t *__restrict__ seg_perm, uint32_t *__restrict__ status, uint32_t *ctl,
     unsigned long long *__restrict__ tprof, uint32_t mflags) {
-  // mflags (A/B knobs CW_MAP_DIR, CW_MAP_LBW, CW_MAP_RELAXED): bit 0 = sort 1
-  // through the id directory where it fits, bit 1 = four look-back windows a
-  // round trip, bit 2 = relaxed look-back atomics (the 64-bit word is the
-  // whole message: flag and count; no acquire / release fences around it)
+  // mflags (A/B knobs CW_MAP_DIR, CW_MAP_LBW, CW_MAP_RELAXED, CW_MAP_DIRJOIN):
+  // bit 0 = sort 1 through the id directory where it fits, bit 1 = four
+  // look-back windows a round trip, bit 2 = relaxed look-back atomics (the
+  // 64-bit word is the whole message: flag and count; no acquire / release
+  // fences around it), bit 3 = causes found through that directory too (no
+  // binary search), bit 4 = the element loads issued before the collection
+  // starts come in
   constexpr uint32_t IT = PK / NT;
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -112,9 +116,23 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   uint32_t *SZ = reinterpret_cast<uint32_t *>(EFF + PK);
 
   const uint32_t pk = blockIdx.x, tid = threadIdx.x;
+  // the pack's node range from the host's pack table: the element loads go out
+  // first, in flight while the collection starts come in
   const uint32_t d0 = pack_doc0[pk], nd = pack_doc0[pk + 1] - d0;
-  const uint64_t s0 = coll_off[d0];
-  const uint32_t len = (uint32_t)(coll_off[d0 + nd] - s0);
+  const uint64_t s0 = pack_s0[pk];
+  const uint32_t len = (uint32_t)(pack_s0[pk + 1] - s0);
+  const bool early = mflags & 16;
+  uint64_t lc[IT], lid[IT];
+  uint8_t lcis[IT], lkd[IT];
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint32_t j = wb_elem<IT>(u);
+    const bool ok = early && j < len;
+    lc[u] = ok ? cause[s0 + j] : 0ull;
+    lid[u] = ok ? id_key[s0 + j] : 0ull;
+    lcis[u] = ok ? cause_is_id[s0 + j] : 0;
+    lkd[u] = ok ? kind[s0 + j] : 0;
+  }
   for (uint32_t i = tid; i <= nd; i += NT) dstart[i] = (uint32_t)(coll_off[d0 + i] - s0);
   for (uint32_t i = tid; i < nd; i += NT) dstat[i] = 0;
   if (tid < 2) s_or[tid] = 0;
@@ -138,13 +156,13 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         const uint32_t m = (lo + hi) >> 1;
         if (dstart[m] <= j) lo = m; else hi = m;
       }
-      const uint64_t c = cause[s0 + j];
-      const uint8_t cis = cause_is_id[s0 + j];
+      const uint64_t c = early ? lc[u] : cause[s0 + j];
+      const uint8_t cis = early ? lcis[u] : cause_is_id[s0 + j];
       const bool cid = cis == 1;
       B[j] = c;
       // 0x80: the cause is an id; 0x40: the cause is nil (cause_is_id = 2)
-      K8[j] = (uint8_t)((cid ? 0x80u : cis == 2 ? 0x40u : 0u) | (kind[s0 + j] & KIND_CLASS));
-      ck[u] = id_key[s0 + j];
+      K8[j] = (uint8_t)((cid ? 0x80u : cis == 2 ? 0x40u : 0u) | ((early ? lkd[u] : kind[s0 + j]) & KIND_CLASS));
+      ck[u] = early ? lid[u] : id_key[s0 + j];
       oid |= ck[u];
       oca |= cid ? c : 0ull;
       val[u] = j;
@@ -175,12 +193,14 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // pack-wide bitmap (P16 | Q | LQ, 1.5 PK words), an id's sorted position is
   // the number of set bits before it -- one atomicOr and one lookup a node
   // instead of the radix passes.  A repeated id (DUP) takes the sort.
-  constexpr uint32_t DIRW = 3 * PK / 2;
+  // The directory and its word prefixes (VS) stay for step 2, which then finds
+  // each id cause the same way instead of by binary search (DIRJOIN).
+  constexpr uint32_t DIRW = PK;
   const uint32_t lw = kbits > 5 ? kbits - 5 : 0;  // log2 of the words per collection
   bool sorted = false;
+  uint32_t *const dir = reinterpret_cast<uint32_t *>(P16);
+  uint16_t *const wpre = VS;
   if ((mflags & 1) && fits && ((uint64_t)nd << lw) <= DIRW) {
-    uint32_t *const dir = reinterpret_cast<uint32_t *>(P16);
-    uint16_t *const wpre = VS;  // (VS | I2J: 2 PK >= DIRW prefix counts)
     const uint32_t nwd = nd << lw;
     for (uint32_t w = tid; w < nwd; w += NT) dir[w] = 0;
     __syncthreads();
@@ -213,7 +233,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       for (uint32_t u = 0; u < IT; u++)
         if (wb_elem<IT>(u) < len) {
           A[pos[u]] = ck[u];
-          VS[pos[u]] = (uint16_t)val[u];
+          I2J[pos[u]] = (uint16_t)val[u];
         }
       __syncthreads();
 #pragma unroll
@@ -221,7 +241,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         const uint32_t j = wb_elem<IT>(u);
         if (j < len) {
           ck[u] = A[j];
-          val[u] = VS[j];
+          val[u] = I2J[j];
         }
       }
       __syncthreads();
@@ -241,26 +261,41 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   __syncthreads();
 
   stamp(0);
-  // 2. key and cause-in-weave of every node, in id order (map.cljc:31-37)
+  // 2. key and cause-in-weave of every node, in id order (map.cljc:31-37).
+  // With the directory of sort 1 still in P16 | Q | LQ (DIRJOIN), an id cause
+  // is a bit test and a popcount; P16 is written after a barrier then.
+  const bool djoin = sorted && (mflags & 8);
+  uint16_t pv[IT];
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t i = wb_elem<IT>(u);
+    pv[u] = 0;
     if (i >= len) continue;
     const uint32_t dl = (uint32_t)(ck[u] >> kbits), j = val[u];
     const uint64_t c = B[j];
     uint64_t key;
     uint16_t p;
     uint32_t st = 0;
-    if (K8[j] & 0x80u) {  // (spec/valid? ::s/id cause): the cause node by binary search
+    if (K8[j] & 0x80u) {  // (spec/valid? ::s/id cause): the cause node
       const uint32_t a1 = dstart[dl + 1];
-      const uint64_t want = ((uint64_t)dl << kbits) | c;
       const bool inrange = (c & ~imask) == 0;
-      uint32_t lo = dstart[dl], hi = a1;
-      while (inrange && lo < hi) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (A[m] < want) lo = m + 1; else hi = m;
+      uint32_t lo = dstart[dl];
+      bool found;
+      if (djoin) {
+        const uint32_t x = (uint32_t)c, w = (dl << lw) + (x >> 5);
+        const uint32_t dw = inrange ? dir[w] : 0u;
+        found = (dw >> (x & 31)) & 1u;
+        lo = found ? wpre[w] + __popc(dw & ((1u << (x & 31)) - 1)) : lo;
+      } else {  // binary search among the collection's sorted ids
+        const uint64_t want = ((uint64_t)dl << kbits) | c;
+        uint32_t hi = a1;
+        while (inrange && lo < hi) {
+          const uint32_t m = (lo + hi) >> 1;
+          if (A[m] < want) lo = m + 1; else hi = m;
+        }
+        found = inrange && lo < a1 && A[lo] == want;
       }
-      if (inrange && lo < a1 && A[lo] == want) {
+      if (found) {
         const uint32_t jc = I2J[lo];
         const uint64_t gc = B[jc];
         if (K8[jc] & 0x80u) {  // the cause node is id-caused: the key is that id (F8c)
@@ -288,11 +323,15 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       if (c > tmask) st |= CW_STATUS_MAP_KEY;
       p = MP_ROOT;
     }
-    P16[i] = p;
+    pv[u] = p;
     if (st) atomicOr(&dstat[dl], st);
     ck[u] = fits ? (((uint64_t)dl << (W + 2)) | key) : 0ull;
     val[u] = i;
   }
+  if (djoin) __syncthreads();  // (every directory lookup done before P16 is written)
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++)
+    if (wb_elem<IT>(u) < len) P16[wb_elem<IT>(u)] = pv[u];
   __syncthreads();
 
   stamp(1);
@@ -699,9 +738,14 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
     if (pc.ok) {
       uint32_t *dp = scratch_t<uint32_t>(c, "mp_doc0", pc.doc0.size());
       uint64_t *dof = scratch_t<uint64_t>(c, "mp_off", D + 1);
+      uint64_t *ds0 = scratch_t<uint64_t>(c, "mp_s0", pc.doc0.size());  // each pack's first node
       if (!dp || !dof) return fail(c, "out of device memory (map packs)");
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipMemcpy(dp, pc.doc0.data(), pc.doc0.size() * 4, hipMemcpyHostToDevice));
+      std::vector<uint64_t> s0(pc.doc0.size());
+      for (size_t k = 0; k < s0.size(); k++) s0[k] = off[pc.doc0[k]];
+      if (!ds0) return fail(c, "out of device memory (map packs)");
+      HIPCHK(c, hipMemcpy(ds0, s0.data(), s0.size() * 8, hipMemcpyHostToDevice));
       HIPCHK(c, hipMemcpy(dof, off, (D + 1) * 8, hipMemcpyHostToDevice));
     }
   }
@@ -739,6 +783,7 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
 #define CW_MAP_PACK_LAUNCH(PK_, NT_)                                                              \
   hipLaunchKernelGGL((k_map_pack<PK_, NT_>), dim3(P), dim3(NT_), 0, c->stream, id, cause, cis, kind, \
                      (const uint64_t *)c->bufs["mp_off"].p, (const uint32_t *)c->bufs["mp_doc0"].p, \
+                     (const uint64_t *)c->bufs["mp_s0"].p,                                             \
                      P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
                      sp, st, ctl, tprof, c->map_flags)
     if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
