@@ -51,6 +51,24 @@ using namespace cw;
 
 // Block-wide exclusive scan of one value per thread (blockDim.x = 64*W,
 // wtot has blockDim.x/64 entries).  NT = 0: block size taken at run time.
+// Last reads of a handoff and write-once outputs (CW_NT builds): non-temporal
+// accesses, so streams that are never read again do not push the lines that
+// will be (the tour's scattered records, the handoffs of the fused kernel) out
+// of the XCD's L2.
+#ifndef CW_NT
+#define CW_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ld_last(const T &x) {
+  if (CW_NT) return __builtin_nontemporal_load(&x);
+  return x;
+}
+template <typename T>
+__device__ __forceinline__ void st_last(T &x, T v) {
+  if (CW_NT) __builtin_nontemporal_store(v, &x);
+  else x = v;
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uint32_t *total) {
   const int nw = NT ? NT / 64 : (int)(blockDim.x >> 6);
@@ -1203,7 +1221,10 @@ __host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) 
 // when the document's ids leave the directory (big[0] counts it).  PT / VT:
 // the width of par / sval (u16 inside k_weave_doc: n < 2^16); skind may be
 // null (the tree reads the class bitmaps).
-template <int NT, typename PT = uint32_t, typename VT = uint32_t>
+// U1 / U2 / U3: items a thread keeps in flight in the directory, rank and
+// input-index passes (the fused kernel's front end is latency-bound: CW_FRONT_U)
+template <int NT, typename PT = uint32_t, typename VT = uint32_t, uint32_t U1 = 4, uint32_t U2 = 4,
+          uint32_t U3 = 4>
 __device__ __forceinline__ bool front_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
@@ -1244,16 +1265,15 @@ __device__ __forceinline__ bool front_doc(
   const uint64_t lim = (uint64_t)sg * FR_GROUP_BITS;
   uint64_t mx = 0;
   bool dup = false, far = false;
-  constexpr uint32_t U = 4;
-  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
-    uint64_t x[U];
+  for (uint32_t i0 = tid; i0 < n; i0 += U1 * NT) {
+    uint64_t x[U1];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U1; u++) {
       const uint32_t i = i0 + u * NT;
       x[u] = i < n ? lane_at(idD, i) : 0ull;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U1; u++) {
       if (i0 + u * NT >= n) continue;
       mx = max(mx, x[u]);
       if (x[u] >= lim) {
@@ -1302,30 +1322,30 @@ __device__ __forceinline__ bool front_doc(
   const uint64_t xend = (uint64_t)G * FR_GROUP_BITS;
   uint32_t st = 0;
   // the next group's loads are issued before this group is ranked
-  uint64_t qk[U], qc[U];
-  uint8_t qd[U];
+  uint64_t qk[U2], qc[U2];
+  uint8_t qd[U2];
   auto load_group = [&](uint32_t i0) {
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U2; u++) {
       const uint32_t i = i0 + u * NT;
-      qk[u] = i < n ? lane_at(idD, i) : 0ull;
-      qc[u] = i < n ? lane_at(causeD, i) : 0ull;
-      qd[u] = i < n ? lane_at(kindD, i) : 0;
+      qk[u] = i < n ? ld_last(lane_at(idD, i)) : 0ull;
+      qc[u] = i < n ? ld_last(lane_at(causeD, i)) : 0ull;
+      qd[u] = i < n ? ld_last(lane_at(kindD, i)) : 0;
     }
   };
   load_group(tid);
-  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
-    uint64_t k[U], c[U];
-    uint8_t kd[U];
+  for (uint32_t i0 = tid; i0 < n; i0 += U2 * NT) {
+    uint64_t k[U2], c[U2];
+    uint8_t kd[U2];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U2; u++) {
       k[u] = qk[u];
       c[u] = qc[u];
       kd[u] = qd[u];
     }
-    if (i0 + U * NT < n) load_group(i0 + U * NT);
+    if (i0 + U2 * NT < n) load_group(i0 + U2 * NT);
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U2; u++) {
       const uint32_t i = i0 + u * NT;
       if (i >= n) continue;
       bool pres;
@@ -1387,15 +1407,15 @@ __device__ __forceinline__ bool front_doc(
   stamp(2);
   // 3. the input index of every rank (the rank scratch was written by this
   // workgroup: one CU, one L1, lines not cached before; the barrier orders it)
-  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
-    uint32_t r[U];
+  for (uint32_t i0 = tid; i0 < n; i0 += U3 * NT) {
+    uint32_t r[U3];
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++) {
+    for (uint32_t u = 0; u < U3; u++) {
       const uint32_t i = i0 + u * NT;
-      r[u] = i < n ? lane_at(rankD, i) : 0xFFFFu;
+      r[u] = i < n ? ld_last(lane_at(rankD, i)) : 0xFFFFu;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < U; u++)
+    for (uint32_t u = 0; u < U3; u++)
       if (r[u] < n) p16[r[u]] = (uint16_t)(i0 + u * NT);
   }
   __syncthreads();
@@ -1870,7 +1890,7 @@ __device__ __forceinline__ void tree_l_doc(
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + wb_elem<IT>(k);
-      qpar[k] = r < n ? lane_at(parD, r) : 0u;
+      qpar[k] = r < n ? ld_last(lane_at(parD, r)) : 0u;
     }
   };
   // sweep 1: group keys, next siblings, last-child tables.  A group (effective
@@ -2117,8 +2137,8 @@ __device__ __forceinline__ void tree_l_doc(
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + k * NT + tid;
       const bool ok = r < n;
-      q.fs[k] = ok ? lane_at(fcSD, r) : 0u;
-      q.ns[k] = ok ? lane_at(nscD, r) : 0u;
+      q.fs[k] = ok ? ld_last(lane_at(fcSD, r)) : 0u;
+      q.ns[k] = ok ? ld_last(lane_at(nscD, r)) : 0u;
     }
   };
   // one tile: X holds its loads (and is refilled with tile r0 + 2 TILE_T)
@@ -2828,7 +2848,7 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT + lane;
-      L[k] = r < n ? lane_at(linkD, r) : 0u;
+      L[k] = r < n ? ld_last(lane_at(linkD, r)) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2924,8 +2944,8 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT;
-      lc[k] = r < n ? lane_at(locD, r) : 0u;
-      x[k] = r < n ? (sval ? lane_at(sval + base, r) : r) : 0u;
+      lc[k] = r < n ? ld_last(lane_at(locD, r)) : 0u;
+      x[k] = r < n ? (sval ? ld_last(lane_at(sval + base, r)) : r) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2944,7 +2964,7 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
   __syncthreads();
   stamp(3);
   uint32_t nvis = 0;
-  for (uint32_t g = tid; g < n; g += NT) lane_at(permD, g) = out[g];
+  for (uint32_t g = tid; g < n; g += NT) st_last(lane_at(permD, g), (uint32_t)out[g]);
   for (uint32_t w = tid; w < nw; w += NT) nvis += __popc(pvis[w]);
   if (vbits) {
     // the render bits straight into the batch's bitmap: global word W holds
@@ -3001,7 +3021,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 // there is one tail instead of three.  A document whose ids leave the front
 // end's directory counts itself in big[0] and stops: the host then weaves the
 // batch with the separate kernels.
-template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0>
+template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0, int FV = 0>
 __global__ __launch_bounds__(NT) void k_weave_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
@@ -3017,7 +3037,10 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   const uint32_t d = blockIdx.x;
   // (tprof, CW_TREE_PROF: the three phases' clocks per document)
   const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
-  if (!front_doc<NT, uint16_t, VT>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
+  // FV (CW_FRONT_U): items in flight per thread in the front end's directory
+  // and input-index passes (1: 16, 0: 4 as in k_front)
+  constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
+  if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, 0u, d,
                      reinterpret_cast<uint4 *>(lds_w)))
     return;
@@ -3751,7 +3774,7 @@ struct cw_ctx {
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
   uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
   uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
-  uint32_t tl_mode = 0;            // CW_TL_MODE: k_tree_l variant bits (A/B)
+  uint32_t tl_mode = 4;            // CW_TL_MODE: k_tree_l variant bits (A/B; 4 = direct list heads)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
@@ -3764,6 +3787,8 @@ struct cw_ctx {
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
+  uint32_t front_u = 1;            // CW_FRONT_U: k_weave_doc's front end keeps 16 ids a thread in
+                                   // flight in its directory and input-index passes (0: 4)
   uint32_t map_flags = 1 | 4 | 8 | 16;  // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
                                    // CW_MAP_RELAXED (bit 2), CW_MAP_DIRJOIN (bit 3), CW_MAP_EARLY (bit 4)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
@@ -4295,11 +4320,12 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       else tree_l_kernel(k_tree_l<TL_NT, 1024, P, M>);
     };
     auto tree_l_prof = [&](auto prof) {
-      switch (c->tl_mode & 3) {
+      switch (c->tl_mode) {
         case 0: tree_l_mode(prof, std::integral_constant<int, 0>()); break;
         case 1: tree_l_mode(prof, std::integral_constant<int, 1>()); break;
         case 2: tree_l_mode(prof, std::integral_constant<int, 2>()); break;
-        default: tree_l_mode(prof, std::integral_constant<int, 3>()); break;
+        case 3: tree_l_mode(prof, std::integral_constant<int, 3>()); break;
+        default: tree_l_mode(prof, std::integral_constant<int, 4>()); break;
       }
     };
     if (tree_l) {
@@ -4565,11 +4591,16 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              out->visible_count, loc, tprof_f);
         };
         if (tprof_f) {
-          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true>, sval);
-          else launch(k_weave_doc<1024, 2048, uint16_t, true>, sval16);
+          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true, 4>, sval);
+          else launch(k_weave_doc<1024, 2048, uint16_t, true, 4>, sval16);
         } else if (c->tl_mode == 4) {
-          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false, 4>, sval);
-          else launch(k_weave_doc<1024, 2048, uint16_t, false, 4>, sval16);
+          auto fv = [&](auto fvc) {
+            constexpr int F = decltype(fvc)::value;
+            if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, F>, sval);
+            else launch(k_weave_doc<1024, 2048, uint16_t, false, 4, F>, sval16);
+          };
+          if (c->front_u) fv(std::integral_constant<int, 1>());
+          else fv(std::integral_constant<int, 0>());
         } else {
           if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false>, sval);
           else launch(k_weave_doc<1024, 2048, uint16_t, false>, sval16);
@@ -5931,7 +5962,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_prof = knob("CW_TREE_PROF", 0);
   c->tree_pad = knob("CW_TREE_PAD", 0);
   c->tree_l = knob("CW_TREE_L", 2048);
-  c->tl_mode = knob("CW_TL_MODE", 0);
+  c->tl_mode = knob("CW_TL_MODE", 4);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
   c->front_eff = knob("CW_FRONT_EFF", 0);
@@ -5945,6 +5976,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->fused = knob("CW_FUSED", 1);
+  c->front_u = knob("CW_FRONT_U", 1);
   c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |
                  (knob("CW_MAP_RELAXED", 1) ? 4u : 0u) | (knob("CW_MAP_DIRJOIN", 1) ? 8u : 0u) |
                  (knob("CW_MAP_EARLY", 1) ? 16u : 0u);

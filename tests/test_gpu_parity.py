@@ -304,7 +304,8 @@ KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2C
          # raw parents from the front end (the tree climbs)
          {"CW_TREE_L": "0"}, {"CW_TREE_L": "0", "CW_TREE": "0"}, {"CW_TREE_L": "0", "CW_TREE": "1"},
          {"CW_TREE_L": "1024"},
-         {"CW_TL_MODE": "1"}, {"CW_TL_MODE": "2"}, {"CW_TL_MODE": "3"}, {"CW_FRONT_EFF": "1"}]
+         {"CW_TL_MODE": "0"}, {"CW_TL_MODE": "1"}, {"CW_TL_MODE": "2"}, {"CW_TL_MODE": "3"},
+         {"CW_TL_MODE": "0", "CW_FUSED": "0"}, {"CW_FRONT_EFF": "1"}]
 
 
 @pytest.mark.parametrize("n", [59_204, 60_000, 65_534, 65_535])
