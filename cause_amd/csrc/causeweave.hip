@@ -51,24 +51,6 @@ using namespace cw;
 
 // Block-wide exclusive scan of one value per thread (blockDim.x = 64*W,
 // wtot has blockDim.x/64 entries).  NT = 0: block size taken at run time.
-// Last reads of a handoff and write-once outputs (CW_NT builds): non-temporal
-// accesses, so streams that are never read again do not push the lines that
-// will be (the tour's scattered records, the handoffs of the fused kernel) out
-// of the XCD's L2.
-#ifndef CW_NT
-#define CW_NT 0
-#endif
-template <typename T>
-__device__ __forceinline__ T ld_last(const T &x) {
-  if (CW_NT) return __builtin_nontemporal_load(&x);
-  return x;
-}
-template <typename T>
-__device__ __forceinline__ void st_last(T &x, T v) {
-  if (CW_NT) __builtin_nontemporal_store(v, &x);
-  else x = v;
-}
-
 template <int NT>
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *wtot, uint32_t *total) {
   const int nw = NT ? NT / 64 : (int)(blockDim.x >> 6);
@@ -1328,9 +1310,9 @@ __device__ __forceinline__ bool front_doc(
 #pragma unroll
     for (uint32_t u = 0; u < U2; u++) {
       const uint32_t i = i0 + u * NT;
-      qk[u] = i < n ? ld_last(lane_at(idD, i)) : 0ull;
-      qc[u] = i < n ? ld_last(lane_at(causeD, i)) : 0ull;
-      qd[u] = i < n ? ld_last(lane_at(kindD, i)) : 0;
+      qk[u] = i < n ? lane_at(idD, i) : 0ull;
+      qc[u] = i < n ? lane_at(causeD, i) : 0ull;
+      qd[u] = i < n ? lane_at(kindD, i) : 0;
     }
   };
   load_group(tid);
@@ -1412,7 +1394,7 @@ __device__ __forceinline__ bool front_doc(
 #pragma unroll
     for (uint32_t u = 0; u < U3; u++) {
       const uint32_t i = i0 + u * NT;
-      r[u] = i < n ? ld_last(lane_at(rankD, i)) : 0xFFFFu;
+      r[u] = i < n ? lane_at(rankD, i) : 0xFFFFu;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U3; u++)
@@ -1890,7 +1872,7 @@ __device__ __forceinline__ void tree_l_doc(
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + wb_elem<IT>(k);
-      qpar[k] = r < n ? ld_last(lane_at(parD, r)) : 0u;
+      qpar[k] = r < n ? lane_at(parD, r) : 0u;
     }
   };
   // sweep 1: group keys, next siblings, last-child tables.  A group (effective
@@ -2137,8 +2119,8 @@ __device__ __forceinline__ void tree_l_doc(
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t r = r0 + k * NT + tid;
       const bool ok = r < n;
-      q.fs[k] = ok ? ld_last(lane_at(fcSD, r)) : 0u;
-      q.ns[k] = ok ? ld_last(lane_at(nscD, r)) : 0u;
+      q.fs[k] = ok ? lane_at(fcSD, r) : 0u;
+      q.ns[k] = ok ? lane_at(nscD, r) : 0u;
     }
   };
   // one tile: X holds its loads (and is refilled with tile r0 + 2 TILE_T)
@@ -2848,7 +2830,7 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT + lane;
-      L[k] = r < n ? ld_last(lane_at(linkD, r)) : 0u;
+      L[k] = r < n ? lane_at(linkD, r) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2944,8 +2926,8 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
       const uint32_t r = r0 + k * NT;
-      lc[k] = r < n ? ld_last(lane_at(locD, r)) : 0u;
-      x[k] = r < n ? (sval ? ld_last(lane_at(sval + base, r)) : r) : 0u;
+      lc[k] = r < n ? lane_at(locD, r) : 0u;
+      x[k] = r < n ? (sval ? lane_at(sval + base, r) : r) : 0u;
     }
 #pragma unroll
     for (uint32_t k = 0; k < LU; k++) {
@@ -2964,7 +2946,7 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
   __syncthreads();
   stamp(3);
   uint32_t nvis = 0;
-  for (uint32_t g = tid; g < n; g += NT) st_last(lane_at(permD, g), (uint32_t)out[g]);
+  for (uint32_t g = tid; g < n; g += NT) lane_at(permD, g) = out[g];
   for (uint32_t w = tid; w < nw; w += NT) nvis += __popc(pvis[w]);
   if (vbits) {
     // the render bits straight into the batch's bitmap: global word W holds
