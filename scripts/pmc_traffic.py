@@ -20,8 +20,8 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# k_tree_l is the library's "tree" stat, k_weave_doc its "weave"
-ALIAS = {"pack_bits": "packbits", "tree_l": "tree", "weave_doc": "weave"}
+# k_tree_l is the library's "tree" stat, k_weave_doc its "weave", k_map_pack its "m_pack"
+ALIAS = {"pack_bits": "packbits", "tree_l": "tree", "weave_doc": "weave", "map_pack": "m_pack"}
 
 
 def stat_name(sym):
