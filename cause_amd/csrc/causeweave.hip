@@ -795,10 +795,26 @@ __global__ __launch_bounds__(256) void k_gd_first(const uint64_t *__restrict__ s
 // gathered by input index (as k_join), the cause's rank from one directory
 // line instead of the bucket index and a search.
 constexpr int GJOIN_ITEMS = 4;
+// ckk (CW_GPACK): cause | kind << 56 in one word per input node (k_gpack), so
+// the gather by input index is one random line a node instead of two
+__global__ __launch_bounds__(256) void k_gpack(const uint64_t *__restrict__ cause_key,
+                                               const uint8_t *__restrict__ kind, uint32_t n,
+                                               uint64_t *__restrict__ ckk) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  // (a cause of 2^56 or more can be no id -- the ids fit 55 bits here -- so it
+  // packs as 2^56 - 1, which is above every id as well)
+  constexpr uint64_t M56 = (1ull << 56) - 1;
+  if (i < n) {
+    const uint64_t c = cause_key[i];
+    ckk[i] = (c < M56 ? c : M56) | ((uint64_t)kind[i] << 56);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey,
                                                const uint32_t *__restrict__ sval,
                                                const uint64_t *__restrict__ cause_key,
                                                const uint8_t *__restrict__ kind, uint32_t n,
+                                               const uint64_t *__restrict__ ckk,
                                                const uint4 *__restrict__ dir,
                                                uint32_t *__restrict__ par, uint8_t *__restrict__ skind,
                                                uint32_t *__restrict__ status) {
@@ -815,8 +831,14 @@ __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey
 #pragma unroll
   for (int k = 0; k < GJOIN_ITEMS; k++) {
     const uint32_t i = i0 + k * 256;
-    ck[k] = i < n ? cause_key[gi[k]] : 0ull;
-    kd[k] = i < n ? kind[gi[k]] : 0;
+    if (ckk) {
+      const uint64_t w = i < n ? ckk[gi[k]] : 0ull;
+      ck[k] = w & ((1ull << 56) - 1);
+      kd[k] = (uint8_t)(w >> 56);
+    } else {
+      ck[k] = i < n ? cause_key[gi[k]] : 0ull;
+      kd[k] = i < n ? kind[gi[k]] : 0;
+    }
   }
   uint32_t st = 0;
 #pragma unroll
@@ -3759,6 +3781,7 @@ struct cw_ctx {
   uint32_t tl_mode = 4;            // CW_TL_MODE: k_tree_l variant bits (A/B; 4 = direct list heads)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
+  uint32_t gpack = 0;              // CW_GPACK: ... gathering cause and kind as one packed word
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
@@ -4744,10 +4767,17 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            out->status);
       }
       if (check_launch(c, "index")) return -1;
+      // cause and kind packed in one word per input node when the ids leave
+      // 9 bits (the id sort's other key buffer is free by now)
+      uint64_t *ckk = c->gpack && key_bits <= 55 ? (skey == skA ? skB : skA) : nullptr;
+      if (ckk) {
+        Launch L(c, "gpack", (double)N * (8 + 1 + 8));
+        hipLaunchKernelGGL(k_gpack, dim3((N + 255) / 256), B256, 0, c->stream, cause_key, kind, N, ckk);
+      }
       {
         Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1) + (double)N * 64);
         hipLaunchKernelGGL(k_gjoin, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
-                           c->stream, skey, sval, cause_key, kind, N,
+                           c->stream, skey, sval, cause_key, kind, N, ckk,
                            reinterpret_cast<const uint4 *>(gdir), par, skind, out->status);
       }
       if (check_launch(c, "join")) return -1;
@@ -5947,6 +5977,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tl_mode = knob("CW_TL_MODE", 4);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
+  c->gpack = knob("CW_GPACK", 0);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
