@@ -3781,7 +3781,7 @@ struct cw_ctx {
   uint32_t tl_mode = 4;            // CW_TL_MODE: k_tree_l variant bits (A/B; 4 = direct list heads)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
-  uint32_t gpack = 0;              // CW_GPACK: ... gathering cause and kind as one packed word
+  uint32_t gpack = 1;              // CW_GPACK: ... gathering cause and kind as one packed word
   uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
@@ -5977,7 +5977,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tl_mode = knob("CW_TL_MODE", 4);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
-  c->gpack = knob("CW_GPACK", 0);
+  c->gpack = knob("CW_GPACK", 1);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
