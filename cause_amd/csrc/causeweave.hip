@@ -3806,11 +3806,13 @@ struct cw_ctx {
     std::vector<uint64_t> off;
     std::vector<uint32_t> doc0;
     uint32_t dbits = 0, pk = 0;
+    uint64_t maxcoll = 0;          // the largest collection of the cached layout
     bool ok = false;
     bool same = false;             // this call's coll_offsets equal off (set by cw_weave_maps)
   } mpack;
-  uint32_t map_pack = 0;           // CW_MAP_PACK: 0 = 2048 nodes / 512 threads, 1 = 1024 / 256,
-                                   // 2 = 2048 / 1024
+  uint32_t map_pack = 0;           // CW_MAP_PACK: 0 = the smallest pack that holds the largest
+                                   // collection (512 / 128 threads, 1024 / 256, else 2048 / 512),
+                                   // 1 = 1024 / 256, 2 = 2048 / 1024, 3 = 2048 / 512, 4 = 512 / 128
 };
 
 namespace {
@@ -5404,11 +5406,13 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
                   memcmp(c->mpack.off.data(), bt->coll_offsets, (D + 1) * 8) == 0;
   if (!c->mpack.same) {
     const uint64_t *o = bt->coll_offsets;
-    uint64_t back = 0, big = 0;
+    uint64_t back = 0, big = 0, mx = 0;
     for (uint64_t d = 0; d < D; d++) {  // branch-free: vectorizes
       back |= (uint64_t)(o[d + 1] < o[d]);
       big |= (uint64_t)(o[d + 1] - o[d] >= LINK_IDX - 1);
+      mx = std::max<uint64_t>(mx, o[d + 1] - o[d]);
     }
+    c->mpack.maxcoll = mx;
     if (back) return fail(c, "coll_offsets not monotone");
     if (big)
       for (uint64_t d = 0; d < D; d++)

@@ -716,7 +716,13 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
   const uint32_t N = (uint32_t)off[D];
   // pack table, cached while the collection layout repeats
   auto &pc = c->mpack;
-  const uint32_t PKN = c->map_pack == 1 ? 1024u : MPK;  // CW_MAP_PACK=1: packs of 1024 nodes
+  // pack size (CW_MAP_PACK): by default the smallest of 512 / 1024 / 2048
+  // nodes that holds the largest collection -- smaller packs are more
+  // workgroups a CU with cheaper barriers (config 4: 2048 nodes 3.77 ms,
+  // 1024 3.26, 512 3.15; 256 nodes / one wave: 3.95)
+  const uint64_t mc = pc.maxcoll;
+  const uint32_t PKN = c->map_pack == 1 ? 1024u : c->map_pack == 4 ? 512u
+                       : c->map_pack != 0 ? MPK : mc <= 512 ? 512u : mc <= 1024 ? 1024u : MPK;
   if (!(pc.pk == PKN && pc.same)) {
     pc.off.assign(off, off + D + 1);
     pc.pk = PKN;
@@ -786,7 +792,8 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
                      (const uint64_t *)c->bufs["mp_s0"].p,                                             \
                      P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
                      sp, st, ctl, tprof, c->map_flags)
-    if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
+    if (pc.pk == 512) CW_MAP_PACK_LAUNCH(512, 128);
+    else if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
     else if (c->map_pack == 2) CW_MAP_PACK_LAUNCH(2048, 1024);
     else CW_MAP_PACK_LAUNCH(2048, 512);
 #undef CW_MAP_PACK_LAUNCH
