@@ -3791,6 +3791,7 @@ struct cw_ctx {
                                    // go through the giant path document by document
   uint32_t front_fused = 1;        // CW_FRONT_FUSED: one-kernel front end (k_front)
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
+  uint32_t giant_log2k = 4;        // CW_GIANT_LOG2K: least splitter block of a giant document
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
   uint32_t front_u = 1;            // CW_FRONT_U: k_weave_doc's front end keeps 16 ids a thread in
                                    // flight in its directory and input-index passes (0: 4)
@@ -3984,6 +3985,9 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     // counter; 32-entry slots overflow ~8x less often (walk 2.8 -> 1.5 ms at
     // 6.7e7 nodes) for 8 more bytes a node, so below 2^30 nodes
     if (giant && n < (1u << 30)) log2cap = std::max(log2cap, 5u);
+    // and 16-node splitter blocks: half the sublists to rank for a slightly
+    // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8)
+    if (giant) log2k = std::max(log2k, c->giant_log2k);
     auto subl = [&]() {
       return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;
@@ -5992,6 +5996,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->giant_docs_max = knob("CW_GIANT_DOCS", 32);
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
+  c->giant_log2k = std::max(MIN_LOG2K, std::min(knob("CW_GIANT_LOG2K", 4), 12u));
   c->fused = knob("CW_FUSED", 1);
   c->front_u = knob("CW_FRONT_U", 1);
   c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |

@@ -420,6 +420,27 @@ def test_giant_path_shapes(giant_weaver):
                 method=oracle.METHOD_LINKED)
 
 
+@pytest.mark.parametrize("log2k", ["3", "5"])
+def test_giant_path_splitter_blocks(log2k, monkeypatch):
+    """The giant path under other splitter blocks than its default 16 nodes
+    (CW_GIANT_LOG2K): 8 (the round-2 geometry) and 32."""
+    monkeypatch.setenv("CW_GIANT_MIN", "0")
+    monkeypatch.setenv("CW_GIANT_LOG2K", log2k)
+    rng = random.Random(7)
+    with abi.Weaver(0) as w:
+        for steps, tx in ((2000, 0.0), (1500, 0.3)):
+            d = G.stress_history(rng, steps, tx_chain=tx)
+            rng.shuffle(d)
+            b = pack.pack_lists([d])
+            check_batch(w, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+        spec = dataclasses.replace(gen.CONFIG1, nodes_per_doc=200_000, n_sites=1, p_chain=1.0)
+        off, idk, ck, kd = gen.generate(spec, 0, 1)
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_LINKED)
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=1_000_000)
+        off, idk, ck, kd = gen.generate(spec, 0, 1)
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+
+
 def test_few_large_documents_per_document_giant_path():
     """A batch of a few large documents goes through the giant path one
     document at a time (render bits merged at unaligned offsets); a small one
