@@ -4021,8 +4021,10 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     // 6.7e7 nodes) for 8 more bytes a node, so below 2^30 nodes
     if (giant && n < (1u << 30)) log2cap = std::max(log2cap, 5u);
     // and 16-node splitter blocks: half the sublists to rank for a slightly
-    // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8)
-    if (giant) log2k = std::max(log2k, c->giant_log2k);
+    // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8),
+    // once there are walkers enough to fill the chip (config 1's 10^5 nodes:
+    // walk 0.044 -> 0.085 ms with 16)
+    if (giant && n >= (1u << 22)) log2k = std::max(log2k, c->giant_log2k);
     auto subl = [&]() {
       return (uint64_t)((n + (1u << log2k) - 1) >> log2k) +
              (uint64_t)((n + (1u << log2cap) - 1) >> log2cap) + 1;

@@ -423,7 +423,7 @@ def test_giant_path_shapes(giant_weaver):
 @pytest.mark.parametrize("log2k", ["3", "5"])
 def test_giant_path_splitter_blocks(log2k, monkeypatch):
     """The giant path under other splitter blocks than its default 16 nodes
-    (CW_GIANT_LOG2K): 8 (the round-2 geometry) and 32."""
+    (CW_GIANT_LOG2K, lists of >= 2^22 nodes): 8 (the round-2 geometry) and 32."""
     monkeypatch.setenv("CW_GIANT_MIN", "0")
     monkeypatch.setenv("CW_GIANT_LOG2K", log2k)
     rng = random.Random(7)
@@ -436,7 +436,8 @@ def test_giant_path_splitter_blocks(log2k, monkeypatch):
         spec = dataclasses.replace(gen.CONFIG1, nodes_per_doc=200_000, n_sites=1, p_chain=1.0)
         off, idk, ck, kd = gen.generate(spec, 0, 1)
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_LINKED)
-        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=1_000_000)
+        # (the knob applies from 2^22 nodes: smaller lists keep 8-node blocks)
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 1000)
         off, idk, ck, kd = gen.generate(spec, 0, 1)
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
 
