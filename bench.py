@@ -374,7 +374,8 @@ def main_giant_dist(a, world, rank, local, dist, torch, dev):
     if res is not None and res.status not in (None, 0):
         raise SystemExit(f"status {res.status}")
     if a.check and res is not None:
-        check_giant_dist(res, idk, ck, kd, world, rank, dist, N, ruling and a.out == "sharded")
+        with heartbeat("--check against the oracle"):
+            check_giant_dist(res, idk, ck, kd, world, rank, dist, N, ruling and a.out == "sharded")
     w.reset_kernel_stats()
     w.set_profiling(True)
     dist.barrier()
@@ -482,7 +483,8 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     traffic, tnote = pmc_traffic(name, "config4", a.colls == 1_000_000)
     check = None
     if a.check:
-        bad = check_maps(off, idk, ck, ci, kd, o, S)
+        with heartbeat("--check against the oracle"):
+            bad = check_maps(off, idk, ck, ci, kd, o, S)
         tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
         check = {"collections_checked": tot[1], "mismatches": tot[0],
                  "against": "literal c.map/weave fold + active-node (oracle, C)"}
@@ -616,7 +618,8 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                 bad[0] += 0 if ok else 1
             bad[1] += b1 - b0
 
-        s.run(nb, fill, consume_check)
+        with heartbeat("--check against the oracle"):
+            s.run(nb, fill, consume_check)
         tot = shard.reduce_sum(bad, dist, dev) if world > 1 else bad
         check = {"documents_checked": tot[1], "mismatches": tot[0],
                  "against": "effective-tree preorder + visibility (oracle, C)"}
@@ -811,9 +814,51 @@ def main():
     dt_max = shard.reduce_max_time(dt, dist, dev) if world > 1 else dt
     total_nodes = N * world * a.steps
     value = total_nodes / dt_max
+    # the full reconstitute path (s/refresh-caches, shared.cljc:259-266: spin ->
+    # refresh-ts -> weave-fn): the same steps with the yarns (yarn_perm, the id
+    # order partitioned by site) asked for as well; `value` stays the weave's
+    refresh = None
+    if a.config in (2, 5) and not k32:
+        yarn = torch.empty(N, dtype=torch.int32, device=dev)
+        outs_y = dict(outs, yarn_perm=yarn.data_ptr())
+
+        def step_y():
+            call(off, g_id.data_ptr(), g_ca.data_ptr(), g_kd.data_ptr(), layout, outs_y)
+
+        step_y()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step_y()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dty = time.perf_counter() - t0
+        dty = shard.reduce_max_time(dty, dist, dev) if world > 1 else dty
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        for _ in range(a.steps):
+            step_y()
+        torch.cuda.synchronize()
+        w.set_profiling(False)
+        ys = w.kernel_stats()
+        yk = {k: v for k, v in ys.items() if k not in stats or k.startswith("yarn")}
+        refresh = {"value": total_nodes / dty, "unit": "nodes/s", "ms_per_step": dty / a.steps * 1e3,
+                   "note": "the weave step plus the yarns (yarn_perm: spin's id order partitioned "
+                           "by site) and ::lamport-ts: s/refresh-caches in full",
+                   "kernels_ms_per_step": {k: round(v[1] / a.steps, 4) for k, v in
+                                           sorted(ys.items(), key=lambda kv: -kv[1][1])},
+                   "yarn_kernels": {k: {"ms_per_step": round(v[1] / a.steps, 4),
+                                        "alg_bytes_per_step": v[2] / a.steps,
+                                        "achieved_gbs": round(v[2] / (v[1] / 1e3) / 1e9, 1)
+                                        if v[1] > 0 else None} for k, v in yk.items()}}
+        del yarn
     check = None
     if a.check:
-        bad = check_lists(off, *_k64(idk, ck), kd, perm, bits, vcount, status)
+        with heartbeat("--check against the oracle"):
+            bad = check_lists(off, *_k64(idk, ck), kd, perm, bits, vcount, status)
         tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
         check = {"documents_checked": tot[1], "mismatches": tot[0],
                  "against": "effective-tree preorder + visibility (oracle, C)"}
@@ -862,8 +907,9 @@ def main():
     if rank == 0:
         cpu = None
         if not a.no_cpu:  # after the GPU region, on rank 0 at every N
-            cpu = (cpu_baseline_prefix(*_k64(idk, ck), kd, 100_000) if a.config == 5 else
-                   cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64))
+            with heartbeat("cpu_baseline"):
+                cpu = (cpu_baseline_prefix(*_k64(idk, ck), kd, 100_000) if a.config == 5 else
+                       cpu_baseline(spec, a.cpu_seconds, max_docs=1 if a.config == 1 else 64))
         line = {
             "metric": "nodes woven/sec (whole node) + % of HBM roofline at 1/2/4/8 MI355X",
             "value": value, "unit": "nodes/s", "n_gpus": world, "steps": a.steps,
@@ -896,8 +942,11 @@ def main():
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]
         if check:
             line["check"] = check
+        if refresh:
+            line["refresh_caches"] = refresh
         if not a.no_cpu and a.config == 2:
-            par = cpu_baseline_parallel(spec)
+            with heartbeat("cpu_baseline_parallel"):
+                par = cpu_baseline_parallel(spec)
             line["cpu_baseline_parallel"] = par
             line["speedup_vs_cpu_parallel"] = value / par["value"]
         print(json.dumps(line), flush=True)

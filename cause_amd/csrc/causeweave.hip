@@ -850,11 +850,14 @@ __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey
                                                const uint64_t *__restrict__ cause_key,
                                                const uint8_t *__restrict__ kind, uint32_t n,
                                                const uint64_t *__restrict__ ckk,
-                                               const uint4 *__restrict__ dir,
+                                               const uint4 *__restrict__ dir, uint64_t E,
                                                uint32_t *__restrict__ par, uint8_t *__restrict__ skind,
                                                uint32_t *__restrict__ status) {
   const uint32_t i0 = blockIdx.x * (256 * GJOIN_ITEMS) + threadIdx.x;
-  const uint64_t kmax = skey[n - 1];
+  // causes are looked up only up to the largest id the directory holds: ids
+  // past its E entries (a key_bits too small for the batch) were flagged
+  // INTERNAL by k_gd_set_sorted and must not be read
+  const uint64_t kmax = min(skey[n - 1], E * GD_KEYS - 1);
   uint32_t gi[GJOIN_ITEMS];
   uint64_t ck[GJOIN_ITEMS];
   uint8_t kd[GJOIN_ITEMS];
@@ -2614,9 +2617,13 @@ __global__ __launch_bounds__(256) void k_lvl_walk(const uint32_t *__restrict__ c
                                                   uint32_t *__restrict__ pb, uint32_t *__restrict__ sa,
                                                   uint32_t *__restrict__ sb,
                                                   uint32_t *__restrict__ snext,
-                                                  uint32_t *__restrict__ status) {
+                                                  uint32_t *__restrict__ status,
+                                                  const uint32_t *__restrict__ dyn, uint32_t Wstat) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= S) return;
+  // Wall is the capacity; with dyn the walkers in use are the static ones plus
+  // those the walk added, so a link into the unused range is caught
+  if (dyn) Wall = min(Wstat + dyn[0], Wall);
   uint32_t x = q * K, acc = 0, cnt = 0, nq = NX_END;
   for (uint32_t steps = 0; steps <= Wall; steps++) {
     sup[x] = q;
@@ -3833,7 +3840,8 @@ struct cw_ctx {
   uint32_t map_flags = 1 | 4 | 8 | 16;  // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
                                    // CW_MAP_RELAXED (bit 2), CW_MAP_DIRJOIN (bit 3), CW_MAP_EARLY (bit 4)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
-  uint32_t x_iters = 0;            // synthetic-list iterations of the last exact path (exact.hip)
+  uint32_t x_iters = 0;            // synthetic-list weaves of the last exact path (exact.hip)
+  uint32_t xfold = 0;              // CW_XFOLD: documents with an early node take the serial fold
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
   hipEvent_t ev_status = nullptr;  // ... and recorded there (exact.hip waits on it, not the stream)
   bool x_pending = false;          // pin_status / ev_status hold this call's giant document
@@ -4494,10 +4502,11 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       {
         Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
         hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
-                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status);
+                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status,
+                           dyn_ctr, W);
         if (three) {
           hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
-                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status);
+                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status, nullptr, 0u);
           hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
                              sn3, S3, N, Weff, nb3, tb3, out->status, nullptr, dyn_ctr, W, Wcap);
           hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
@@ -4609,9 +4618,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t tl_lds = tree_l_lds_bytes(t.nmax) + tree_l_tile_bytes(1024, 2048);
       const uint32_t to_lds = tour_lds_bytes(t.nmax, t.tour_log2k);
       const uint32_t wd_lds = std::max(fr_lds, std::max(tl_lds, to_lds));
+      // (the fused kernel is built for the tree variants 0 and 4 only: another
+      // CW_TL_MODE runs the separate kernels, so the knob means the same thing
+      // on both paths; CW_TREE_PROF runs variant 4)
       fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 && !c->tree_pad &&
-                   !c->front_eff && tl_lds + 64 * 4 + 4 <= c->lds_max && wd_lds + 1024 <= c->lds_max &&
-                   to_lds <= TOUR_LDS_MAX;
+                   !c->front_eff && (c->tl_mode == 0 || c->tl_mode == 4) &&
+                   (!c->tree_prof || c->tl_mode == 4) && tl_lds + 64 * 4 + 4 <= c->lds_max &&
+                   wd_lds + 1024 <= c->lds_max && to_lds <= TOUR_LDS_MAX;
       if (fused_done) {
         uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *thr = scratch_t<uint32_t>(c, "thr", N);
         uint32_t *loc = scratch_t<uint32_t>(c, "tour_loc", N);
@@ -4821,7 +4834,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1) + (double)N * 64);
         hipLaunchKernelGGL(k_gjoin, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
                            c->stream, skey, sval, cause_key, kind, N, ckk,
-                           reinterpret_cast<const uint4 *>(gdir), par, skind, out->status);
+                           reinterpret_cast<const uint4 *>(gdir), E, par, skind, out->status);
       }
       if (check_launch(c, "join")) return -1;
     } else {
@@ -4858,16 +4871,27 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       HIPCHK(c, hipEventRecord(c->ev_status, c->stream));
       c->x_pending = true;
     }
+    // A large list the front end flagged for the exact path (exact.hip, which
+    // rewrites every output of it) skips the fast path's tree, tour and yarns:
+    // one wait for the status copy, worth it above 2^22 nodes (the tail of
+    // 6.7e7 nodes is ~9 ms; config 1's 1e5 nodes keep the call sync-free).
+    bool flagged = false;
+    if (c->x_pending && N >= (1u << 22) && bt->key_bits && bt->key_bits < 64) {
+      HIPCHK(c, hipEventSynchronize(c->ev_status));
+      const uint32_t st = c->pin_status[0];
+      flagged = (st & (CW_STATUS_ROOT | CW_STATUS_ORPHAN | CW_STATUS_NON_LAMPORT)) &&
+                !(st & (CW_STATUS_DUP | CW_STATUS_KEY_RANGE | CW_STATUS_INTERNAL));
+    }
     // without yarns the id-sort buffers are free once the ids are joined
     const bool spare = !want_yarns;
-    if (!fused_done &&
+    if (!fused_done && !flagged &&
         weave_tail(c, D, N, is_giant(c, D, bt->doc_offsets), par, skind, sval, kbm,
                    front_done ? nullptr : skey, bt->ts_shift, out, spare ? skA : nullptr,
                    spare ? skB : nullptr))
       return -1;
 
     // 10. yarns: stable partition of the id order by site rank
-    if (want_yarns) {
+    if (want_yarns && !flagged) {
       uint64_t *yk;
       uint32_t *yv;
       uint64_t *ykA = skey == skA ? skB : skA;
@@ -6035,6 +6059,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->giant_log2k = std::max(MIN_LOG2K, std::min(knob("CW_GIANT_LOG2K", 4), 12u));
   c->fused = knob("CW_FUSED", 1);
+  c->xfold = knob("CW_XFOLD", 0);
   c->front_u = knob("CW_FRONT_U", 1);
   c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |
                  (knob("CW_MAP_RELAXED", 1) ? 4u : 0u) | (knob("CW_MAP_DIRJOIN", 1) ? 8u : 0u) |

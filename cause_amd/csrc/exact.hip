@@ -7,7 +7,9 @@
 // assumes none of this: c.list/weave folds s/weave-node over (sort ::nodes)
 // (list.cljc:26-28, shared.cljc:225-241) whatever the causes are.  Documents
 // with status ORPHAN, NON_LAMPORT or ROOT (and no DUP: ::nodes is a map, so the
-// reference never sees a repeated id) are rewoven here by that fold.
+// reference never sees a repeated id) are rewoven here, data-parallel, with
+// the fold's result for every such document (tests/exact_model.py is the CPU
+// model of this rule, checked against the literal fold on corrupted histories).
 //
 // The fold, restated for a full reweave.  Nodes arrive in ascending id order,
 // so every node nr already in the weave has a smaller id than the incoming m:
@@ -16,63 +18,74 @@
 //   * clause A (:208-212) is special(nr) & cause(nr) != id(m) & !special(m);
 //   * weave-asap? (:194-200) first holds at the split right after cause(m), at
 //     split 0 when cause(m) is nil ((first nil) = nil), or right before a node
-//     already woven whose cause is m (only when that node's id is smaller than
-//     its cause's: a non-Lamport cause);
+//     already woven whose cause is m (a node with a smaller id than its cause:
+//     a non-Lamport cause; m is then an "early" node);
 //   * from that split m skips the nodes A holds for; if weave-asap? never holds
-//     (an absent cause, or one with a larger id that is not woven yet) the loop
-//     runs to the (empty? right) branch (:236-237) and m is appended.
-// So one sequential pass per document over a linked list gives the literal
-// result: O(n + skips) plus, for each node that has an earlier-id child, a walk
-// from the head (O(n) each).  That serial fold (k_xfold, one lane per document,
-// ~1 us a node) is kept only for documents with such a non-Lamport cause, up to
-// XFOLD_MAX nodes; larger ones get CW_STATUS_UNWOVEN.
+//     (an absent cause, or one that is not older, and no older child) the loop
+//     runs to the (empty? right) branch (:236-237): m is APPENDED.
 //
-// Every other flagged document (absent causes, nil causes, no root or several,
-// a root that is not the smallest id) is woven data-parallel.  With every cause
-// present and older, or nil, or absent:
-//   * a nil cause puts the node at the split before the first node: it is a
-//     child of a virtual head H (rank 0 of a synthetic list, the document's
-//     rank r becomes r + 1);
-//   * an absent cause appends the node at the end of the weave of the nodes
-//     older than it.  Appending m is the same as weaving m under the node that
-//     is last at that moment, T(m) (nothing follows it, so the skip of clause A
-//     finds nothing either), and no later step of the fold reads m's cause
-//     (clause A compares cause(nr) with the incoming id, never equal; asap
-//     reads the incoming node's own cause).  The fold only inserts, so the
-//     weave at time m is the final weave restricted to the older nodes:
-//     T(m) = the older node with the largest final position (H if none);
-//   * with every orphan attached under its T(m) the list is in the fast path's
-//     domain (effective-tree preorder), and render bits are F6's
-//     with one change: an attached orphan hide does not hide its new parent
-//     (hide? compares the real cause), so it weaves as an h.show (still
-//     special).  Roots (KIND_ROOT, nil cause) are weaved as normal nodes under H
-//     and rendered hidden.
-// T(m) depends on the final weave, so the attachments are found by iteration:
-// start with T(m) = the previous rank, weave the synthetic lists (weave_tail,
-// the fast path's tree and tour: no sort), recompute every T(m) as a prefix
-// arg-max of positions over the id order, repeat until no attachment changes.
-// The fixed point is the fold's result (by induction over the orphans in id
-// order: with the older orphans attached right, the weave restricted to the
-// nodes older than m is the fold's, so the recomputed T(m) is right), and
-// iteration k has the k oldest orphans right, so it ends within (orphans + 1)
-// weaves -- in practice 2 for a document with one orphan.  Tested against
-// the literal fold on corrupted histories (tests/test_gpu_exact.py).
+// Phase 1 -- synthetic lists (every flagged document).  A synthetic list is
+// the document's ranks behind a virtual head H (rank r = synthetic r + 1, H
+// = 0), woven by the fast path's tree and tour (weave_tail: parents in, no
+// sort).  An appended node m is the same as a node woven under T(m), the node
+// last in the weave at that moment (nothing follows it, so clause A's skip
+// finds nothing, and no later step reads m's cause).  T(m) is found without
+// iterating over the appended nodes (round 3 placed one per weave):
+//   * everything woven after an appended node o stays in the region o opens
+//     (o is last; a later node lands after o only through o's own subtree, or,
+//     for a special o, through the special run o ends), so T of the next
+//     appended node o' is the last node older than o' in that region, which
+//     does not depend on where o itself went;
+//   * o non-special: the region is o's subtree of the effective tree (F5);
+//   * o special: o hides nothing (hide? compares the real cause: it renders
+//     like an h.show) and ends the special run of N, the nearest non-special
+//     ancestor of T(o).  The oldest non-special node y in (o, o') whose
+//     effective parent is N opens the next region (y's subtree); without one,
+//     the region is o's own special run;
+//   * all of this is read off ONE weave of a static forest in which every
+//     appended node hangs under H as a non-special root (k_xsyn_build): "the
+//     last node < o' in [pos(s), end(s))" and "end(s) = the first later
+//     position holding an older node" are two searches in a min-tree over the
+//     synthetic index at each position (mt_first_after / mt_last_before).
+//     Regions after a non-special node resolve in parallel (k_xres1); a run of
+//     special appended nodes is followed in order by one wave (k_xres2).
+// A second weave with every appended node under its T(m) is the fold's result
+// for every document without an early node; render bits are F6's, roots
+// hidden.
+//
+// Phase 2 -- documents with an early node.  The fold is the preorder of its
+// insertion tree: each node's parent is the node right before its insertion
+// point at its time, children by descending id.  From any weave W, k_xpred
+// finds every node's insertion point in W restricted to the older nodes (the
+// scan above, with searches in min-trees), the insertion tree is woven (all
+// classes normal: a plain preorder), and the rounds repeat until the weave no
+// longer changes.  A weave that reproduces itself is the fold's (by induction
+// over the nodes in id order), and each round fixes at least the oldest
+// misplaced node; from phase 1's weave a few rounds suffice (the appended
+// nodes after round 1 use the region rule above on the insertion tree, where
+// a subtree ends at the first older node).  Render bits then come from the
+// weave itself (hide? against the next node).
+//
+// The literal fold on one lane per document (k_xfold, ~1 us a node) is kept
+// as a cross-check behind CW_XFOLD=1.
 
 constexpr uint32_t X_NIL = 0xFFFFFFFEu;  // cause is nil (the root's, shared.cljc:22-23)
 constexpr uint32_t X_END = 0xFFFFFFFFu;  // no cause in the document / end of the list
 constexpr uint32_t X_HEAD = 0xFFFFFFFDu; // the split before the first node
 constexpr uint32_t X_MASK = CW_STATUS_ROOT | CW_STATUS_ORPHAN | CW_STATUS_NON_LAMPORT;
-// not a ::nodes map of the reference (a repeated id) or not a K64 key
-constexpr uint32_t X_SKIP = CW_STATUS_DUP | CW_STATUS_KEY_RANGE;
-constexpr uint32_t XFOLD_MAX = 1u << 22;     // the serial fold's largest document (nodes)
-// Routing of the documents without a non-Lamport cause: the synthetic lists
-// take at most (orphans + 1) iterations, so documents with few orphans, or
-// too large for the serial fold, go there; others take the serial fold.
-constexpr uint32_t XSYN_FEW = 32;            // orphans: always the synthetic lists
-constexpr uint32_t XSYN_MAX_ORPH = 1024;     // orphans: a document above XFOLD_MAX with more
-                                             // is left CW_STATUS_UNWOVEN
+// not a ::nodes map of the reference (a repeated id), not a K64 key, or a
+// batch the pipeline found inconsistent (ids wider than the declared key_bits)
+constexpr uint32_t X_SKIP = CW_STATUS_DUP | CW_STATUS_KEY_RANGE | CW_STATUS_INTERNAL;
+constexpr uint32_t XFOLD_MAX = 1u << 22;     // CW_XFOLD: the serial fold's largest document
 constexpr uint32_t X_NONE = 0xFFFFFFFFu;     // not on the synthetic path
-constexpr unsigned long long X_HEADKEY = 0xFFFFFFFFull;  // (position 0 << 32) | H
+constexpr uint32_t MT_MAX = 0xFFFFFFFFu;     // min-tree padding ("no node")
+
+// A node weave-asap? never holds for: its cause is absent, or not older than
+// it (c = its cause's rank, or X_NIL / X_END).  (An early node among these is
+// appended in phase 1 and placed by phase 2.)
+__device__ __forceinline__ bool x_appended(uint32_t c, uint32_t r, uint32_t n) {
+  return c == X_END || (c < n && c >= r);
+}
 
 // Documents the exact path takes: non-empty, flagged by the domain checks, no
 // repeated id.
@@ -118,8 +131,9 @@ __global__ __launch_bounds__(256) void k_xgather(
 }
 
 // Cause rank of every node in id order (X_NIL for a nil cause, X_END when the
-// cause is not an id of the document), its kind by rank, and early[c] = 1 for
-// every node c that has a child with a smaller id (weave-asap?'s second test).
+// cause is not an id of the document), its kind by rank, early[c] = 1 for
+// every node c that has a child with a smaller id (weave-asap?'s second test),
+// per document "has an early node" and its number of appended nodes.
 __global__ __launch_bounds__(256) void k_xjoin(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint64_t *__restrict__ skey,
@@ -147,7 +161,7 @@ __global__ __launch_bounds__(256) void k_xjoin(
       early[base + p] = 1;
       doc_early[f] = 1;
     }
-    if (p == X_END) atomicAdd(&doc_orph[f], 1u);  // (orphans are few: rarely contended)
+    if (x_appended(p, r, n)) atomicAdd(&doc_orph[f], 1u);  // (appended nodes are few)
   }
 }
 
@@ -170,7 +184,7 @@ __global__ __launch_bounds__(256) void k_xranked_prep(const uint32_t *__restrict
     early[p] = 1;
     *doc_early = 1;
   }
-  if (p == X_END) atomicAdd(doc_orph, 1u);
+  if (x_appended(p, r, n)) atomicAdd(doc_orph, 1u);
 }
 
 // Visible bits [g0, g0 + 32) of one weave word: the bits of this document
@@ -286,13 +300,109 @@ __global__ __launch_bounds__(256) void k_xscatter(
     dst[i + shift] = src[i];
 }
 
-// --- the synthetic lists (documents without a non-Lamport cause) ------------
-// Sub-batch index i = doc_off[f] + r (rank r of flagged document f); the
-// synthetic list of f starts at sbase[f] (X_NONE: f takes the serial fold):
-// sbase[f] = H, sbase[f] + 1 + r = rank r.
+// --- min-trees over a synthetic weave -----------------------------------------
+// Level 0 = an array over synthetic positions (padded with MT_MAX to a multiple
+// of 16), level l + 1 = the minimum of each 16 entries of level l (padded too),
+// up to a level of 16 entries.  Blocks of 16 are 64-byte aligned: a block is
+// four 16-byte loads.
 
-// Build: synthetic parent rank and kind of every rank (orphans attached under
-// the previous rank to start), H at rank 0.
+constexpr uint32_t MT_LEVELS = 10;
+struct XMinTree {
+  const uint32_t *lv[MT_LEVELS];
+  uint32_t len[MT_LEVELS];
+  uint32_t levels;
+};
+
+// Bit k set: entry k of the 16-entry block at b is < v.
+__device__ __forceinline__ uint32_t mt_mask16(const uint32_t *b, uint32_t v) {
+  const uint4 *b4 = reinterpret_cast<const uint4 *>(b);
+  const uint4 x = b4[0], y = b4[1], z = b4[2], w = b4[3];
+  return (x.x < v) | (x.y < v) << 1 | (x.z < v) << 2 | (x.w < v) << 3 | (y.x < v) << 4 |
+         (y.y < v) << 5 | (y.z < v) << 6 | (y.w < v) << 7 | (z.x < v) << 8 | (z.y < v) << 9 |
+         (z.z < v) << 10 | (z.w < v) << 11 | (w.x < v) << 12 | (w.y < v) << 13 | (w.z < v) << 14 |
+         (w.w < v) << 15;
+}
+
+// The first position q > p whose entry is < v; t.len[0] if none.
+__device__ uint32_t mt_first_after(const XMinTree &t, uint32_t p, uint32_t v) {
+  uint32_t i = p + 1;
+  for (uint32_t l = 0; l < t.levels; l++) {
+    if (i >= t.len[l]) break;
+    const uint32_t b0 = i & ~15u;
+    const uint32_t m = mt_mask16(t.lv[l] + b0, v) & (0xFFFFu << (i & 15u));
+    if (m) {
+      uint32_t j = b0 + (uint32_t)__builtin_ctz(m);
+      while (l > 0) {  // a block's minimum < v: one of its 16 entries is
+        l--;
+        j = 16 * j + (uint32_t)__builtin_ctz(mt_mask16(t.lv[l] + 16 * j, v));
+      }
+      return j;
+    }
+    i = (i >> 4) + 1;
+  }
+  return t.len[0];
+}
+
+// The last position q < h whose entry is < v; MT_MAX if none.
+__device__ uint32_t mt_last_before(const XMinTree &t, uint32_t h, uint32_t v) {
+  if (h == 0) return MT_MAX;
+  uint32_t i = min(h, t.len[0]) - 1;
+  for (uint32_t l = 0; l < t.levels; l++) {
+    const uint32_t b0 = i & ~15u;
+    const uint32_t m = mt_mask16(t.lv[l] + b0, v) & (0xFFFFu >> (15u - (i & 15u)));
+    if (m) {
+      uint32_t j = b0 + 31u - (uint32_t)__builtin_clz(m);
+      while (l > 0) {
+        l--;
+        j = 16 * j + 31u - (uint32_t)__builtin_clz(mt_mask16(t.lv[l] + 16 * j, v));
+      }
+      return j;
+    }
+    if (b0 == 0) break;
+    i = (i >> 4) - 1;
+  }
+  return MT_MAX;
+}
+
+// The minimum entry of positions [a, b) (MT_MAX when empty): the fringes of
+// each level entry by entry, the whole blocks between them one level up.
+__device__ uint32_t mt_range_min(const XMinTree &t, uint32_t a, uint32_t b) {
+  uint32_t m = MT_MAX;
+  for (uint32_t l = 0; l < t.levels && a < b; l++) {
+    const uint32_t al = min(b, (a + 15u) & ~15u), br = max(al, b & ~15u);
+    for (uint32_t i = a; i < al; i++) m = min(m, t.lv[l][i]);
+    for (uint32_t i = br; i < b; i++) m = min(m, t.lv[l][i]);
+    a = al >> 4;
+    b = br >> 4;
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_mt_level(const uint32_t *__restrict__ in,
+                                                  uint32_t in_len, uint32_t *__restrict__ out,
+                                                  uint32_t out_len) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= out_len) return;
+  uint32_t m = MT_MAX;
+  if (16 * j < in_len) {
+    const uint4 *b4 = reinterpret_cast<const uint4 *>(in + 16 * j);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 x = b4[k];
+      m = min(m, min(min(x.x, x.y), min(x.z, x.w)));
+    }
+  }
+  out[j] = m;
+}
+
+// --- phase 1: the static forest -----------------------------------------------
+// Sub-batch index i = doc_off[f] + r (rank r of flagged document f); the
+// synthetic list of f starts at sbase[f] (X_NONE: f is not on this path):
+// sbase[f] = H, sbase[f] + 1 + r = rank r.  Synthetic parents are local
+// (0 = H); "global synthetic indices" sbase[f] + s grow with f.
+
+// Parents and kinds of the static forest: an appended node under H as a
+// non-special root, a nil cause under H, every other node under its cause.
 __global__ __launch_bounds__(256) void k_xsyn_build(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
@@ -305,13 +415,11 @@ __global__ __launch_bounds__(256) void k_xsyn_build(
     const uint32_t r = i - base, p = xpar[i];
     uint8_t k = xk[i] & KIND_CLASS;
     uint32_t sp;
-    if (p < n) {
-      sp = p + 1;  // a present, older cause
-    } else if (p == X_NIL) {
-      sp = 0;      // a nil cause: under H
-    } else {       // an absent cause: under the synthetic rank r (= rank r - 1, or H)
-      sp = r;
-      if (k == KIND_HIDE || k == KIND_HHIDE) k = 3;  // hides nothing: renders like an h.show
+    if (x_appended(p, r, n)) {
+      sp = 0;
+      k = 0;
+    } else {
+      sp = p == X_NIL ? 0 : p + 1;
     }
     spar[sb + 1 + r] = sp;
     skd[sb + 1 + r] = k;
@@ -322,158 +430,440 @@ __global__ __launch_bounds__(256) void k_xsyn_build(
   }
 }
 
-// Positions: pos[i] = weave position (>= 1) of rank i's synthetic rank.  A tile
-// of the sub-batch stands for the same range of positions (q = 0 .. n-1 is
-// synthetic position q + 1).
-__global__ __launch_bounds__(256) void k_xsyn_pos(
+// Positions of a woven synthetic list: G[x] = the global synthetic index at
+// global position x, pos[g] = the position of g.  AUX[x] (mode 0, the static
+// forest) = 0 where the node is structurally non-special, else G[x] -- "the
+// first later position < s" then ends a special run; (mode 1, phase 2) =
+// G[x] where the node is non-special, else MT_MAX.  posold != nullptr: count
+// the positions that changed (phase 2's fixed point).
+__global__ __launch_bounds__(256) void k_xs_pos(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ wperm, uint32_t *__restrict__ pos, uint32_t *__restrict__ bad) {
+    const uint8_t *__restrict__ only, const uint32_t *__restrict__ wperm,
+    const uint8_t *__restrict__ skd, const uint8_t *__restrict__ xk, uint32_t mode,
+    uint32_t *__restrict__ G, uint32_t *__restrict__ AUX, uint32_t *__restrict__ pos,
+    const uint32_t *__restrict__ posold, uint32_t *__restrict__ ctl) {
   const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
-  if (sb == X_NONE) return;
+  if (sb == X_NONE || (only && !only[f])) return;
   const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+  uint32_t changed = 0;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t q = i - base, s = wperm[sb + 1 + q];
-    if (s >= 1 && s <= n) pos[base + s - 1] = q + 1;
-    else atomicOr(bad, 1u);  // H is always first: a position 1.. that holds it is an error
+    const uint32_t q = i - base, x = sb + 1 + q, s = wperm[x];
+    if (q == 0) {
+      G[sb] = sb;
+      pos[sb] = sb;
+      AUX[sb] = mode == 0 ? 0u : sb;
+    }
+    if (s < 1 || s > n) {
+      atomicOr(&ctl[1], 1u);  // H is always first: a later position that holds it is an error
+      continue;
+    }
+    const uint32_t g = sb + s;
+    G[x] = g;
+    if (posold && posold[g] != x) changed++;
+    pos[g] = x;
+    const bool ns = mode == 0 ? (skd[g] & KIND_CLASS) == 0 : (xk[base + s - 1] & KIND_CLASS) == 0;
+    AUX[x] = mode == 0 ? (ns ? 0u : g) : (ns ? g : MT_MAX);
+  }
+  if (posold) {
+    for (int o = 32; o > 0; o >>= 1) changed += __shfl_xor(changed, o, 64);
+    if ((threadIdx.x & 63) == 0 && changed) atomicAdd(&ctl[0], changed);
   }
 }
 
-// Largest (position << 32 | rank) of each tile.
-__global__ __launch_bounds__(256) void k_xsyn_tmax(
+// ctop[g] = the first of g and its static ancestors that is non-special
+// (structurally: an appended node counts as non-special), or H: a special
+// node's nearest non-special ancestor, and the effective parent of a
+// non-special child of g.
+__global__ __launch_bounds__(256) void k_xctop(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ pos, unsigned long long *__restrict__ tmax) {
-  __shared__ unsigned long long wm[4];
+    const uint32_t *__restrict__ spar, const uint8_t *__restrict__ skd, uint32_t *__restrict__ ctop) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
+  if (sb == X_NONE) return;
+  const uint32_t base = doc_off[f];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base;
+    uint32_t s = r + 1;
+    while (s != 0 && (skd[sb + s] & KIND_CLASS)) s = spar[sb + s];
+    ctop[sb + 1 + r] = sb + s;
+    if (r == 0) ctop[sb] = sb;
+  }
+}
+
+// The appended nodes of every synthetic document in id order: count per tile,
+// scan over tiles, write in order.
+__global__ __launch_bounds__(256) void k_xapp_count(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ xpar, uint32_t *__restrict__ tcnt) {
+  __shared__ uint32_t ws[4];
+  const uint32_t t = blockIdx.x, f = tile_doc[t];
+  uint32_t c = 0;
+  if (sbase[f] != X_NONE) {
+    const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+    for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x)
+      c += x_appended(xpar[i], i - base, n) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[t] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Exclusive scan of T tile counts in place (one workgroup of 1024).
+__global__ __launch_bounds__(1024) void k_xapp_scan(uint32_t *__restrict__ tcnt, uint32_t T) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < T; c0 += 1024) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint32_t v = t < T ? tcnt[t] : 0;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (uint32_t w = 0; w < wv; w++) pre += wsum[w];
+    if (t < T) tcnt[t] = pre + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + inc;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_xapp_scatter(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ xpar, const uint32_t *__restrict__ toff,
+    uint32_t *__restrict__ app_list, uint32_t *__restrict__ app_doc, uint32_t *__restrict__ app_idx) {
+  __shared__ uint32_t ws[4];
   const uint32_t t = blockIdx.x, f = tile_doc[t];
   if (sbase[f] == X_NONE) return;
-  const uint32_t base = doc_off[f];
-  unsigned long long m = 0;
-  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x)
-    m = max(m, ((unsigned long long)pos[i] << 32) | (i - base));
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) tmax[t] = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
-}
-
-// Per document (one block): tcar[t] = the largest key of the ranks before tile t
-// (H's key before the first).
-__global__ __launch_bounds__(256) void k_xsyn_tcarry(const uint32_t *__restrict__ tile_first,
-                                                     const uint32_t *__restrict__ sbase,
-                                                     const unsigned long long *__restrict__ tmax,
-                                                     unsigned long long *__restrict__ tcar) {
-  __shared__ unsigned long long wm[4];
-  const uint32_t f = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (sbase[f] == X_NONE) return;
-  const uint32_t t0 = tile_first[f], t1 = tile_first[f + 1];
-  unsigned long long carry = X_HEADKEY;
-  for (uint32_t c0 = t0; c0 < t1; c0 += 256) {
-    const uint32_t t = c0 + threadIdx.x;
-    const unsigned long long v = t < t1 ? tmax[t] : 0ull;
-    unsigned long long inc = v;  // inclusive max scan inside the wave
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long y = __shfl_up(inc, o, 64);
-      if (lane >= (uint32_t)o) inc = max(inc, y);
-    }
-    if (lane == 63) wm[wv] = inc;
-    __syncthreads();
-    unsigned long long pre = carry;
-    for (uint32_t w = 0; w < wv; w++) pre = max(pre, wm[w]);
-    const unsigned long long up = __shfl_up(inc, 1, 64);
-    const unsigned long long exc = max(pre, lane ? up : 0ull);
-    if (t < t1) tcar[t] = exc;
-    const unsigned long long total = max(max(wm[0], wm[1]), max(wm[2], wm[3]));
-    __syncthreads();
-    carry = max(carry, total);
-  }
-}
-
-// At every orphan rank r: T = the rank with the largest position among ranks
-// < r (H if none); its synthetic parent becomes T's synthetic rank.  Each
-// thread runs over a contiguous piece of the tile with the exclusive prefix of
-// the pieces before it.  Counts the attachments that change.
-__global__ __launch_bounds__(256) void k_xsyn_apply(
-    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
-    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ xpar, const uint32_t *__restrict__ pos,
-    const unsigned long long *__restrict__ tcar, uint32_t *__restrict__ spar,
-    uint32_t *__restrict__ changed, uint8_t *__restrict__ doc_changed) {
-  __shared__ unsigned long long wm[4];
-  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
-  if (sb == X_NONE) return;
   const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
-  const uint32_t s = tile_start[t], e = tile_start[t + 1], len = e - s;
-  const uint32_t per = (len + 255) / 256;
-  const uint32_t j0 = min(e, s + threadIdx.x * per), j1 = min(e, j0 + per);
-  unsigned long long m = 0;
-  for (uint32_t i = j0; i < j1; i++) m = max(m, ((unsigned long long)pos[i] << 32) | (i - base));
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  unsigned long long inc = m;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc = max(inc, y);
+  uint32_t k0 = toff[t];
+  for (uint32_t c0 = tile_start[t]; c0 < tile_start[t + 1]; c0 += 256) {
+    const uint32_t i = c0 + threadIdx.x;
+    const bool a = i < tile_start[t + 1] && x_appended(xpar[i], i - base, n);
+    const uint64_t b = __ballot(a);
+    if (lane == 0) ws[wv] = (uint32_t)__popcll(b);
+    __syncthreads();
+    uint32_t pre = k0;
+    for (uint32_t w = 0; w < wv; w++) pre += ws[w];
+    if (a) {
+      const uint32_t k = pre + lanes_below(b);
+      app_list[k] = i;
+      app_doc[k] = f;
+      if (app_idx) app_idx[i] = k;
+    }
+    k0 += ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
   }
-  if (lane == 63) wm[wv] = inc;
+}
+
+// Regions after a non-special node (or H): T of every appended node whose
+// previous appended node (in id order, same document) is non-special or H.
+// Tsyn[k] = the global synthetic index of T; Nof[o] = N for a special o.
+__global__ __launch_bounds__(256) void k_xres1(
+    const uint32_t *__restrict__ app_list, const uint32_t *__restrict__ app_doc, uint32_t A,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint8_t *__restrict__ xk, const uint32_t *__restrict__ pos, const uint32_t *__restrict__ G,
+    const uint32_t *__restrict__ ctop, XMinTree mt, uint32_t *__restrict__ Tsyn,
+    uint32_t *__restrict__ Nof, uint32_t *__restrict__ ctl) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= A) return;
+  const uint32_t i = app_list[k], f = app_doc[k], sb = sbase[f], base = doc_off[f];
+  const uint32_t o = sb + 1 + (i - base);
+  uint32_t prev = sb;
+  if (k > 0 && app_doc[k - 1] == f) {
+    const uint32_t ip = app_list[k - 1];
+    if (xk[ip] & KIND_CLASS) return;  // after a special appended node: k_xres2
+    prev = sb + 1 + (ip - base);
+  }
+  const uint32_t e = mt_first_after(mt, pos[prev], prev);
+  const uint32_t q = mt_last_before(mt, e, o);
+  if (q == MT_MAX || q < pos[prev]) {  // prev itself is older than o: never
+    atomicOr(&ctl[1], 2u);
+    return;
+  }
+  const uint32_t T = G[q];
+  Tsyn[k] = T;
+  if (xk[i] & KIND_CLASS) Nof[o] = ctop[T];
+}
+
+// The smallest non-special child of s in the static forest with an id in
+// (lo, hi), MT_MAX if none.  s's non-special children follow its special
+// children's (all-special) subtrees in descending id order, and every node of
+// a child's subtree is younger than the child: with the first child at or
+// below lo at position qs, the wanted child is the minimum over [s0, qs).
+__device__ uint32_t x_child_between(const XMinTree &mt, const XMinTree &mtx,
+                                    const uint32_t *__restrict__ pos, uint32_t s, uint32_t lo,
+                                    uint32_t hi) {
+  const uint32_t p = pos[s];
+  const uint32_t e = mt_first_after(mt, p, s);   // the end of s's subtree
+  const uint32_t s0 = mt_first_after(mtx, p, s);  // its first non-special child (or e)
+  if (s0 >= e) return MT_MAX;
+  const uint32_t qs = min(e, mt_first_after(mt, s0 - 1, lo + 1));
+  if (qs <= s0) return MT_MAX;
+  const uint32_t y = mt_range_min(mt, s0, qs);
+  return y < hi ? y : MT_MAX;
+}
+
+constexpr uint32_t XRUN_MAX = 64;  // special appended nodes a wave keeps (N, node) for
+
+// Runs of special appended nodes, in order, one wave each: the wave that
+// starts at entry k (its previous appended node is special and was resolved
+// by k_xres1) follows the run.  The next region's y is N's oldest non-special
+// child between the two appended nodes, or the oldest non-special child of a
+// special appended node of the run with the same N (a node caused through it
+// climbs to N): both by x_child_between, one lane per candidate parent.  With
+// N = H (H also holds the appended roots) or a run longer than XRUN_MAX, the
+// ranks between are scanned instead.
+__global__ __launch_bounds__(64) void k_xres2(
+    const uint32_t *__restrict__ app_list, const uint32_t *__restrict__ app_doc, uint32_t A,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ xpar, const uint8_t *__restrict__ xk,
+    const uint32_t *__restrict__ pos, const uint32_t *__restrict__ G,
+    const uint32_t *__restrict__ ctop, XMinTree mt, XMinTree mtx, uint32_t *__restrict__ Tsyn,
+    uint32_t *__restrict__ Nof, uint32_t *__restrict__ ctl) {
+  __shared__ uint32_t runO[XRUN_MAX], runN[XRUN_MAX];
+  uint32_t k = blockIdx.x;
+  const uint32_t lane = threadIdx.x;
+  if (k == 0 || k >= A) return;
+  const uint32_t f = app_doc[k];
+  if (app_doc[k - 1] != f || !(xk[app_list[k - 1]] & KIND_CLASS)) return;  // not after a special
+  // the run starts here when the previous one was resolved by k_xres1
+  if (k >= 2 && app_doc[k - 2] == f && (xk[app_list[k - 2]] & KIND_CLASS)) return;
+  const uint32_t sb = sbase[f], base = doc_off[f], n = doc_off[f + 1] - base;
+  // every lane follows the run with the same values; N stays in registers
+  uint32_t N = Nof[sb + 1 + (app_list[k - 1] - base)];
+  uint32_t nrun = 0;
+  if (lane == 0) {
+    runO[0] = sb + 1 + (app_list[k - 1] - base);
+    runN[0] = N;
+  }
+  nrun = 1;
   __syncthreads();
-  unsigned long long run = tcar[t];
-  for (uint32_t w = 0; w < wv; w++) run = max(run, wm[w]);
-  const unsigned long long up = __shfl_up(inc, 1, 64);
-  run = max(run, lane ? up : 0ull);
-  uint32_t ch = 0;
-  for (uint32_t i = j0; i < j1; i++) {
-    const uint32_t p = xpar[i];
-    if (!(p < n) && p != X_NIL) {  // an orphan: under the last node older than it
-      const uint32_t T = (uint32_t)run;
-      const uint32_t want = T == 0xFFFFFFFFu ? 0u : T + 1;
-      uint32_t *slot = &spar[sb + 1 + (i - base)];
-      if (*slot != want) {
-        *slot = want;
-        ch++;
+  for (; k < A && app_doc[k] == f; k++) {
+    const uint32_t ip = app_list[k - 1], i = app_list[k];
+    const uint32_t rp = ip - base, ro = i - base;
+    const uint32_t prev = sb + 1 + rp, o = sb + 1 + ro;
+    // y: the oldest non-special node between them whose effective parent is N
+    uint32_t y = MT_MAX;
+    if (N != sb && nrun <= XRUN_MAX) {
+      uint32_t c = lane == 0 ? x_child_between(mt, mtx, pos, N, prev, o) : MT_MAX;
+      for (uint32_t j = lane; j < nrun; j += 64)
+        if (runN[j] == N) c = min(c, x_child_between(mt, mtx, pos, runO[j], prev, o));
+      for (int s2 = 32; s2 > 0; s2 >>= 1) c = min(c, (uint32_t)__shfl_xor(c, s2, 64));
+      y = c;
+    } else {
+      for (uint32_t y0 = rp + 1; y0 < ro && y == MT_MAX; y0 += 64) {
+        const uint32_t r = y0 + lane;
+        bool hit = false;
+        if (r < ro && !(xk[base + r] & KIND_CLASS)) {
+          const uint32_t cz = xpar[base + r];
+          if (!x_appended(cz, r, n)) {
+            uint32_t e = cz == X_NIL ? sb : ctop[sb + 1 + cz];
+            if (e != sb) {  // through a special appended node of this run: its N
+              const uint32_t er = e - sb - 1;
+              if ((xk[base + er] & KIND_CLASS) && x_appended(xpar[base + er], er, n))
+                e = __hip_atomic_load(&Nof[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            hit = e == N;
+          }
+        }
+        const uint64_t b = __ballot(hit);
+        if (b) y = sb + 1 + y0 + (uint32_t)__builtin_ctzll(b);
       }
     }
-    run = max(run, ((unsigned long long)pos[i] << 32) | (i - base));
+    uint32_t q, lo;
+    bool in_run;
+    if (y != MT_MAX) {
+      lo = pos[y];
+      q = mt_last_before(mt, mt_first_after(mt, lo, y), o);
+      in_run = false;
+    } else {
+      lo = pos[prev];
+      q = mt_last_before(mt, mt_first_after(mtx, lo, prev), o);
+      in_run = true;
+    }
+    if (q == MT_MAX || q < lo) {
+      if (lane == 0) atomicOr(&ctl[1], 4u);
+      return;
+    }
+    const uint32_t T = G[q];
+    const bool sp = (xk[i] & KIND_CLASS) != 0;
+    if (sp) N = in_run ? N : ctop[T];
+    if (lane == 0) {
+      Tsyn[k] = T;
+      if (sp) {
+        __hip_atomic_store(&Nof[o], N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nrun < XRUN_MAX) {
+          runO[nrun] = o;
+          runN[nrun] = N;
+        }
+      }
+    }
+    if (!sp) break;  // the run ends
+    nrun++;  // (past XRUN_MAX: the scan from here on)
+    __syncthreads();
   }
-  if (ch) {
-    atomicAdd(changed, ch);
-    doc_changed[f] = 1;
+}
+
+// Every appended node under its T; an appended hide hides nothing (hide?
+// compares the real cause), so it weaves like an h.show.
+__global__ __launch_bounds__(256) void k_xsyn_final(
+    const uint32_t *__restrict__ app_list, const uint32_t *__restrict__ app_doc, uint32_t A,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint8_t *__restrict__ xk, const uint32_t *__restrict__ Tsyn, uint32_t *__restrict__ spar,
+    uint8_t *__restrict__ skd) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= A) return;
+  const uint32_t i = app_list[k], f = app_doc[k], sb = sbase[f];
+  const uint32_t o = sb + 1 + (i - doc_off[f]);
+  const uint8_t c = xk[i] & KIND_CLASS;
+  spar[o] = Tsyn[k] - sb;
+  skd[o] = c == KIND_HIDE || c == KIND_HHIDE ? 3 : c;
+}
+
+// --- phase 2: insertion-tree rounds ------------------------------------------
+
+// xf[c] = the smallest position of an older child of c (weave-asap?'s second
+// test), MT_MAX when none.
+__global__ __launch_bounds__(256) void k_xf(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint8_t *__restrict__ only, const uint32_t *__restrict__ xpar,
+    const uint32_t *__restrict__ pos, uint32_t *__restrict__ xf) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
+  if (sb == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base, p = xpar[i];
+    if (p < n && p > r) atomicMin(&xf[base + p], pos[sb + 1 + r]);
+  }
+}
+
+// Each node's insertion-tree parent from the weave W (G, pos; mt over G, mtn
+// over G of the non-special nodes): weave-node's scan on W restricted to the
+// older nodes.  first: W is phase 1's weave (an appended node goes after the
+// last older node of the whole weave; later rounds use its region).
+__global__ __launch_bounds__(256) void k_xpred(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint8_t *__restrict__ only, const uint32_t *__restrict__ xpar,
+    const uint8_t *__restrict__ xk, const uint8_t *__restrict__ early,
+    const uint32_t *__restrict__ xf, const uint32_t *__restrict__ app_list,
+    const uint32_t *__restrict__ app_idx, const uint32_t *__restrict__ pos,
+    const uint32_t *__restrict__ G, XMinTree mt, XMinTree mtn, uint32_t first,
+    uint32_t *__restrict__ spar, uint8_t *__restrict__ skd, uint32_t *__restrict__ ctl) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
+  if (sb == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base, p = xpar[i], m = sb + 1 + r;
+    const bool sp = (xk[i] & KIND_CLASS) != 0;
+    const uint32_t x1 = xf[i];
+    const uint32_t cp = p == X_NIL ? sb : (p < r ? pos[sb + 1 + p] : MT_MAX);
+    uint32_t pred;
+    if (cp == MT_MAX && x1 == MT_MAX) {  // appended
+      uint32_t e = sb + n + 1, lo = sb;
+      if (!first) {
+        // the region of the previous appended node (not an early one)
+        uint32_t prev = sb;
+        for (uint32_t k = app_idx[i]; k-- > 0;) {
+          const uint32_t ip = app_list[k];
+          if (ip < base) break;
+          if (!early[ip]) {
+            prev = sb + 1 + (ip - base);
+            break;
+          }
+        }
+        lo = pos[prev];
+        e = mt_first_after(mt, lo, prev);
+      }
+      const uint32_t q = mt_last_before(mt, e, m);
+      pred = q == MT_MAX || q < lo ? MT_MAX : G[q];
+    } else if (cp != MT_MAX && cp < x1) {  // right after the cause, then clause A's skip
+      if (sp) {
+        pred = p == X_NIL ? sb : sb + 1 + p;
+      } else {
+        const uint32_t stop = min(mt_first_after(mtn, cp, m), x1);
+        const uint32_t q = mt_last_before(mt, stop, m);
+        pred = q == MT_MAX || q < cp ? MT_MAX : G[q];
+      }
+    } else {  // right before the older child woven first
+      const uint32_t q = mt_last_before(mt, x1, m);
+      pred = q == MT_MAX || q < sb ? MT_MAX : G[q];
+    }
+    if (pred == MT_MAX || pred >= m) {
+      atomicOr(&ctl[1], 8u);
+      pred = sb;
+    }
+    spar[m] = pred - sb;
+    skd[m] = 0;
   }
 }
 
 // The woven synthetic lists -> the caller's outputs: weave_perm (input index per
-// position, H dropped), rendered bits (the synthetic render bit, roots hidden)
-// and rendered counts.  The tile of the sub-batch stands for the same range of
-// output positions q; one thread per output word.
+// position, H dropped), rendered bits and rendered counts.  adj = 0: the
+// documents with only[f] == 0 (or all, only == nullptr), render bits of the
+// synthetic F5 weave with roots hidden; adj = 1: the documents with only[f],
+// hide? (list.cljc:48-55) against the next node of the weave itself.  The tile
+// of the sub-batch stands for the same range of output positions q; one thread
+// per output word.
 __global__ __launch_bounds__(256) void k_xsyn_emit(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
-    const uint32_t *__restrict__ wperm, const uint32_t *__restrict__ wbits,
-    const uint8_t *__restrict__ xk, const uint32_t *__restrict__ sval,
+    const uint8_t *__restrict__ only, uint32_t adj, const uint32_t *__restrict__ wperm,
+    const uint32_t *__restrict__ wbits, const uint8_t *__restrict__ xk,
+    const uint32_t *__restrict__ xpar, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ out_off, const uint32_t *__restrict__ out_doc,
     uint32_t *__restrict__ weave_perm, uint32_t *__restrict__ visible_bits,
     uint32_t *__restrict__ visible_count) {
   __shared__ uint32_t wsum[4];
   const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
-  if (sb == X_NONE) return;
-  const uint32_t base = doc_off[f];
+  if (sb == X_NONE || (only ? only[f] != 0 : false) != (adj != 0)) return;
+  const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
   const uint32_t q0 = tile_start[t] - base, q1 = tile_start[t + 1] - base;
   const uint64_t g0 = out_off[f];
-  // output words touching [g0 + q0, g0 + q1)
-  const uint64_t W0 = (g0 + q0) >> 5, W1 = (g0 + q1 - 1) >> 5;
+  // one position a lane, waves over 64-aligned output positions: each wave's
+  // bits are two output words (x_flush merges the words a document shares)
+  const uint32_t lane = threadIdx.x & 63;
   uint32_t cnt = 0;
-  for (uint64_t W = W0 + threadIdx.x; W <= W1; W += blockDim.x) {
-    const uint64_t lo = max(W << 5, g0 + q0), hi = min((W << 5) + 32, g0 + q1);
-    uint32_t acc = 0, mask = 0;
-    for (uint64_t g = lo; g < hi; g++) {
+  const uint64_t a0 = (g0 + q0) & ~63ull;
+  for (uint64_t ga = a0 + (threadIdx.x & ~63u); ga < g0 + q1; ga += blockDim.x) {
+    const uint64_t g = ga + lane;
+    const bool in = g >= g0 + q0 && g < g0 + q1;
+    bool vis = false;
+    if (in) {
       const uint32_t q = (uint32_t)(g - g0), x = sb + 1 + q;  // synthetic position
       const uint32_t i = base + wperm[x] - 1;
       weave_perm[g] = sval ? sval[i] : i - base;
-      const bool vis = ((wbits[x >> 5] >> (x & 31)) & 1u) && !(xk[i] & KIND_ROOT);
-      mask |= 1u << (g & 31);
-      if (vis) acc |= 1u << (g & 31);
-      cnt += vis ? 1u : 0u;
+      const uint8_t k = xk[i];
+      if (adj) {
+        vis = !(k & (KIND_CLASS | KIND_ROOT));
+        if (vis && q + 1 < n) {
+          const uint32_t j = base + wperm[x + 1] - 1;
+          vis = !(is_hide(xk[j]) && xpar[j] == i - base);
+        }
+      } else {
+        vis = ((wbits[x >> 5] >> (x & 31)) & 1u) && !(k & KIND_ROOT);
+      }
     }
-    if (visible_bits) x_flush(visible_bits, W, mask, acc);
+    const uint64_t m = __ballot(in), v = __ballot(vis);
+    cnt += vis ? 1u : 0u;
+    if (visible_bits && (lane == 0 || lane == 32)) {
+      const uint32_t sh = lane;
+      const uint32_t mw = (uint32_t)(m >> sh);
+      if (mw) x_flush(visible_bits, (ga >> 5) + (lane >> 5), mw, (uint32_t)(v >> sh));
+    }
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
   if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
@@ -488,13 +878,6 @@ __global__ __launch_bounds__(64) void k_xsyn_zero(const uint32_t *__restrict__ s
   if (f < F && sbase[f] != X_NONE) visible_count[out_doc[f]] = 0;
 }
 
-__global__ __launch_bounds__(64) void k_xunwoven(const uint8_t *__restrict__ mark, uint32_t F,
-                                                 const uint32_t *__restrict__ out_doc,
-                                                 uint32_t *__restrict__ status) {
-  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < F && mark[f]) status[out_doc[f]] |= CW_STATUS_UNWOVEN;
-}
-
 namespace {
 
 // Upload a host array to named scratch (blocking copy: the stream is idle).
@@ -507,15 +890,39 @@ T *x_upload(cw_ctx *c, const char *name, const std::vector<T> &h) {
   return d;
 }
 
+// The upper levels of a min-tree over a (len entries, a multiple of 16,
+// padded with MT_MAX) into scratch `name`.
+int mt_build(cw_ctx *c, const char *name, const uint32_t *a, uint64_t len, XMinTree *t) {
+  std::vector<uint64_t> lens{len};
+  while (lens.back() > 16) lens.push_back(((lens.back() / 16) + 15) & ~15ull);
+  if (lens.size() > MT_LEVELS || len >= 0xFFFFFFFFull) return fail(c, "exact path: min-tree of %llu", (unsigned long long)len);
+  uint64_t tot = 16;
+  for (size_t l = 1; l < lens.size(); l++) tot += lens[l];
+  uint32_t *up = scratch_t<uint32_t>(c, name, tot);
+  if (!up) return fail(c, "out of device memory (%s)", name);
+  t->levels = (uint32_t)lens.size();
+  t->lv[0] = a;
+  t->len[0] = (uint32_t)len;
+  for (size_t l = 1; l < lens.size(); l++) {
+    t->lv[l] = up;
+    t->len[l] = (uint32_t)lens[l];
+    hipLaunchKernelGGL(k_mt_level, dim3((uint32_t)((lens[l] + 255) / 256)), dim3(256), 0, c->stream,
+                       t->lv[l - 1], t->len[l - 1], up, t->len[l]);
+    up += lens[l];
+  }
+  return check_launch(c, "mt_level");
+}
+
 // The flagged documents after the join (xpar: cause rank / X_NIL / X_END by
 // rank, xk: kinds by rank, early: "has an older child" by rank, sval: input
-// index by rank or nullptr; dearly / dorph: per document "has a non-Lamport
-// cause" and its number of orphans): each document to the synthetic lists,
-// the serial fold or CW_STATUS_UNWOVEN, and its outputs written at out_off.
+// index by rank or nullptr; dearly / dapp: per document "has an early node"
+// and its number of appended nodes): every document woven by the synthetic
+// lists (phase 1, and phase 2 rounds for one with an early node), outputs
+// written at out_off.
 int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff,
                         const uint32_t *xpar, const uint8_t *xk, const uint8_t *early,
                         const uint32_t *sval, const uint64_t *d_oof, const uint32_t *d_odoc,
-                        const uint8_t *dearly, const uint32_t *dorph, cw_list_result *out) {
+                        const uint8_t *dearly, const uint32_t *dapp, cw_list_result *out) {
   const uint32_t NX = (uint32_t)xoff.back();
   if (ensure_tables(c, F, xoff.data())) return -1;
   uint32_t *tile_start = dev_tab(c, "t_tile_start"), *tile_doc = dev_tab(c, "t_tile_doc"),
@@ -523,76 +930,77 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
   const dim3 B256(256), GF((F + 63) / 64), B64(64);
   const uint32_t T = c->tab.T;
   if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
-  // which documents take the serial fold (a non-Lamport cause), which the
-  // synthetic lists
-  std::vector<uint8_t> h_early(F), run(F, 0), unwoven(F, 0);
-  std::vector<uint32_t> h_orph(F);
+  std::vector<uint8_t> h_early(F), run(F, 0), x2(F, 0);
+  std::vector<uint32_t> h_app(F);
   HIPCHK(c, hipMemcpyAsync(h_early.data(), dearly, F, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(h_orph.data(), dorph, (size_t)F * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(h_app.data(), dapp, (size_t)F * 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  uint32_t orph_max = 0;
+  // synthetic lists: documents without an early node, documents with one
+  // (phase 2 reweaves only those), then each giant document on its own
   struct Group {
-    bool giant;
+    bool giant, early;
     uint64_t base;  // first synthetic index (a multiple of 32: its bits start a word)
     std::vector<uint64_t> off;
   };
   std::vector<Group> groups;
   std::vector<uint32_t> sb(F, X_NONE);
-  uint64_t NS = 0;
-  bool any_serial = false;
+  uint64_t NS = 0, A = 0;
+  bool any_serial = false, any_x2 = false;
   {
-    Group batch{false, 0, {0}};
-    std::vector<uint32_t> big;
+    std::vector<uint32_t> small[2], big;
     for (uint32_t f = 0; f < F; f++) {
       const uint64_t n = xoff[f + 1] - xoff[f];
-      const bool small = n <= XFOLD_MAX;
-      if (h_early[f] || (small && h_orph[f] > XSYN_FEW) || (!small && h_orph[f] > XSYN_MAX_ORPH)) {
-        (small ? run : unwoven)[f] = 1;
-        any_serial |= small;
+      if (c->xfold && h_early[f] && n <= XFOLD_MAX) {  // CW_XFOLD: the serial fold (cross-check)
+        run[f] = 1;
+        any_serial = true;
         continue;
       }
-      orph_max = std::max(orph_max, h_orph[f]);
-      if (n + 1 >= c->giant_min || n + 1 >= LINK_IDX) {
-        big.push_back(f);
-      } else {
-        sb[f] = (uint32_t)batch.off.back();
-        batch.off.push_back(batch.off.back() + n + 1);
-      }
+      A += h_app[f];
+      x2[f] = h_early[f] ? 1 : 0;
+      any_x2 |= h_early[f] != 0;
+      if (n + 1 >= c->giant_min || n + 1 >= LINK_IDX) big.push_back(f);
+      else small[h_early[f] ? 1 : 0].push_back(f);
     }
-    if (batch.off.size() > 1) {
-      NS = (batch.off.back() + 31) & ~31ull;
-      groups.push_back(std::move(batch));
+    for (int e = 0; e < 2; e++) {
+      if (small[e].empty()) continue;
+      Group g{false, e == 1, NS, {0}};
+      for (uint32_t f : small[e]) {
+        sb[f] = (uint32_t)(NS + g.off.back());
+        g.off.push_back(g.off.back() + (xoff[f + 1] - xoff[f]) + 1);
+      }
+      NS = (NS + g.off.back() + 31) & ~31ull;
+      groups.push_back(std::move(g));
     }
     for (uint32_t f : big) {
       const uint64_t n = xoff[f + 1] - xoff[f];
       sb[f] = (uint32_t)NS;
-      groups.push_back(Group{true, NS, {0, n + 1}});
+      groups.push_back(Group{true, h_early[f] != 0, NS, {0, n + 1}});
       NS = (NS + n + 1 + 31) & ~31ull;
     }
   }
-  if (NS >= 0xFFFFFFFFull) return fail(c, "exact path: %llu synthetic nodes", (unsigned long long)NS);
+  if (NS >= 0xFFFFFFF0ull - 16) return fail(c, "exact path: %llu synthetic nodes", (unsigned long long)NS);
+  c->x_iters = 0;
   if (!groups.empty()) {
+    const uint64_t NP = ((NS + 15) & ~15ull) + 16;  // min-tree level 0, padded
     uint32_t *d_sb = x_upload(c, "x_sbase", sb);
+    uint8_t *d_x2 = x_upload(c, "x_x2", x2);
     uint32_t *spar = scratch_t<uint32_t>(c, "x_spar", NS), *wperm = scratch_t<uint32_t>(c, "x_wperm", NS);
-    uint8_t *skd = scratch_t<uint8_t>(c, "x_skd", NS), *dch = scratch_t<uint8_t>(c, "x_dch", F);
+    uint8_t *skd = scratch_t<uint8_t>(c, "x_skd", NS);
     uint32_t *wbits = scratch_t<uint32_t>(c, "x_wbits", NS / 32 + 1);
-    uint32_t *pos = scratch_t<uint32_t>(c, "x_pos", NX), *ctl = scratch_t<uint32_t>(c, "x_ctl", 2);
-    unsigned long long *tmax = scratch_t<unsigned long long>(c, "x_tmax", T);
-    unsigned long long *tcar = scratch_t<unsigned long long>(c, "x_tcar", T);
+    uint32_t *G = scratch_t<uint32_t>(c, "x_G", NP), *AUX = scratch_t<uint32_t>(c, "x_aux", NP);
+    uint32_t *posA = scratch_t<uint32_t>(c, "x_pos", NS), *ctop = scratch_t<uint32_t>(c, "x_ctop", NS);
+    uint32_t *Nof = scratch_t<uint32_t>(c, "x_nof", NS), *ctl = scratch_t<uint32_t>(c, "x_ctl", 2);
     size_t gmax = 1;
     for (auto &g : groups) gmax = std::max(gmax, g.off.size() - 1);
     uint32_t *wvc = scratch_t<uint32_t>(c, "x_wvc", gmax), *wst = scratch_t<uint32_t>(c, "x_wst", gmax);
-    if (!d_sb || !spar || !wperm || !skd || !dch || !wbits || !pos || !ctl || !tmax || !tcar || !wvc ||
-        !wst)
+    if (!d_sb || !d_x2 || !spar || !wperm || !skd || !wbits || !G || !AUX || !posA || !ctop || !Nof ||
+        !ctl || !wvc || !wst)
       return fail(c, "out of device memory (exact path, %llu synthetic nodes)", (unsigned long long)NS);
-    hipLaunchKernelGGL(k_xsyn_build, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
-                       xpar, xk, spar, skd);
-    if (check_launch(c, "xsyn_build")) return -1;
-    HIPCHK(c, hipMemsetAsync(dch, 0, F, c->stream));
-    uint32_t it = 0;
-    for (;; it++) {
-      // weave every synthetic list (the fast path's tree and tour, no sort)
+    HIPCHK(c, hipMemsetAsync(ctl, 0, 8, c->stream));
+    // weave the synthetic lists of every group (or only those with an early node)
+    auto weave_groups = [&](bool early_only) -> int {
       for (auto &g : groups) {
+        if (early_only && !g.early) continue;
         const uint64_t Dg = g.off.size() - 1, Ng = g.off.back();
         if (ensure_tables(c, Dg, g.off.data(), g.giant)) return -1;
         HIPCHK(c, hipMemsetAsync(wst, 0, Dg * 4, c->stream));
@@ -606,58 +1014,101 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
         if (weave_tail(c, Dg, (uint32_t)Ng, g.giant, spar + g.base, skd + g.base, nullptr, nullptr,
                        nullptr, 0, &sr))
           return -1;
+        c->x_iters++;
       }
       if (ensure_tables(c, F, xoff.data())) return -1;  // the flagged documents' tiles again
       tile_start = dev_tab(c, "t_tile_start");
       tile_doc = dev_tab(c, "t_tile_doc");
       sub_off = dev_tab(c, "t_doc_off");
-      // every orphan under the last older node of that weave
-      HIPCHK(c, hipMemsetAsync(ctl, 0, 8, c->stream));
+      return 0;
+    };
+    auto positions = [&](uint32_t mode, const uint8_t *only, uint32_t *pos, const uint32_t *posold) -> int {
+      HIPCHK(c, hipMemsetAsync(G, 0xFF, NP * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(AUX, 0xFF, NP * 4, c->stream));
+      Launch L(c, "xsyn_pos", (double)NX * 13);
+      hipLaunchKernelGGL(k_xs_pos, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, only,
+                         wperm, skd, xk, mode, G, AUX, pos, posold, ctl);
+      return check_launch(c, "xsyn_pos");
+    };
+    // phase 1: the static forest, every appended node's T, the final weave
+    hipLaunchKernelGGL(k_xsyn_build, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
+                       xpar, xk, spar, skd);
+    if (check_launch(c, "xsyn_build")) return -1;
+    if (weave_groups(false)) return -1;
+    uint32_t *app_list = nullptr, *app_idx = nullptr;
+    if (A > 0) {
+      if (positions(0, nullptr, posA, nullptr)) return -1;
+      XMinTree mt, mtx;
+      if (mt_build(c, "x_mtG", G, NP, &mt) || mt_build(c, "x_mtA", AUX, NP, &mtx)) return -1;
+      app_list = scratch_t<uint32_t>(c, "x_app", A);
+      app_idx = scratch_t<uint32_t>(c, "x_appidx", NX);
+      uint32_t *app_doc = scratch_t<uint32_t>(c, "x_appdoc", A), *Tsyn = scratch_t<uint32_t>(c, "x_T", A);
+      uint32_t *tcnt = scratch_t<uint32_t>(c, "x_tcnt", T);
+      if (!app_list || !app_idx || !app_doc || !Tsyn || !tcnt)
+        return fail(c, "out of device memory (exact path, %llu appended nodes)", (unsigned long long)A);
+      const uint32_t A32 = (uint32_t)A;
       {
-        Launch L(c, "xsyn_attach", (double)NX * 4 * 4);
-        hipLaunchKernelGGL(k_xsyn_pos, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
-                           wperm, pos, ctl + 1);
-        hipLaunchKernelGGL(k_xsyn_tmax, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
-                           pos, tmax);
-        hipLaunchKernelGGL(k_xsyn_tcarry, dim3(F), B256, 0, c->stream, dev_tab(c, "t_tile_first"), d_sb,
-                           tmax, tcar);
-        hipLaunchKernelGGL(k_xsyn_apply, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off,
-                           d_sb, xpar, pos, tcar, spar, ctl, dch);
+        Launch L(c, "xsyn_resolve", (double)NX * 16 + (double)A * 256);
+        hipLaunchKernelGGL(k_xctop, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, spar,
+                           skd, ctop);
+        hipLaunchKernelGGL(k_xapp_count, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
+                           xpar, tcnt);
+        hipLaunchKernelGGL(k_xapp_scan, dim3(1), dim3(1024), 0, c->stream, tcnt, T);
+        hipLaunchKernelGGL(k_xapp_scatter, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off,
+                           d_sb, xpar, tcnt, app_list, app_doc, app_idx);
+        HIPCHK(c, hipMemsetAsync(Nof, 0xFF, NS * 4, c->stream));
+        hipLaunchKernelGGL(k_xres1, dim3((A32 + 255) / 256), B256, 0, c->stream, app_list, app_doc, A32,
+                           sub_off, d_sb, xk, posA, G, ctop, mt, Tsyn, Nof, ctl);
+        hipLaunchKernelGGL(k_xres2, dim3(A32), B64, 0, c->stream, app_list, app_doc, A32, sub_off, d_sb,
+                           xpar, xk, posA, G, ctop, mt, mtx, Tsyn, Nof, ctl);
+        hipLaunchKernelGGL(k_xsyn_final, dim3((A32 + 255) / 256), B256, 0, c->stream, app_list, app_doc,
+                           A32, sub_off, d_sb, xk, Tsyn, spar, skd);
       }
-      if (check_launch(c, "xsyn_attach")) return -1;
-      HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 8, hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      if (c->pin_small[1]) return fail(c, "exact path: inconsistent synthetic weave");
-      if (c->pin_small[0] == 0) break;
-      if (it > orph_max) {  // iteration k places the k-th orphan for good: never taken
-        // (not seen: one orphan is placed right per iteration) the documents
-        // still moving take the serial fold, or are left unwoven
-        std::vector<uint8_t> h_dch(F);
-        HIPCHK(c, hipMemcpy(h_dch.data(), dch, F, hipMemcpyDeviceToHost));
-        for (uint32_t f = 0; f < F; f++) {
-          if (!h_dch[f] || sb[f] == X_NONE) continue;
-          sb[f] = X_NONE;
-          const uint64_t n = xoff[f + 1] - xoff[f];
-          (n <= XFOLD_MAX ? run : unwoven)[f] = 1;
-          any_serial |= n <= XFOLD_MAX;
-        }
-        d_sb = x_upload(c, "x_sbase", sb);
-        if (!d_sb) return fail(c, "out of device memory (exact path)");
-        break;
-      }
-      HIPCHK(c, hipMemsetAsync(dch, 0, F, c->stream));
+      if (check_launch(c, "xsyn_resolve")) return -1;
+      if (weave_groups(false)) return -1;
     }
-    c->x_iters = it + 1;
+    // phase 2: documents with an early node, insertion-tree rounds from there
+    if (any_x2) {
+      uint32_t *posB = scratch_t<uint32_t>(c, "x_posB", NS), *xf = scratch_t<uint32_t>(c, "x_xf", NX);
+      if (!posB || !xf || !app_list) return fail(c, "out of device memory (exact path rounds)");
+      if (positions(1, d_x2, posA, nullptr)) return -1;
+      for (uint32_t round = 0;; round++) {
+        XMinTree mt, mtn;
+        if (mt_build(c, "x_mtG", G, NP, &mt) || mt_build(c, "x_mtA", AUX, NP, &mtn)) return -1;
+        {
+          Launch L(c, "xins_round", (double)NX * 40);
+          HIPCHK(c, hipMemsetAsync(xf, 0xFF, (size_t)NX * 4, c->stream));
+          hipLaunchKernelGGL(k_xf, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, d_x2,
+                             xpar, posA, xf);
+          hipLaunchKernelGGL(k_xpred, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
+                             d_x2, xpar, xk, early, xf, app_list, app_idx, posA, G, mt, mtn,
+                             round == 0 ? 1u : 0u, spar, skd, ctl);
+        }
+        if (check_launch(c, "xins_round")) return -1;
+        if (weave_groups(true)) return -1;
+        HIPCHK(c, hipMemsetAsync(ctl, 0, 4, c->stream));
+        if (positions(1, d_x2, posB, posA)) return -1;
+        std::swap(posA, posB);
+        HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->pin_small[1]) return fail(c, "exact path: inconsistent synthetic weave (%u)", c->pin_small[1]);
+        if (c->pin_small[0] == 0) break;  // the weave reproduced itself: the fold's
+        if (round > NX + 2) return fail(c, "exact path: no fixed point after %u rounds", round);
+      }
+    }
+    HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->pin_small[1]) return fail(c, "exact path: inconsistent synthetic weave (%u)", c->pin_small[1]);
     hipLaunchKernelGGL(k_xsyn_zero, GF, B64, 0, c->stream, d_sb, F, d_odoc, out->visible_count);
-    {
+    for (uint32_t adj = 0; adj < (any_x2 ? 2u : 1u); adj++) {
       Launch L(c, "xsyn_emit", (double)NX * (4 + 4 + 4 + 1) + (double)NX / 8);
-      hipLaunchKernelGGL(k_xsyn_emit, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
-                         wperm, wbits, xk, sval, d_oof, d_odoc, out->weave_perm, out->visible_bits,
-                         out->visible_count);
+      hipLaunchKernelGGL(k_xsyn_emit, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, d_x2,
+                         adj, wperm, wbits, xk, xpar, sval, d_oof, d_odoc, out->weave_perm,
+                         out->visible_bits, out->visible_count);
     }
     if (check_launch(c, "xsyn_emit")) return -1;
   }
-  if (any_serial) {  // documents with a non-Lamport cause: the literal fold, one lane each
+  if (any_serial) {  // CW_XFOLD: the literal fold, one lane a document
     uint8_t *d_run = x_upload(c, "x_run", run);
     uint32_t *xnext = scratch_t<uint32_t>(c, "x_next", NX);
     if (!d_run || !xnext) return fail(c, "out of device memory (exact path)");
@@ -665,14 +1116,7 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
     hipLaunchKernelGGL(k_xfold, GF, B64, 0, c->stream, sub_off, F, xpar, xk, early, xnext, sval,
                        d_oof, d_odoc, out->weave_perm, out->visible_bits, out->visible_count, d_run);
   }
-  if (check_launch(c, "xfold")) return -1;
-  if (std::find(unwoven.begin(), unwoven.end(), 1) != unwoven.end()) {
-    uint8_t *d_un = x_upload(c, "x_unwoven", unwoven);
-    if (!d_un) return fail(c, "out of device memory (exact path)");
-    hipLaunchKernelGGL(k_xunwoven, GF, B64, 0, c->stream, d_un, F, d_odoc, out->status);
-    if (check_launch(c, "xunwoven")) return -1;
-  }
-    return 0;
+  return check_launch(c, "xfold");
 }
 
 // After the fast path has woven a batch (device arrays id/cause/kind laid out
@@ -803,7 +1247,7 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
 }
 
 // cw_weave_ranked's exact path: the one list given by (par, kind) in rank order
-// (the same routing as exact_fixup: synthetic lists, serial fold or UNWOVEN).
+// (the same path as exact_fixup's documents).
 int exact_ranked(cw_ctx *c, const cw_ranked_list *l, cw_list_result *out) {
   const uint32_t n = (uint32_t)l->n;
   uint32_t *xpar = scratch_t<uint32_t>(c, "x_par", n), *dorph = scratch_t<uint32_t>(c, "x_dorph", 1);

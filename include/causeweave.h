@@ -69,12 +69,9 @@ enum {
   CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits                      */
   CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
   CW_STATUS_WEFT = 1u << 6,        /* weft: a cut id is not a node of the document         */
-  CW_STATUS_KEY_RANGE = 1u << 7,   /* an id key >= 2^63: it does not fit the K64 layout
+  CW_STATUS_KEY_RANGE = 1u << 7    /* an id key >= 2^63: it does not fit the K64 layout
                                       (CW_NIL and its neighbours are reserved); weave the
                                       document with cw_weave_lists_k128                     */
-  CW_STATUS_UNWOVEN = 1u << 8      /* a document with a non-Lamport cause (NON_LAMPORT)
-                                      larger than the literal fold's limit (2^22 nodes):
-                                      its outputs are unspecified                         */
 };
 
 /* Where the arrays of a batch/result live. */

@@ -143,7 +143,7 @@ def test_weave_ranked_exact(case):
     par = par.view(np.uint32).copy()
     kd = kd.copy()
     rng = np.random.default_rng(1)
-    if case in ("orphan", "orphan_few"):  # the serial fold / the synthetic list
+    if case in ("orphan", "orphan_few"):  # absent causes: phase 1 of the synthetic lists
         k = 40 if case == "orphan" else 7
         par[rng.choice(np.arange(1, len(par)), k, replace=False)] = 0xFFFFFFFF
     elif case == "non_lamport":
@@ -195,47 +195,81 @@ def _orphaned(spec, D, per_doc, rng, nil_every=0):
     return off, idk, ck, kd
 
 
-def _attach_iterations(w):
-    return w.kernel_stats().get("xsyn_attach", (0, 0.0, 0.0))[0]
+def _stage_launches(w, name):
+    return w.kernel_stats().get(name, (0, 0.0, 0.0))[0]
 
 
-def test_orphan_documents_synthetic_lists_few_iterations():
-    """Documents with 1 .. 32 orphans (and nil causes) go through the synthetic
-    lists: bit-exact against the literal fold, in at most (orphans + 1)
-    iterations (one weave each) -- 2 when every document has one orphan."""
+def _nonlamport(spec, D, per_doc, rng, orphans=None):
+    """Config-2-shaped documents whose per_doc[d] random nodes get a cause with
+    a larger id (some a node's own id), plus orphans[d] absent causes."""
+    off, idk, ck, kd = _orphaned(spec, D, orphans or [0] * D, rng)
+    for d in range(D):
+        a, b = int(off[d]), int(off[d + 1])
+        srt = np.sort(idk[a:b])
+        for j in rng.choice(np.arange(a + 1, b), per_doc[d], replace=False):
+            k = int(np.searchsorted(srt, idk[j]))
+            self_cause = rng.random() < 0.1 or k + 1 >= len(srt)
+            ck[j] = srt[k] if self_cause else srt[rng.integers(k + 1, len(srt))]
+    return off, idk, ck, kd
+
+
+def test_orphan_documents_one_resolve_no_rounds():
+    """Documents with 1 .. 500 orphans (and nil causes): phase 1 places every
+    appended node from one static weave -- one resolve step and two weaves
+    whatever the number of orphans (round 3 took one weave per orphan), no
+    phase-2 round -- bit-exact against the literal fold."""
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=6000, seed=31)
     rng = np.random.default_rng(31)
+    per = [1, 2, 3, 5, 8, 13, 21, 32, 4, 7, 16, 30, 200, 500, 64, 33]
+    off, idk, ck, kd = _orphaned(spec, len(per), per, rng, nil_every=3)
     with abi.Weaver(0) as w:
-        off, idk, ck, kd = _orphaned(spec, 24, [1] * 24, rng)
         w.reset_kernel_stats()
         w.set_profiling(True)
         res = check_batch(w, off, idk, ck, kd, spec.layout())
         w.set_profiling(False)
         assert (res.status & abi.STATUS_ORPHAN).all()
-        assert 1 <= _attach_iterations(w) <= 2
-        per = [1, 2, 3, 5, 8, 13, 21, 32, 4, 7, 16, 30]
-        off, idk, ck, kd = _orphaned(spec, len(per), per, rng, nil_every=3)
+        assert _stage_launches(w, "xsyn_resolve") == 1
+        assert _stage_launches(w, "xins_round") == 0
+        assert "xfold" not in w.kernel_stats()
+
+
+def test_non_lamport_documents_rounds():
+    """Non-Lamport causes (a node caused by a younger node, or by its own id)
+    next to orphans and clean documents: phase 2's insertion-tree rounds reach
+    the fold's weave; the same batch through the serial fold (CW_XFOLD=1)
+    agrees."""
+    import os
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000, seed=32)
+    rng = np.random.default_rng(32)
+    nl = [1, 0, 3, 10, 0, 40, 2, 100]
+    orph = [0, 5, 2, 0, 0, 30, 200, 3]
+    off, idk, ck, kd = _nonlamport(spec, len(nl), nl, rng, orphans=orph)
+    with abi.Weaver(0) as w:
         w.reset_kernel_stats()
         w.set_profiling(True)
         res = check_batch(w, off, idk, ck, kd, spec.layout())
         w.set_profiling(False)
-        assert 2 <= _attach_iterations(w) <= max(per) + 1
+        assert 1 <= _stage_launches(w, "xins_round") <= 12
+        assert "xfold" not in w.kernel_stats()
+    assert all(bool(res.status[d] & abi.STATUS_NON_LAMPORT) == (nl[d] > 0) for d in range(len(nl)))
+    os.environ["CW_XFOLD"] = "1"
+    try:
+        with abi.Weaver(0) as w:
+            w.set_profiling(True)
+            check_batch(w, off, idk, ck, kd, spec.layout())
+            assert "xfold" in w.kernel_stats()
+    finally:
+        del os.environ["CW_XFOLD"]
 
 
-def test_many_orphans_take_the_serial_fold_next_to_synthetic_ones():
-    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=3000, seed=32)
-    rng = np.random.default_rng(32)
-    off, idk, ck, kd = _orphaned(spec, 8, [1, 200, 3, 64, 0, 33, 2, 500], rng, nil_every=5)
-    with abi.Weaver(0) as w:
-        check_batch(w, off, idk, ck, kd, spec.layout())
-
-
-@pytest.mark.parametrize("orphans", [1, 10])
+@pytest.mark.parametrize("orphans", [1, 10, 300])
 def test_giant_list_orphans_synthetic(orphans):
     """A one-document batch on the giant path with absent and nil causes: the
-    synthetic list is woven on the giant path too (compared with the C
-    restatement of the exact path's rule, or_list_fold_general, itself pinned
-    to the literal fold by test_oracle)."""
+    synthetic lists are woven on the giant path too, one resolve step whatever
+    the number of orphans (compared with the C restatement of the exact path's
+    rule, or_list_fold_general, itself pinned to the literal fold by
+    test_oracle)."""
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=300_000, seed=33 + orphans)
     rng = np.random.default_rng(orphans)
     off, idk, ck, kd = _orphaned(spec, 1, [orphans], rng, nil_every=4)
@@ -244,20 +278,26 @@ def test_giant_list_orphans_synthetic(orphans):
         w.set_profiling(True)
         res = check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_GENERAL)
         w.set_profiling(False)
-        assert _attach_iterations(w) <= orphans + 1
+        assert _stage_launches(w, "xsyn_resolve") == 1
+        assert _stage_launches(w, "xins_round") == 0
         assert "xfold" not in w.kernel_stats()  # no serial lane
     assert res.status[0] & abi.STATUS_ORPHAN
 
 
-def test_unwoven_above_the_serial_limit():
-    """A non-Lamport cause in a document above the serial fold's limit (2^22
-    nodes) is not folded on one lane: CW_STATUS_UNWOVEN, the call returns."""
-    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 10, seed=34)
-    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=16)
-    ck = ck.copy()
-    srt = np.sort(idk)
-    ck[100] = srt[-5]  # a cause with a larger id
+def test_large_list_orphans_and_non_lamport():
+    """a list of 2^23 nodes with 2,000 orphans and 50 non-Lamport
+    causes -- above the old serial fold's limit, where round 3 returned
+    CW_STATUS_UNWOVEN -- bit-exact against the oracle's general fold."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 23) - 1, seed=34)
+    rng = np.random.default_rng(34)
+    off, idk, ck, kd = _nonlamport(spec, 1, [50], rng, orphans=[2000])
     with abi.Weaver(0) as w:
-        res = w.weave_lists(off, idk, ck, kd, spec.layout())
-    assert res.status[0] & abi.STATUS_NON_LAMPORT
-    assert res.status[0] & abi.STATUS_UNWOVEN
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_GENERAL,
+                          yarns=False)
+        w.set_profiling(False)
+        rounds = _stage_launches(w, "xins_round")
+        print(f"2^23 nodes, 2000 orphans, 50 non-Lamport: {rounds} rounds")
+        assert 1 <= rounds <= 12
+    assert res.status[0] & abi.STATUS_NON_LAMPORT and res.status[0] & abi.STATUS_ORPHAN

@@ -368,22 +368,37 @@ def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
 
 
 # ------------------------------------------------- one giant document (config 5)
-@pytest.fixture(scope="module")
-def giant_weaver():
-    """A context that sends every one-document batch through the giant-document
-    tree (k_geff / radix sort / k_gsib / k_gthr + the walk's thread chase)."""
+# Giant-path front ends: the directory over the whole key range
+# (k_gd_place, small key ranges: the default here), the sorted-id directory
+# join (CW_GDIR=0: k_gd_first / k_gd_set_sorted / k_gpack / k_gjoin, config
+# 5's default), without the packed cause + kind word (CW_GPACK=0), and the
+# bucket index + searching join (CW_GJOIN=0).
+GIANT_FRONTS = {"gdplace": {}, "gjoin": {"CW_GDIR": "0"},
+                "gjoin-unpacked": {"CW_GDIR": "0", "CW_GPACK": "0"},
+                "bucket": {"CW_GDIR": "0", "CW_GJOIN": "0"}}
+
+
+def _weaver_with(env):
     import os
 
-    old = os.environ.get("CW_GIANT_MIN")
-    os.environ["CW_GIANT_MIN"] = "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        w = abi.Weaver(0)
+        return abi.Weaver(0)  # knobs are read when the context is created
     finally:
-        if old is None:
-            os.environ.pop("CW_GIANT_MIN", None)
-        else:
-            os.environ["CW_GIANT_MIN"] = old
-    with w:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module", params=sorted(GIANT_FRONTS))
+def giant_weaver(request):
+    """A context that sends every one-document batch through the giant-document
+    tree (k_geff / radix sort / k_gsib / k_gthr + the walk's thread chase),
+    under each giant front end."""
+    with _weaver_with(dict(GIANT_FRONTS[request.param], CW_GIANT_MIN="0")) as w:
         yield w
 
 
@@ -398,10 +413,33 @@ def test_giant_path_small_documents(giant_weaver):
     for steps, tx in ((200, 0.0), (2000, 0.0), (1500, 0.3)):
         docs.append(G.stress_history(rng, steps, tx_chain=tx))
     docs.append([R.ROOT_NODE])
+    # out of the fast path's domain: absent, younger and nil causes, no root,
+    # a repeated id (its output is unspecified, its status is not)
+    from tests import outdomain as X
+
+    for kinds in [("orphan",), ("non_lamport",), ("nil_cause",), ("no_root",), X.KINDS]:
+        nodes = G.stress_history(rng, 400, p_special=0.3)
+        docs.append(X.corrupt(nodes, rng, kinds, rate=0.03))
+    nodes = G.stress_history(rng, 300)
+    docs.append(nodes + [nodes[7]])
     for d in docs:
         rng.shuffle(d)
         b = pack.pack_lists([d])
         check_batch(giant_weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
+
+
+def test_giant_join_misdeclared_key_bits():
+    """ids wider than the declared key_bits on the sorted-id directory join
+    (ADVICE r3): the directory is never read past its end, the list is flagged
+    INTERNAL instead of faulting."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=100_000, seed=41)
+    off, idk, ck, kd = gen.generate(spec, 0, 1)
+    lay = spec.layout()
+    with _weaver_with({"CW_GDIR": "0", "CW_GIANT_MIN": "0"}) as w:
+        res = w.weave_lists(off, idk, ck, kd, lay, key_bits=max(1, lay.key_bits - 6))
+        assert res.status[0] & abi.STATUS_INTERNAL
+        again = w.weave_lists(off, idk, ck, kd, lay)  # the context still works
+        assert again.status[0] == 0
 
 
 def test_giant_path_shapes(giant_weaver):
