@@ -3845,6 +3845,15 @@ struct cw_ctx {
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
   hipEvent_t ev_status = nullptr;  // ... and recorded there (exact.hip waits on it, not the stream)
   bool x_pending = false;          // pin_status / ev_status hold this call's giant document
+  struct XFront {                  // a flagged giant list's front end, handed to the exact path
+    const uint64_t *skey = nullptr;  // sorted ids
+    const uint32_t *sval = nullptr;  // input index by rank
+    const uint4 *dir = nullptr;      // rank directory of the sorted ids (E entries)
+    uint64_t E = 0;
+    const uint64_t *ckk = nullptr;   // cause | kind << 56 by input index, or nullptr
+    uint32_t n = 0;
+    bool ok = false;
+  } xfront;
   uint32_t map_fused = 1;          // CW_MAP_FUSED: one-kernel map weave of small collections
   struct MapPacks {                // k_map_pack's pack table, cached by collection layout
     std::vector<uint64_t> off;
@@ -4560,6 +4569,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
   const dim3 B256(256);
 
   HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
+  c->xfront = cw_ctx::XFront{};
   // one giant document: k_geff zeroes the count, k_pack_bits writes every word
   const bool giant1 = is_giant(c, D, bt->doc_offsets);
   if (!giant1) HIPCHK(c, hipMemsetAsync(out->visible_count, 0, D * 4, c->stream));
@@ -4837,6 +4847,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            reinterpret_cast<const uint4 *>(gdir), E, par, skind, out->status);
       }
       if (check_launch(c, "join")) return -1;
+      c->xfront = {skey, sval, reinterpret_cast<const uint4 *>(gdir), E, ckk, N, false};
     } else {
     uint32_t *bkt = scratch_t<uint32_t>(c, "bkt", t.Btot);
     if (!bkt) return fail(c, "out of device memory (bucket index)");
@@ -4881,6 +4892,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t st = c->pin_status[0];
       flagged = (st & (CW_STATUS_ROOT | CW_STATUS_ORPHAN | CW_STATUS_NON_LAMPORT)) &&
                 !(st & (CW_STATUS_DUP | CW_STATUS_KEY_RANGE | CW_STATUS_INTERNAL));
+      // the sorted ids and the directory stay intact (no tail): the exact path
+      // joins from them instead of sorting again
+      c->xfront.ok = flagged && c->xfront.skey && c->xfront.n == N;
     }
     // without yarns the id-sort buffers are free once the ids are joined
     const bool spare = !want_yarns;

@@ -165,6 +165,52 @@ __global__ __launch_bounds__(256) void k_xjoin(
   }
 }
 
+// One giant list flagged by its front end (cw_ctx::xfront): the exact path's
+// join from the front end's sorted ids and rank directory, no second sort --
+// the cause of every rank by input index (cause | kind in one word when the
+// front end packed it), its rank from one directory line (X_NIL, X_END, or a
+// rank that may be younger), early children and the appended count.
+__global__ __launch_bounds__(256) void k_xjoin_dir(
+    const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
+    const uint64_t *__restrict__ cause_key, const uint8_t *__restrict__ kind,
+    const uint64_t *__restrict__ ckk, uint32_t n, const uint4 *__restrict__ dir, uint64_t E,
+    uint32_t *__restrict__ xpar, uint8_t *__restrict__ xk, uint8_t *__restrict__ early,
+    uint8_t *__restrict__ doc_early, uint32_t *__restrict__ doc_orph) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  bool app = false;
+  if (r < n) {
+    constexpr uint64_t M56 = (1ull << 56) - 1;
+    const uint32_t v = sval[r];
+    uint64_t c;
+    uint8_t kd;
+    if (ckk) {
+      const uint64_t w = ckk[v];
+      c = w & M56;
+      kd = (uint8_t)(w >> 56);
+      if (c == M56) c = cause_key[v];  // nil, or a cause no id can be
+    } else {
+      c = cause_key[v];
+      kd = kind[v];
+    }
+    uint32_t p = X_NIL;
+    if (c != CW_NIL) {
+      const uint64_t kmax = min(skey[n - 1], E * GD_KEYS - 1);
+      bool present = false;
+      const uint32_t rc = c <= kmax ? gd_rank(dir, c, present) : 0u;
+      p = present ? rc : X_END;
+    }
+    xpar[r] = p;
+    xk[r] = kd;
+    if (p < n && p > r) {
+      early[p] = 1;
+      *doc_early = 1;
+    }
+    app = x_appended(p, r, n);
+  }
+  const uint64_t b = __ballot(app);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(doc_orph, (uint32_t)__popcll(b));
+}
+
 // A list handed over in rank order (cw_weave_ranked): the root's cause is nil,
 // CW_NOT_FOUND stays "absent"; early children as in k_xjoin.
 __global__ __launch_bounds__(256) void k_xranked_prep(const uint32_t *__restrict__ par,
@@ -1119,6 +1165,51 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
   return check_launch(c, "xfold");
 }
 
+// exact_fixup for one giant list whose front end left its sorted ids and rank
+// directory (cw_ctx::xfront): no gather, no second sort, the join through the
+// directory (k_xjoin_dir), then the same path as every flagged document.
+int exact_giant_front(cw_ctx *c, const cw_list_batch *bt, cw_list_result *out) {
+  const auto &xf = c->xfront;
+  const uint32_t N = xf.n;
+  const std::vector<uint64_t> xoff = {0, N};
+  if (ensure_tables(c, 1, xoff.data())) return -1;
+  uint8_t *xk = scratch_t<uint8_t>(c, "x_k", N), *early = scratch_t<uint8_t>(c, "x_early", N);
+  uint8_t *dearly = scratch_t<uint8_t>(c, "x_dearly", 1);
+  uint32_t *dorph = scratch_t<uint32_t>(c, "x_dorph", 1), *xpar = scratch_t<uint32_t>(c, "x_par", N);
+  uint32_t *odoc = scratch_t<uint32_t>(c, "x_rodoc", 1);
+  uint64_t *oof = scratch_t<uint64_t>(c, "x_roof", 1);
+  if (!xk || !early || !dearly || !dorph || !xpar || !odoc || !oof)
+    return fail(c, "out of device memory (exact path, %u nodes)", N);
+  HIPCHK(c, hipMemsetAsync(odoc, 0, 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(oof, 0, 8, c->stream));
+  HIPCHK(c, hipMemsetAsync(early, 0, N, c->stream));
+  HIPCHK(c, hipMemsetAsync(dearly, 0, 1, c->stream));
+  HIPCHK(c, hipMemsetAsync(dorph, 0, 4, c->stream));
+  {
+    Launch L(c, "xjoin", (double)N * (4 + 8 + 4 + 1) + (double)N * 64);
+    hipLaunchKernelGGL(k_xjoin_dir, dim3((N + 255) / 256), dim3(256), 0, c->stream, xf.skey, xf.sval,
+                       bt->cause_key, bt->kind, xf.ckk, N, xf.dir, xf.E, xpar, xk, early, dearly, dorph);
+  }
+  if (check_launch(c, "xjoin")) return -1;
+  if (out->max_ts) {
+    hipLaunchKernelGGL(k_xmaxts, dim3(1), dim3(64), 0, c->stream, dev_tab(c, "t_doc_off"), 1u, xf.skey,
+                       bt->ts_shift, odoc, out->max_ts);
+    if (check_launch(c, "xmaxts")) return -1;
+  }
+  if (out->yarn_perm && bt->site_bits) {  // spin: the id order partitioned by site
+    uint64_t *ykA = scratch_t<uint64_t>(c, "x_skA", N), *ykB = scratch_t<uint64_t>(c, "x_skB", N);
+    uint32_t *yvA = scratch_t<uint32_t>(c, "x_svA", N), *yvB = scratch_t<uint32_t>(c, "x_yv", N);
+    if (!ykA || !ykB || !yvA || !yvB) return fail(c, "out of device memory (exact path yarns)");
+    uint64_t *yk;
+    uint32_t *yv;
+    if (radix_sort<uint64_t>(c, "xyarns", xf.skey, xf.sval, ykA, yvA, ykB, yvB, bt->site_bits,
+                             bt->site_shift, N, &yk, &yv))
+      return -1;
+    HIPCHK(c, hipMemcpyAsync(out->yarn_perm, yv, (size_t)N * 4, hipMemcpyDeviceToDevice, c->stream));
+  }
+  return exact_weave_flagged(c, 1, xoff, xpar, xk, early, xf.sval, oof, odoc, dearly, dorph, out);
+}
+
 // After the fast path has woven a batch (device arrays id/cause/kind laid out
 // by bt->doc_offsets, results in `out`): reweave its flagged documents by the
 // literal fold and overwrite their weave_perm, rendered bits and count, and
@@ -1137,6 +1228,7 @@ int exact_fixup(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id, const ui
     HIPCHK(c, hipEventSynchronize(c->ev_status));
     const uint32_t st = c->pin_status[0];
     if (!(st & X_MASK) || (st & X_SKIP)) return 0;
+    if (c->xfront.ok && c->xfront.n == off[1]) return exact_giant_front(c, bt, out);
   } else if (D <= 16) {
     // a few documents: their status words in one readback
     HIPCHK(c, hipMemcpyAsync(c->pin_small, out->status, D * 4, hipMemcpyDeviceToHost, c->stream));
