@@ -206,13 +206,15 @@ def lib():
         L.cw_sort_keys.argtypes = [P, P, U64, U32, P, P]
         L.cw_lookup_keys.argtypes = [P, P, U64, P, U64, U32, P, P]
         L.cw_partition_keys.argtypes = [P, P, U64, P, U32, P, P]
+        L.cw_partition_keys_dev.argtypes = [P, P, U64, P, U32, P, P]
         L.cw_gather.argtypes = [P, P, P, U64, U32, P]
         L.cw_scatter32.argtypes = [P, P, P, U64, P]
         L.cw_weave_ranked.argtypes = [P, C.POINTER(CwRankedList), C.POINTER(CwListResult)]
         L.cw_weave_linked.argtypes = [P, C.POINTER(CwLinkedList), C.POINTER(CwListResult)]
         L.cw_sort_keys32.argtypes = [P, P, U64, U32, P, P]
         L.cw_sort_keys32.restype = C.c_int
-        for f in ("cw_sort_keys", "cw_lookup_keys", "cw_partition_keys", "cw_gather", "cw_scatter32",
+        for f in ("cw_sort_keys", "cw_lookup_keys", "cw_partition_keys", "cw_partition_keys_dev",
+                  "cw_gather", "cw_scatter32",
                   "cw_weave_ranked", "cw_weave_linked"):
             getattr(L, f).restype = C.c_int
         for f, a in _DIST_ARGS.items():
@@ -490,6 +492,11 @@ class Weaver:
         self._check(self._L.cw_partition_keys(self._h, keys_ptr, m, split_ptr, n_split, perm_ptr,
                                               counts.ctypes.data), "cw_partition_keys")
         return counts
+
+    def partition_keys_dev(self, keys_ptr, m, split_ptr, n_split, perm_ptr, counts_ptr):
+        """cw_partition_keys with the n_split + 1 counts (u64) left in device memory."""
+        self._check(self._L.cw_partition_keys_dev(self._h, keys_ptr, m, split_ptr, n_split, perm_ptr,
+                                                  counts_ptr), "cw_partition_keys_dev")
 
     def gather_device(self, src_ptr, idx_ptr, m, elem_size, dst_ptr):
         self._check(self._L.cw_gather(self._h, src_ptr, idx_ptr, m, elem_size, dst_ptr), "cw_gather")

@@ -2349,7 +2349,8 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
                                              const uint32_t *__restrict__ fcS,
                                              const uint32_t *__restrict__ fcN,
                                              const uint8_t *__restrict__ skind, uint32_t n,
-                                             uint32_t log2k, uint32_t *__restrict__ thr,
+                                             const uint32_t *__restrict__ sval,
+                                             uint32_t *__restrict__ thr,
                                              uint64_t *__restrict__ link) {
   // T: a pointer to a lower rank of the tile, RES | resolved thread, or OUT | an
   // ancestor outside the tile (its thread is left to the walk)
@@ -2375,8 +2376,7 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
     }
     T[j] = tv;
     const bool vis = !sp && r != 0 && !(fs && is_hide(skind[fs]));
-    const bool split = r == split_node(0, r >> log2k, log2k, n);
-    flg[k] = (vis ? LINK_VIS : 0u) | (split ? LINK_SPLIT : 0u);
+    flg[k] = vis ? LINK_VIS : 0u;
   }
   __syncthreads();
   for (;;) {  // pointer jumping inside the tile (pointers go to lower ranks)
@@ -2404,8 +2404,7 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
     const uint32_t v = (uint32_t)a;  // resolved thread, or the ancestor to chase
     thr[r] = res ? v : (THRW_PEND | v);
     const uint32_t succ = fcr[k] ? fcr[k] : v;
-    const uint32_t f = flg[k] | (!fcr[k] && !res ? LINK_PEND : 0u);
-    link[r] = (uint64_t)succ | ((uint64_t)f << 32);
+    link[r] = wide_link(succ, !fcr[k] && !res, sval ? sval[r] : r, flg[k] != 0);
   }
 }
 
@@ -2435,26 +2434,34 @@ __global__ __launch_bounds__(1024) void k_walk(
   // link word of node x: successor index and LINK_* flags (narrow: one u32;
   // wide: u64 = successor | flags << 32)
   constexpr uint32_t END = WIDE ? SUCCW_END : SUCC_END;
-  auto load = [&](uint32_t x, uint32_t &succ) -> uint32_t {
+  // (wide: the LINK_* flags rebuilt -- the splitter bit from the rank -- and
+  // the node's slot entry = the value it emits, so the emit gathers nothing;
+  // narrow: the entry is the rank)
+  auto load = [&](uint32_t x, uint32_t &succ, uint32_t &ent) -> uint32_t {
     if (WIDE) {
       const uint64_t L = static_cast<const uint64_t *>(linkp)[base + x];
-      succ = (uint32_t)L;
-      return (uint32_t)(L >> 32);
+      succ = (uint32_t)L & SUCCW_END;
+      const bool vis = (L >> 63) != 0;
+      ent = (uint32_t)(L >> 32) & SLOT_IDX;
+      ent |= vis ? 0x80000000u : 0u;
+      return (vis ? LINK_VIS : 0u) | (((uint32_t)L >> 31) ? LINK_PEND : 0u) |
+             (x == split_node(d, x >> log2k, log2k, n) ? LINK_SPLIT : 0u);
     }
     const uint32_t L = static_cast<const uint32_t *>(linkp)[base + x];
     succ = L & LINK_IDX;
+    ent = x | (L & LINK_VIS);
     return L & ~LINK_IDX;
   };
   if (threadIdx.x == 0) next_walker = w0 + blockDim.x;
   __syncthreads();
   for (uint32_t lw = w0 + threadIdx.x; lw < w1; lw = atomicAdd(&next_walker, 1u)) {
     const uint32_t v = split_node(d, lw, log2k, n);
-    uint32_t sv;
-    uint32_t L = load(v, sv);
+    uint32_t sv, ev;
+    uint32_t L = load(v, sv, ev);
     uint32_t x = lw, cnt = 1, nextsub = NX_END;
     // entries are buffered four at a time and written as one 16-byte store
     // (slots are 16-byte aligned: cap >= 4 and every slot start is a multiple)
-    uint4 q = make_uint4(v | (L & LINK_VIS), 0u, 0u, 0u);
+    uint4 q = make_uint4(ev, 0u, 0u, 0u);
     for (uint32_t steps = 0;; steps++) {
       uint32_t u = sv;
       if (L & LINK_PEND)  // the successor is the thread of an ancestor: chase it
@@ -2474,8 +2481,8 @@ __global__ __launch_bounds__(1024) void k_walk(
         if (u != END) atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
         break;
       }
-      uint32_t su;
-      const uint32_t Lu = load(u, su);
+      uint32_t su, eu;
+      const uint32_t Lu = load(u, su, eu);
       if (Lu & LINK_SPLIT) {
         nextsub = u >> log2k;
         break;
@@ -2501,7 +2508,7 @@ __global__ __launch_bounds__(1024) void k_walk(
         x = y;
         cnt = 0;
       }
-      const uint32_t e = u | (Lu & LINK_VIS);
+      const uint32_t e = eu;
       switch (cnt & 3) {
         case 0: q.x = e; break;
         case 1: q.y = e; break;
@@ -4347,7 +4354,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     {
       Launch L(c, "gthr", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
       hipLaunchKernelGGL((k_gthr<256, 1024>), dim3((N + 1023) / 1024), B256, 0, c->stream, nsc,
-                         fcS, fcN, skind, N, t.doc_log2k[0], thr, link);
+                         fcS, fcN, skind, N, sval, thr, link);
     }
     if (check_launch(c, "gthr")) return -1;
   }
@@ -4540,8 +4547,10 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     // 8. emit
     {
       Launch L(c, "emit", (double)N * (4 + 4 + 4 + 1) + (double)t.Wtot * 8);
+      // (giant: the slot entries hold the emitted values already, see k_walk)
       hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
-                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order, sval,
+                         (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order,
+                         giant ? nullptr : sval,
                          dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
                          dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
                          out->visible_count, out->status);
@@ -5195,6 +5204,91 @@ __global__ __launch_bounds__(256) void k_gather(const E *__restrict__ src,
   if (i < m) dst[i] = src[idx[i]];
 }
 
+// A stable partition by bucket for few buckets (<= PB_MAX: the exchange of
+// a distributed round has W + 1), with no sort and no host tables: count per
+// block and bucket, one scan (bucket-major), scatter in order.  The sizes of
+// the buckets land in device memory, so the caller need not wait.
+constexpr uint32_t PB_MAX = 16, PB_ITEMS = 8, PB_NT = 256, PB_CHUNK = PB_ITEMS * PB_NT;
+
+__device__ __forceinline__ uint32_t pb_bucket(const uint64_t *__restrict__ split, uint32_t ns,
+                                              uint64_t x) {
+  uint32_t lo = 0, hi = ns;  // first splitter > x
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (split[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(PB_NT) void k_pb_count(const uint64_t *__restrict__ keys, uint32_t m,
+                                                    const uint64_t *__restrict__ split, uint32_t ns,
+                                                    uint32_t *__restrict__ bcnt, uint32_t nblk) {
+  __shared__ uint32_t c[PB_MAX];
+  if (threadIdx.x < PB_MAX) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * PB_CHUNK + threadIdx.x * PB_ITEMS;
+#pragma unroll
+  for (uint32_t u = 0; u < PB_ITEMS; u++)
+    if (i0 + u < m) atomicAdd(&c[pb_bucket(split, ns, keys[i0 + u])], 1u);
+  __syncthreads();
+  if (threadIdx.x <= ns) bcnt[threadIdx.x * nblk + blockIdx.x] = c[threadIdx.x];
+}
+
+// exclusive scan of the (ns + 1) x nblk counts, bucket-major, in place; the
+// bucket sizes into counts[0..ns]
+__global__ __launch_bounds__(1024) void k_pb_scan(uint32_t *__restrict__ bcnt, uint32_t nblk,
+                                                  uint32_t ns, unsigned long long *__restrict__ counts) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, T = (ns + 1) * nblk;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < T; c0 += 1024) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint32_t v = t < T ? bcnt[t] : 0;
+    uint32_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (uint32_t w = 0; w < wv; w++) pre += wsum[w];
+    if (t < T) bcnt[t] = pre + inc - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = pre + inc;
+    __syncthreads();
+  }
+  // bucket b spans [bcnt[b * nblk], bcnt[(b + 1) * nblk]) (the last ends at the total)
+  if (threadIdx.x <= ns) {
+    const uint32_t b = threadIdx.x;
+    const uint32_t lo = bcnt[b * nblk], hi = b < ns ? bcnt[(b + 1) * nblk] : carry;
+    counts[b] = hi - lo;
+  }
+}
+
+__global__ __launch_bounds__(PB_NT) void k_pb_scatter(const uint64_t *__restrict__ keys, uint32_t m,
+                                                      const uint64_t *__restrict__ split, uint32_t ns,
+                                                      const uint32_t *__restrict__ boff,
+                                                      uint32_t nblk, uint32_t *__restrict__ perm) {
+  __shared__ uint32_t wtot[PB_NT / 64];
+  const uint32_t i0 = blockIdx.x * PB_CHUNK + threadIdx.x * PB_ITEMS;
+  uint32_t bk[PB_ITEMS];
+#pragma unroll
+  for (uint32_t u = 0; u < PB_ITEMS; u++)
+    bk[u] = i0 + u < m ? pb_bucket(split, ns, keys[i0 + u]) : 0xFFFFFFFFu;
+  for (uint32_t b = 0; b <= ns; b++) {
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < PB_ITEMS; u++) mine += bk[u] == b ? 1u : 0u;
+    uint32_t at = boff[b * nblk + blockIdx.x] + block_exscan<PB_NT>(mine, wtot, nullptr);
+#pragma unroll
+    for (uint32_t u = 0; u < PB_ITEMS; u++)
+      if (bk[u] == b) perm[at++] = i0 + u;
+  }
+}
+
 // Bucket of each key among ns ascending splitters (number of splitters <= key)
 // as a sort key, and the bucket sizes.
 __global__ __launch_bounds__(256) void k_bucket(const uint64_t *__restrict__ keys, uint64_t m,
@@ -5384,18 +5478,41 @@ int gather_impl(cw_ctx *c, const void *src, const uint32_t *idx, uint64_t m, uin
   return check_launch(c, "gather");
 }
 
+// counts: host memory (the call waits for it), or device memory when
+// dev_counts (nothing waits: the caller's next collective reads it in order)
 int partition_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t m64, const uint64_t *split,
-                        uint32_t ns, uint32_t *perm, uint64_t *counts) {
+                        uint32_t ns, uint32_t *perm, uint64_t *counts, bool dev_counts = false) {
   if (ns > 1023) return fail(c, "partition: at most 1023 splitters");
   if (!counts) return fail(c, "null counts");
   if (m64 == 0) {
-    memset(counts, 0, (size_t)(ns + 1) * 8);
+    if (dev_counts) HIPCHK(c, hipMemsetAsync(counts, 0, (size_t)(ns + 1) * 8, c->stream));
+    else memset(counts, 0, (size_t)(ns + 1) * 8);
     return 0;
   }
   if (!keys || !perm || (ns && !split)) return fail(c, "null array");
   if (m64 >= 0xFFFFFFFFull) return fail(c, "too many keys: %llu", (unsigned long long)m64);
   const uint32_t m = (uint32_t)m64;
   HIPCHK(c, hipSetDevice(c->device));
+  if (ns + 1 <= PB_MAX) {  // few buckets: counts, one scan, an ordered scatter
+    const uint32_t nblk = (m + PB_CHUNK - 1) / PB_CHUNK;
+    uint32_t *bcnt = scratch_t<uint32_t>(c, "pb_cnt", (size_t)(ns + 1) * nblk);
+    unsigned long long *dc = dev_counts ? reinterpret_cast<unsigned long long *>(counts)
+                                        : scratch_t<unsigned long long>(c, "pt_counts", ns + 1);
+    if (!bcnt || !dc) return fail(c, "out of device memory (partition)");
+    {
+      Launch L(c, "bucket", (double)m * 8 * 2 + (double)m * 4);
+      hipLaunchKernelGGL(k_pb_count, dim3(nblk), dim3(PB_NT), 0, c->stream, keys, m, split, ns, bcnt,
+                         nblk);
+      hipLaunchKernelGGL(k_pb_scan, dim3(1), dim3(1024), 0, c->stream, bcnt, nblk, ns, dc);
+      hipLaunchKernelGGL(k_pb_scatter, dim3(nblk), dim3(PB_NT), 0, c->stream, keys, m, split, ns, bcnt,
+                         nblk, perm);
+    }
+    if (check_launch(c, "bucket")) return -1;
+    if (dev_counts) return 0;
+    HIPCHK(c, hipMemcpyAsync(counts, dc, (size_t)(ns + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return 0;
+  }
   const uint64_t off[2] = {0, m64};
   if (ensure_tables(c, 1, off)) return -1;
   uint64_t *bk = scratch_t<uint64_t>(c, "pt_bucket", m), *kA = scratch_t<uint64_t>(c, "skA", m);
@@ -5416,6 +5533,10 @@ int partition_keys_impl(cw_ctx *c, const uint64_t *keys, uint64_t m64, const uin
                            0, m, &ko, &vo))
     return -1;
   if (vo != perm) HIPCHK(c, hipMemcpyAsync(perm, vo, (size_t)m * 4, hipMemcpyDeviceToDevice, c->stream));
+  if (dev_counts) {
+    HIPCHK(c, hipMemcpyAsync(counts, dc, (size_t)(ns + 1) * 8, hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+  }
   HIPCHK(c, hipMemcpyAsync(counts, dc, (size_t)(ns + 1) * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return 0;
@@ -6218,6 +6339,16 @@ int cw_partition_keys(cw_ctx *c, const uint64_t *keys, uint64_t m, const uint64_
   if (!c) return -1;
   c->err.clear();
   if (partition_keys_impl(c, keys, m, splitters, n_split, perm, counts)) return -1;
+  return c->prof ? collect_prof(c) : 0;
+}
+
+int cw_partition_keys_dev(cw_ctx *c, const uint64_t *keys, uint64_t m, const uint64_t *splitters,
+                          uint32_t n_split, uint32_t *perm, uint64_t *counts) {
+  if (!c) return -1;
+  c->err.clear();
+  HIPCHK(c, hipSetDevice(c->device));
+  if (partition_keys_impl(c, keys, m, splitters, n_split, perm, counts, true)) return -1;
+  if (!c->async) HIPCHK(c, hipStreamSynchronize(c->stream));
   return c->prof ? collect_prof(c) : 0;
 }
 

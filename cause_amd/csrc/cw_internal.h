@@ -40,10 +40,17 @@ constexpr uint32_t NSC_UP = 0x80000000u;         // nsc: no next sibling, low bi
 constexpr uint32_t SUCC_END = LINK_IDX;           // the last node in preorder
 constexpr uint32_t NX_END = 0xFFFFFFFFu;          // last sublist of a document
 // Wide links (the giant-document path, documents < 2^31 - 1 nodes): a u64 link
-// word = successor (low 32 bits; SUCCW_END for the last node) | the LINK_*
-// flags above << 32; thr entries = node | THRW_PEND when still pending.
+// word = successor (bits 0-30; SUCCW_END for the last node) | pending thread
+// (bit 31) | the value the emit writes for this node (bits 32-62: its input
+// index, so the emit gathers nothing) | renders (bit 63).  Splitters are
+// recomputed from the rank (split_node).  thr entries = node | THRW_PEND when
+// still pending.
 constexpr uint32_t SUCCW_END = 0x7FFFFFFFu;
 constexpr uint32_t THRW_PEND = 0x80000000u;
+__host__ __device__ constexpr uint64_t wide_link(uint32_t succ, bool pend, uint32_t val, bool vis) {
+  return (uint64_t)(succ & SUCCW_END) | (pend ? 0x80000000ull : 0ull) |
+         ((uint64_t)(val & 0x7FFFFFFFu) << 32) | (vis ? (1ull << 63) : 0ull);
+}
 constexpr uint32_t SLOT_IDX = 0x7FFFFFFFu;        // walk slot entry: rank | renders << 31
 
 constexpr uint8_t KIND_CLASS = 3, KIND_ROOT = 4, KIND_HIDE = 1, KIND_HHIDE = 2;

@@ -276,19 +276,20 @@ __global__ __launch_bounds__(256) void k_dist_succ(const uint8_t *__restrict__ k
 // and the thread words (a successor that is a pending thread: LINK_PEND, the
 // walk chases it through thr).
 __global__ __launch_bounds__(256) void k_linked_words(const uint32_t *__restrict__ sv,
-                                                      const uint32_t *__restrict__ th, uint32_t n,
-                                                      uint32_t log2k, uint64_t *__restrict__ link,
+                                                      const uint32_t *__restrict__ th,
+                                                      const uint32_t *__restrict__ val, uint32_t n,
+                                                      uint64_t *__restrict__ link,
                                                       uint32_t *__restrict__ thr) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= n) return;
   const uint32_t w = sv[r], t = th[r];
-  uint32_t succ = w & ~LINK_VIS, f = w & LINK_VIS;
+  uint32_t succ = w & ~LINK_VIS;
+  bool pend = false;
   if (succ == DIST_FROM_THR) {
     succ = t & ~THRW_PEND;
-    if (t & THRW_PEND) f |= LINK_PEND;
+    pend = (t & THRW_PEND) != 0;
   }
-  if (r == split_node(0, r >> log2k, log2k, n)) f |= LINK_SPLIT;
-  link[r] = (uint64_t)(succ < n ? succ : SUCCW_END) | ((uint64_t)f << 32);
+  link[r] = wide_link(succ < n ? succ : SUCCW_END, pend, val ? val[r] : r, (w & LINK_VIS) != 0);
   thr[r] = (t & THRW_PEND) ? t : (t < n ? t : SUCCW_END);
 }
 
@@ -817,8 +818,7 @@ int weave_linked_impl(cw_ctx *c, const cw_linked_list *in, cw_list_result *out) 
   if (!link || !thr) return fail(c, "out of device memory (linked, n=%u)", n);
   {
     Launch L(c, "linked", (double)n * (4 + 4 + 8 + 4));
-    hipLaunchKernelGGL(k_linked_words, DIST_GRID(n), in->succ, in->thr, n, c->tab.doc_log2k[0], link,
-                       thr);
+    hipLaunchKernelGGL(k_linked_words, DIST_GRID(n), in->succ, in->thr, in->val, n, link, thr);
   }
   if (dist_launch_ok(c, "linked")) return -1;
   if (weave_tail(c, 1, n, true, nullptr, nullptr, in->val, nullptr, nullptr, 0, out, nullptr, nullptr,

@@ -107,6 +107,19 @@ class HipOps:
         return perm, [int(x) for x in counts]
 
     @_on_stream
+    def partition_dev(self, keys, splitters):
+        """partition with the bucket sizes left on the device (int64 tensor of
+        len(splitters) + 1): no host readback."""
+        m = keys.numel()
+        perm = self._e(m, torch.int32)
+        sp = splitters.to(self.dev)
+        counts = torch.empty(sp.numel() + 1, dtype=torch.int64, device=self.dev)
+        self.w.partition_keys_dev(keys.data_ptr() if m else 0, m,
+                                  sp.data_ptr() if sp.numel() else 0, sp.numel(),
+                                  perm.data_ptr() if m else 0, counts.data_ptr())
+        return perm, counts
+
+    @_on_stream
     def lookup(self, sorted_keys, queries, base):
         """(global rank of each query or NOT_FOUND, CW_STATUS_DUP if the owner's
         sorted ids repeat one)."""
@@ -354,6 +367,18 @@ def _all_gather_ints(vals, group, device):
     return [[int(x) for x in o.cpu()] for o in out]
 
 
+def _gather_count_rows(counts, W, group):
+    """Every rank's first W bucket sizes (a device or host int64 tensor) as a
+    W x W host matrix: one all_gather and ONE readback -- both the exchange
+    sizes of a ruling-set round and its termination test (all zero)."""
+    c = counts[:W]
+    if dist.get_backend(group) == "gloo" and c.is_cuda:
+        c = c.cpu()
+    out = [torch.empty_like(c) for _ in range(W)]
+    dist.all_gather(out, c, group=group)
+    return torch.stack(out).cpu().tolist()
+
+
 def choose_splitters(samples, weights, W):
     """W-1 splitters from weighted samples (each stands for `weight` ids):
     splitter j = the first sample whose cumulative weight reaches j*N/W."""
@@ -479,16 +504,20 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
     own = ops.zeros32(2 * n)
     links = ops.zeros32(4 * M).view(M, 4)   # any walk may end on this rank
     nlinks, status = ops.zeros32(1), ops.zeros32(1)
-    walkers, m, rounds, sent = None, nr, 0, 0
+    walkers, m, rounds, sent, syncs = None, nr, 0, 0, 0
     while True:
         msg, key = ops.rs_walk(walkers, m, rlist, rbase, word, thr, base, own, links, nlinks,
                                status)
         rounds += 1
         if W == 1:
             break
-        perm, counts = ops.partition(key, split_t)   # W + 1 buckets: the last stopped here
-        send = counts[:W]
-        mat = _all_gather_ints(send, group, dev)
+        # W + 1 buckets (the last: walks that stopped here); the sizes stay on
+        # the device until the all_gather, whose one readback is both the
+        # exchange's split sizes and the termination test
+        perm, counts = ops.partition_dev(key, split_t)
+        mat = _gather_count_rows(counts, W, group)
+        syncs += 1
+        send = mat[r]
         if not any(any(row) for row in mat):
             break
         if rounds > 2 * N + 4:
@@ -500,7 +529,8 @@ def _rank_ruling(ops, succ, thr, org, base, owns, group, dev, root, out, k, n_ow
                        [4 * x for x in recv], group).view(-1, 4)
         m = walkers.shape[0]
     del word, rlist, walkers
-    info = {"rulers": M, "ruler_k": k, "rounds": rounds, "messages": sent}
+    info = {"rulers": M, "ruler_k": k, "rounds": rounds, "messages": sent,
+            "syncs_per_round": syncs / rounds if rounds else 0.0}
     nl = int(nlinks[0])
     agg = _all_gather_ints([nl, int(status[0])], group, dev)
     bad = sum(v[0] for v in agg) != M or any(v[1] for v in agg)

@@ -341,6 +341,11 @@ int cw_lookup_keys(cw_ctx *ctx, const uint64_t *sorted, uint64_t n, const uint64
  * sizes.  Synchronous (the counts are read back). */
 int cw_partition_keys(cw_ctx *ctx, const uint64_t *keys, uint64_t m, const uint64_t *splitters,
                       uint32_t n_split, uint32_t *perm, uint64_t *counts);
+/* cw_partition_keys with counts[n_split + 1] in DEVICE memory: no host
+ * readback inside the call (the ruling set's rounds hand the counts to the
+ * next collective on the device; async contexts do not wait at all). */
+int cw_partition_keys_dev(cw_ctx *ctx, const uint64_t *keys, uint64_t m, const uint64_t *splitters,
+                          uint32_t n_split, uint32_t *perm, uint64_t *counts);
 
 /* dst[i] = src[idx[i]], elements of elem_size 1, 4, 8 or 16 bytes. */
 int cw_gather(cw_ctx *ctx, const void *src, const uint32_t *idx, uint64_t m, uint32_t elem_size,

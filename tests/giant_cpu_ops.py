@@ -29,6 +29,10 @@ class CpuOps:
         counts = np.bincount(b, minlength=splitters.numel() + 1)
         return torch.from_numpy(perm), [int(x) for x in counts]
 
+    def partition_dev(self, keys, splitters):
+        perm, counts = self.partition(keys, splitters)
+        return perm, torch.tensor(counts, dtype=torch.int64)
+
     def lookup(self, sorted_keys, queries, base):
         s, q = _u64(sorted_keys), _u64(queries)
         i = np.searchsorted(s, q)
