@@ -3865,10 +3865,13 @@ struct cw_ctx {
   struct MapPacks {                // k_map_pack's pack table, cached by collection layout
     std::vector<uint64_t> off;
     std::vector<uint32_t> doc0;
-    uint32_t dbits = 0, pk = 0;
+    uint32_t dbits = 0, pk = 0, dmax = 1;  // (dmax: most collections in one pack)
+    uint32_t epoch = 0, lb_packs = 0;      // look-back words' epoch (mappack.hip)
+    const void *lb = nullptr;
     uint64_t maxcoll = 0;          // the largest collection of the cached layout
     bool ok = false;
     bool same = false;             // this call's coll_offsets equal off (set by cw_weave_maps)
+    bool verify = false;           // ... taken on trust: compared while the kernel runs
   } mpack;
   uint32_t map_pack = 0;           // CW_MAP_PACK: 0 = the smallest pack that holds the largest
                                    // collection (512 / 128 threads, 1024 / 256, else 2048 / 512),
@@ -5601,10 +5604,21 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
                                         (unsigned long long)N64);
   // the layout of the previous call (validated then, its pack table cached):
   // one compare instead of the checks (10^6 collections: ~1 ms of host time
-  // a call otherwise)
-  c->mpack.same = c->mpack.off.size() == D + 1 &&
-                  memcmp(c->mpack.off.data(), bt->coll_offsets, (D + 1) * 8) == 0;
-  if (!c->mpack.same) {
+  // a call otherwise).  For device memory that compare runs while the map
+  // kernel does (c->mpack.verify, mappack.hip): the cached table is taken when
+  // the size and a few offsets agree, and a layout that then differs is woven
+  // again from a fresh table (every output rewritten).
+  c->mpack.verify = false;
+  if (dev && c->map_fused && c->mpack.ok && c->mpack.off.size() == D + 1 && D > 4096 &&
+      c->mpack.off[D] == bt->coll_offsets[D] && c->mpack.off[D / 2] == bt->coll_offsets[D / 2] &&
+      c->mpack.off[D / 3] == bt->coll_offsets[D / 3]) {
+    c->mpack.same = true;
+    c->mpack.verify = true;
+  } else {
+    c->mpack.same = c->mpack.off.size() == D + 1 &&
+                    memcmp(c->mpack.off.data(), bt->coll_offsets, (D + 1) * 8) == 0;
+  }
+  auto check_layout = [&]() -> int {
     const uint64_t *o = bt->coll_offsets;
     uint64_t back = 0, big = 0, mx = 0;
     for (uint64_t d = 0; d < D; d++) {  // branch-free: vectorizes
@@ -5617,7 +5631,9 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
     if (big)
       for (uint64_t d = 0; d < D; d++)
         if (o[d + 1] - o[d] >= LINK_IDX - 1) return fail(c, "collection %llu too large", (unsigned long long)d);
-  }
+    return 0;
+  };
+  if (!c->mpack.same && check_layout()) return -1;
   if (!res->seg_offsets || !res->seg_coll || !res->seg_key || !res->seg_active ||
       !res->seg_perm || !res->status)
     return fail(c, "every cw_map_result array is required");
@@ -5652,7 +5668,13 @@ int weave_maps_impl(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, int m
     HIPCHK(c, hipMemcpy((void *)kind, bt->kind, N, hipMemcpyHostToDevice));
   }
   if (c->map_fused) {  // small collections: one kernel (mappack.hip)
-    const int rc = weave_maps_packed(c, bt, res, dev, id, cause, cis, kind);
+    int rc = weave_maps_packed(c, bt, res, dev, id, cause, cis, kind);
+    if (rc == 2) {  // the speculated layout was not the cached one: check it, weave again
+      c->mpack.same = false;
+      c->mpack.verify = false;
+      if (check_layout()) return -1;
+      rc = weave_maps_packed(c, bt, res, dev, id, cause, cis, kind);
+    }
     if (rc <= 0) return rc;
   }
   // significant bits of the ids and of the causes (id keys, SURVEY F8c, are

@@ -35,6 +35,10 @@ constexpr uint16_t MP_CHAIN = 0xFFFEu;         // appended after the previous no
 constexpr uint16_t MP_ROOT_ID = 0xFFFDu;       // caused by the root id [0 "0" 0] (not a node)
 constexpr uint16_t ML_ABSENT = 0xFFFFu;        // literal fold: the cause is not in the key weave
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
+// look-back word: flags (2 bits) | the call's epoch (16 bits, LB_EPOCH) | count:
+// a word of an earlier call reads as "not published yet", so the words need
+// no clearing before each call (cw_ctx::mpack.epoch; cleared when it wraps)
+constexpr uint32_t LB_EPOCH = 46;
 
 // Stable LDS radix sort of the pack's wave-blocked items by the low `bits` of
 // ck (carrying val), 6 bits per sub-pass.  On return item u holds the element
@@ -77,7 +81,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     uint64_t *__restrict__ seg_offsets, uint32_t *__restrict__ seg_coll,
     uint64_t *__restrict__ seg_key, int64_t *__restrict__ seg_active,
     uint32_t *__restrict__ seg_perm, uint32_t *__restrict__ status, uint32_t *ctl,
-    unsigned long long *__restrict__ tprof, uint32_t mflags) {
+    unsigned long long *__restrict__ tprof, uint32_t mflags, uint32_t nd_max, uint32_t epoch) {
   // mflags (A/B knobs CW_MAP_DIR, CW_MAP_LBW, CW_MAP_RELAXED, CW_MAP_DIRJOIN):
   // bit 0 = sort 1 through the id directory where it fits, bit 1 = four
   // look-back windows a round trip, bit 2 = relaxed look-back atomics (the
@@ -106,10 +110,16 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   uint16_t *const VS = U16, *const I2J = U16 + PK, *const P16 = U16 + 2 * PK, *const Q = U16 + 3 * PK,
                   *const LQ = U16 + 4 * PK;
   __shared__ uint8_t K8[PK], KQ[PK];
-  __shared__ uint32_t dstart[PK + 1], dstat[PK];
+  // per collection of the pack (start, status): dynamic LDS sized by the most
+  // collections a pack of this batch holds, not PK -- 4 KB less a pack at 512
+  // nodes, 10 packs a CU instead of 8 (the kernel is latency-bound)
+  extern __shared__ uint32_t mp_dyn[];
+  uint32_t *const dstart = mp_dyn, *const dstat = mp_dyn + (nd_max + 1);
   __shared__ uint32_t wcnt[NT / 64][SUB_BINS], run[64], wtot[NT / 64];
   __shared__ uint32_t s_base;
   __shared__ unsigned long long s_or[2];
+  __shared__ unsigned long long s_kor;  // sort 2's key widths (step 2)
+  __shared__ uint32_t s_kcls;
   __shared__ uint8_t SLIT[PK];  // key weave woven by the literal fold (root-id / non-Lamport causes)
   uint16_t *SEG = reinterpret_cast<uint16_t *>(A), *SS = SEG + PK, *BEF = SS + PK, *WV = BEF + PK;
   uint16_t *PAR = reinterpret_cast<uint16_t *>(B), *EFF = PAR + PK;
@@ -136,6 +146,10 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   for (uint32_t i = tid; i <= nd; i += NT) dstart[i] = (uint32_t)(coll_off[d0 + i] - s0);
   for (uint32_t i = tid; i < nd; i += NT) dstat[i] = 0;
   if (tid < 2) s_or[tid] = 0;
+  if (tid == 0) {
+    s_kor = 0;
+    s_kcls = 0;
+  }
   __syncthreads();
   const uint64_t tmask = (1ull << token_bits) - 1;
 
@@ -266,6 +280,8 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // is a bit test and a popcount; P16 is written after a barrier then.
   const bool djoin = sorted && (mflags & 8);
   uint16_t pv[IT];
+  unsigned long long kor = 0;
+  uint32_t cor = 0;
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t i = wb_elem<IT>(u);
@@ -325,23 +341,45 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     }
     pv[u] = p;
     if (st) atomicOr(&dstat[dl], st);
-    ck[u] = fits ? (((uint64_t)dl << (W + 2)) | key) : 0ull;
+    kor |= key & ((1ull << W) - 1);
+    cor |= 1u << (uint32_t)(key >> W);
+    ck[u] = ((uint64_t)dl << (W + 2)) | key;
     val[u] = i;
+  }
+  // the widths sort 2 needs in THIS pack: the largest key value's bits, and
+  // the class field only when a key weave that is not a plain key occurs (an
+  // id key or the nil key; config 4's packs have none: 8 + 3 bits, two 6-bit
+  // passes instead of three)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    kor |= __shfl_xor(kor, o, 64);
+    cor |= __shfl_xor(cor, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    if (kor) atomicOr(&s_kor, kor);
+    atomicOr(&s_kcls, cor);
   }
   if (djoin) __syncthreads();  // (every directory lookup done before P16 is written)
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++)
     if (wb_elem<IT>(u) < len) P16[wb_elem<IT>(u)] = pv[u];
   __syncthreads();
+  const uint32_t W2 = s_kor ? 64 - __builtin_clzll(s_kor) : 1;  // (<= W)
+  const uint32_t CB = (s_kcls & ~1u) ? 2u : 0u, KS = W2 + CB;      // key field = class | value
+#pragma unroll
+  for (uint32_t u = 0; u < IT; u++) {
+    const uint64_t g = ck[u] & ((1ull << (W + 2)) - 1), kv = g & ((1ull << W) - 1), cl = g >> W;
+    ck[u] = fits ? (((ck[u] >> (W + 2)) << KS) | (cl << W2) | kv) : 0ull;
+  }
 
   stamp(1);
   // 3. stable sort by (collection, key): every key weave a run, id order kept
-  mp_sort<NT, IT>(ck, val, len, fits ? W + 2 + dbits : 1, A, VS, wcnt, run);
+  mp_sort<NT, IT>(ck, val, len, fits ? KS + dbits : 1, A, VS, wcnt, run);
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t q = wb_elem<IT>(u);
     if (q >= len) continue;
-    const uint32_t i = val[u], j = I2J[i], dl = (uint32_t)(ck[u] >> (W + 2));
+    const uint32_t i = val[u], j = I2J[i], dl = (uint32_t)(ck[u] >> KS);
     Q[i] = (uint16_t)q;
     LQ[q] = (uint16_t)(j - dstart[dl]);
     KQ[q] = K8[j] & KIND_CLASS;
@@ -370,8 +408,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   stamp(2);
   // 4. publish this pack's number of key weaves (its prefix comes after the
   // weave below, so the wait for earlier packs overlaps this pack's work)
+  const unsigned long long ep = (unsigned long long)epoch << LB_EPOCH;
   if (tid == 0) {
-    const unsigned long long w = (pk == 0 ? LB_INC : LB_AGG) | nseg;
+    const unsigned long long w = (pk == 0 ? LB_INC : LB_AGG) | ep | nseg;
     if (mflags & 4) __hip_atomic_store(lb + pk, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else __hip_atomic_store(lb + pk, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -395,7 +434,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     } else if (p == MP_ROOT_ID) {  // a child of the key weave's root, next to appended nodes
       SLIT[sg] = 1;
     } else if (p != MP_ROOT) {  // the cause node: same key, so same key weave
-      const uint32_t qc = Q[p], dl = (uint32_t)(ck[u] >> (W + 2));
+      const uint32_t qc = Q[p], dl = (uint32_t)(ck[u] >> KS);
       if (qc < st0 || qc >= en) {
         atomicOr(&dstat[dl], (uint32_t)CW_STATUS_INTERNAL);
       } else if (qc >= q) {  // the cause has a larger id: the literal fold
@@ -453,7 +492,11 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // then one run in weave order -- and a segmented exclusive prefix sum of
   // their subtree sizes over each run (VS, P16, dstart are free by now)
   {
-    constexpr uint64_t NOKEY = 0x3FFF;  // members of literal key weaves sort last
+    // keys (parent index << 1 | class), parent index < PK + key weaves <= 2 PK:
+    // SB bits (two 6-bit passes at PK = 512, three at 2048); members of literal
+    // key weaves sort last
+    constexpr uint32_t SB = 33 - __builtin_clz(2u * PK);
+    constexpr uint64_t NOKEY = (1ull << SB) - 1;
     uint64_t gk[IT];
     uint32_t gv[IT];
 #pragma unroll
@@ -468,7 +511,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       const uint32_t e = EFF[q], pidx = e ? SS[sg] + e - 1 : PK + sg;  // (PK + sg: the root)
       gk[u] = ((uint64_t)pidx << 1) | (is_special(KQ[q]) ? 0u : 1u);
     }
-    mp_sort<NT, IT, uint16_t>(gk, gv, len, 14, VS, P16, wcnt, run);
+    mp_sort<NT, IT, uint16_t>(gk, gv, len, SB, VS, P16, wcnt, run);
     // segmented inclusive prefix sums in registers: lanes by shuffles, the
     // wave's IT chunks of 64 in order, then the carry from earlier waves
     const uint32_t lane = tid & 63, wv = tid >> 6;
@@ -525,7 +568,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       x = EFF[mst[u] + x - 1];
     }
     if (pos < 1 || pos > mm[u]) {
-      atomicOr(&dstat[(uint32_t)(ck[u] >> (W + 2))], (uint32_t)CW_STATUS_INTERNAL);
+      atomicOr(&dstat[(uint32_t)(ck[u] >> KS)], (uint32_t)CW_STATUS_INTERNAL);
       continue;
     }
     WV[mst[u] + pos - 1] = (uint16_t)q;
@@ -633,9 +676,10 @@ __global__ __launch_bounds__(NT) void k_map_pack(
 #pragma unroll
         for (uint32_t k = 0; k < LBW; k++) {
           const int64_t q = q0 - 64 * (int64_t)k - lane;  // lane 0 of window 0 = the nearest
-          v[k] = !(q >= 0 && k < lbw) ? (k < lbw ? LB_INC : 0ull)
+          v[k] = !(q >= 0 && k < lbw) ? (k < lbw ? LB_INC | ep : 0ull)
                  : (mflags & 4) ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                 : __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+          if (((v[k] >> LB_EPOCH) & 0xFFFFull) != epoch) v[k] = 0;  // an earlier call's word
         }
         bool done = false, retry = false;  // (wave-uniform: ballots)
 #pragma unroll
@@ -661,9 +705,9 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       if (lane == 0)
       {
         if (mflags & 4)
-          __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(lb + pk, LB_INC | ep | (base + nseg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         else
-          __hip_atomic_store(lb + pk, LB_INC | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(lb + pk, LB_INC | ep | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (lane == 0) {
@@ -688,11 +732,11 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       const uint64_t goff = s0 + mst[u] + sbase + sg;
       seg_perm[goff + mpos[u]] = LQ[q];
       if (mr[u] == 1) {
-        const uint64_t g = ck[u] & ((1ull << (W + 2)) - 1), cls = g >> W;  // (W + 2 < 64)
+        const uint64_t g = ck[u] & ((1ull << KS) - 1), cls = g >> W2, kv = g & ((1ull << W2) - 1);
         seg_perm[goff] = 0xFFFFFFFFu;
         seg_offsets[sbase + sg] = goff;
-        seg_coll[sbase + sg] = d0 + (uint32_t)(ck[u] >> (W + 2));
-        seg_key[sbase + sg] = cls == 0 ? g : cls == 1 ? (CW_MAP_ID_KEY | (g & ((1ull << W) - 1))) : CW_NIL;
+        seg_coll[sbase + sg] = d0 + (uint32_t)(ck[u] >> KS);
+        seg_key[sbase + sg] = cls == 0 ? kv : cls == 1 ? (CW_MAP_ID_KEY | kv) : CW_NIL;
       }
     }
     for (uint32_t sg = tid; sg < nseg; sg += NT) seg_active[sbase + sg] = ACT[sg];
@@ -708,7 +752,9 @@ namespace {
 // cw_weave_maps through k_map_pack: every collection <= MPK nodes and every
 // pack's sort keys fit 63 bits (each pack finds its own key widths: no
 // reduction over the batch and no readback before the kernel).  Returns 1 when it does not apply (the caller takes
-// the general path), 0 on success, -1 on error.
+// the general path), 2 when the layout taken on trust (pc.verify) differs from
+// the cached one (the caller checks it and calls again), 0 on success, -1 on
+// error.
 int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, bool dev,
                       const uint64_t *id, const uint64_t *cause, const uint8_t *cis,
                       const uint8_t *kind) {
@@ -729,6 +775,7 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
     pc.doc0.clear();
     pc.ok = true;
     uint32_t dmax = 1;
+    pc.dmax = 1;
     for (uint64_t d = 0; d < D;) {
       const uint64_t a = d;
       while (d < D && off[d + 1] - off[a] <= PKN) d++;
@@ -741,6 +788,7 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
     }
     pc.doc0.push_back((uint32_t)D);
     pc.dbits = ceil_log2(dmax);
+    pc.dmax = dmax;
     if (pc.ok) {
       uint32_t *dp = scratch_t<uint32_t>(c, "mp_doc0", pc.doc0.size());
       uint64_t *dof = scratch_t<uint64_t>(c, "mp_off", D + 1);
@@ -780,18 +828,26 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
     if (!tprof) return fail(c, "out of device memory (tprof)");
     HIPCHK(c, hipMemsetAsync(tprof, 0, (size_t)P * 64, c->stream));
   }
-  HIPCHK(c, hipMemsetAsync(lb, 0, (size_t)P * 8, c->stream));
+  // a new epoch per call; the words are cleared only when the epoch wraps or
+  // the buffer was (re)allocated for more packs than it held
+  if (++pc.epoch >= 0xFFFF || lb != pc.lb || P > pc.lb_packs) {
+    HIPCHK(c, hipMemsetAsync(lb, 0, (size_t)P * 8, c->stream));
+    pc.epoch = 1;
+    pc.lb = lb;
+    pc.lb_packs = P;
+  }
   HIPCHK(c, hipMemsetAsync(ctl, 0, 16, c->stream));
   {
     // ids, causes, flags and kinds in; per node seg_perm, per key weave
     // offsets, collection, key, active node out
     Launch L(c, "m_pack", (double)N * (8 + 8 + 1 + 1 + 4) + (double)N * 0.42 * (4 + 8 + 4 + 8 + 8));
 #define CW_MAP_PACK_LAUNCH(PK_, NT_)                                                              \
-  hipLaunchKernelGGL((k_map_pack<PK_, NT_>), dim3(P), dim3(NT_), 0, c->stream, id, cause, cis, kind, \
+  hipLaunchKernelGGL((k_map_pack<PK_, NT_>), dim3(P), dim3(NT_), (size_t)(2 * pc.dmax + 1) * 4,       \
+                     c->stream, id, cause, cis, kind,                                                  \
                      (const uint64_t *)c->bufs["mp_off"].p, (const uint32_t *)c->bufs["mp_doc0"].p, \
                      (const uint64_t *)c->bufs["mp_s0"].p,                                             \
                      P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
-                     sp, st, ctl, tprof, c->map_flags)
+                     sp, st, ctl, tprof, c->map_flags, pc.dmax, pc.epoch)
     if (pc.pk == 512) CW_MAP_PACK_LAUNCH(512, 128);
     else if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
     else if (c->map_pack == 2) CW_MAP_PACK_LAUNCH(2048, 1024);
@@ -799,6 +855,9 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
 #undef CW_MAP_PACK_LAUNCH
   }
   if (check_launch(c, "map_pack")) return -1;
+  if (pc.verify &&
+      memcmp(pc.off.data(), off, (D + 1) * 8) != 0)  // (the kernel runs meanwhile)
+    return 2;  // another layout after all: the caller checks it and weaves again
   if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
   HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 12, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

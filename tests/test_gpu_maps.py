@@ -349,3 +349,45 @@ def test_device_memory_call_matches_host(weaver):
     np.testing.assert_array_equal(o["seg_perm"][:N + S].cpu().numpy().view(np.uint32),
                                   host.seg_perm)
     np.testing.assert_array_equal(o["status"].cpu().numpy().view(np.uint32), host.status)
+
+
+def test_device_calls_with_a_changed_layout_are_rechecked(weaver):
+    """Device-memory calls take the previous call's pack table on trust when
+    the collection count and a few offsets agree, and compare the whole layout
+    while the kernel runs: a layout that differs elsewhere (two neighbouring
+    collections trading nodes) is woven again from a fresh table."""
+    import torch
+
+    spec = gen.CONFIG4
+    lay, tb = spec.layout()
+    off, idk, ck, ci, kd = gen.generate_maps(spec, 0, 6000, nthreads=8)
+    D, N = len(off) - 1, len(idk)
+    # the same nodes, collections 10 and 11 re-split: every node of 11 joins 10
+    # except its last one (the offsets at D, D/2 and D/3 stay)
+    off2 = off.copy()
+    off2[11] = off[12] - 1
+    dev = torch.device("cuda", 0)
+    g = [torch.from_numpy(x.view(np.int64) if x.dtype == np.uint64 else x).to(dev)
+         for x in (idk, ck, ci, kd)]
+
+    def call(o_off):
+        o = {"seg_offsets": torch.zeros(N + 1, dtype=torch.int64, device=dev),
+             "seg_coll": torch.zeros(N, dtype=torch.int32, device=dev),
+             "seg_key": torch.zeros(N, dtype=torch.int64, device=dev),
+             "seg_active": torch.zeros(N, dtype=torch.int64, device=dev),
+             "seg_perm": torch.zeros(2 * N, dtype=torch.int32, device=dev),
+             "status": torch.zeros(D, dtype=torch.int32, device=dev)}
+        S = weaver.weave_maps_device(o_off, [x.data_ptr() for x in g], tb, lay.key_bits,
+                                     {k: v.data_ptr() for k, v in o.items()}, N)
+        return S, {k: v.cpu().numpy() for k, v in o.items()}
+
+    for o_off in (off, off2, off2, off):
+        S, h = call(o_off)
+        host = weaver.weave_maps(o_off, idk, ck, ci, kd, tb, lay.key_bits)
+        assert S == len(host.seg_key)
+        np.testing.assert_array_equal(h["seg_offsets"][:S + 1].view(np.uint64), host.seg_offsets)
+        np.testing.assert_array_equal(h["seg_coll"][:S].view(np.uint32), host.seg_coll)
+        np.testing.assert_array_equal(h["seg_key"][:S].view(np.uint64), host.seg_key)
+        np.testing.assert_array_equal(h["seg_active"][:S], host.seg_active)
+        np.testing.assert_array_equal(h["seg_perm"][:N + S].view(np.uint32), host.seg_perm)
+        np.testing.assert_array_equal(h["status"].view(np.uint32), host.status)
