@@ -174,6 +174,9 @@ def test_ruling_set_rounds_and_messages_at_w8():
     assert info["ruler_k"] == 16 and 0.04 < info["rulers"] / N < 0.09, info
     assert 0.3 < info["messages"] / N < 0.5, info
     assert 20 < info["rounds"] < 200, info
+    # one host readback a round: the all_gather of the bucket sizes is both the
+    # exchange's split sizes and the termination test
+    assert info["syncs_per_round"] <= 1.0, info
 
 
 def _dup_worker(rank, world, port, q):
