@@ -826,6 +826,101 @@ __global__ __launch_bounds__(256) void k_gd_first(const uint64_t *__restrict__ s
   }
 }
 
+// The same directory in ONE pass over the sorted ids (k_gd_first +
+// k_gd_set_sorted read them twice and wrote every entry twice, the second time
+// as scattered 4-byte words: 28 ms at 2e9 nodes).  A block takes GDB_KEYS
+// consecutive sorted ids and builds the entries they fall in in LDS -- one
+// slot per distinct entry, bits by LDS atomics, word 0 = the index of the
+// entry's first id -- then writes each as a whole 64-byte line.  Every entry
+// has one writer, the block holding its first id ("lead"): ids at the start
+// of a block that continue the previous block's entry are left to that block,
+// which reads ahead for them (<= GD_KEYS ids).  Entries between two ids get
+// word 0 = the next id's index from that id's thread, as in k_gd_first.
+constexpr uint32_t GDB_KEYS = 512;
+__global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ skey, uint32_t n,
+                                                  uint64_t E, uint32_t *__restrict__ dir,
+                                                  uint32_t *__restrict__ status) {
+  constexpr uint32_t KT = GDB_KEYS / 256;  // consecutive ids a thread
+  __shared__ uint32_t sbits[GDB_KEYS][GD_WORDS];
+  __shared__ uint64_t sent[GDB_KEYS];
+  __shared__ uint32_t wtot[4];
+  const uint32_t tid = threadIdx.x, i0 = blockIdx.x * GDB_KEYS;
+  const uint32_t i1 = min(i0 + GDB_KEYS, n);
+  auto ent = [&](uint64_t x) { return min(x / GD_KEYS, E - 1); };  // (ids past E: flagged)
+  for (uint32_t w = tid; w < GDB_KEYS * GD_WORDS; w += 256) (&sbits[0][0])[w] = 0;
+  uint64_t key[KT];
+  bool lead[KT];
+  uint32_t nl = 0, st = 0;
+  uint64_t prev = 0;  // the id before this thread's first
+  {
+    const uint32_t i = i0 + tid * KT;
+    if (i > 0 && i < i1) prev = skey[i - 1];
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < KT; k++) {
+    const uint32_t i = i0 + tid * KT + k;
+    lead[k] = false;
+    key[k] = 0;
+    if (i >= i1) continue;
+    key[k] = skey[i];
+    const uint64_t xp = k > 0 ? key[k - 1] : prev;
+    if (i > 0 && xp == key[k]) st |= CW_STATUS_DUP;
+    if (key[k] / GD_KEYS >= E) st |= CW_STATUS_INTERNAL;  // an id beyond key_bits
+    const uint64_t e = ent(key[k]);
+    lead[k] = i == 0 || ent(xp) != e;
+    if (lead[k]) {
+      nl++;
+      for (uint64_t x = i == 0 ? 0 : ent(xp) + 1; x < e; x++) {  // the gap before it
+        uint4 *q = reinterpret_cast<uint4 *>(dir + x * GD_WORDS);
+        q[0] = make_uint4(i, 0, 0, 0);
+        q[1] = q[2] = q[3] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  }
+  uint32_t nslot;
+  const uint32_t s0 = block_exscan<256>(nl, wtot, &nslot);  // (its barriers order the clear)
+  // an id's slot: the leads at or before it, less one; none: the previous
+  // block's entry (skipped)
+  uint32_t slot[KT], seen = s0;
+#pragma unroll
+  for (uint32_t k = 0; k < KT; k++) {
+    const uint32_t i = i0 + tid * KT + k;
+    if (lead[k]) {
+      sent[seen] = ent(key[k]);
+      sbits[seen][0] = i;
+      seen++;
+    }
+    slot[k] = seen > 0 && i < i1 ? seen - 1 : GDB_KEYS;
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < KT; k++)
+    if (slot[k] < GDB_KEYS && key[k] / GD_KEYS < E) {
+      const uint32_t b = (uint32_t)(key[k] % GD_KEYS);
+      atomicOr(&sbits[slot[k]][1 + (b >> 5)], 1u << (b & 31));
+    }
+  if (nslot > 0) {  // the next block's ids in this block's last entry
+    const uint64_t elast = sent[nslot - 1];
+    for (uint32_t j = i1 + tid; j < n && j < i1 + GD_KEYS; j += 256) {
+      const uint64_t x = skey[j];
+      if (ent(x) == elast && x / GD_KEYS < E) {
+        const uint32_t b = (uint32_t)(x % GD_KEYS);
+        atomicOr(&sbits[nslot - 1][1 + (b >> 5)], 1u << (b & 31));
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t w = tid; w < nslot * GD_WORDS; w += 256) {
+    const uint32_t s = w / GD_WORDS, wd = w % GD_WORDS;
+    dir[sent[s] * GD_WORDS + wd] = sbits[s][wd];
+  }
+  const uint64_t any = __ballot(st != 0);
+  if (any) {
+    for (int o = 32; o > 0; o >>= 1) st |= __shfl_xor(st, o, 64);
+    if ((threadIdx.x & 63) == 0) atomicOr(status, st);
+  }
+}
+
 // k_join for one giant document with the directory: each rank's cause and kind
 // gathered by input index (as k_join), the cause's rank from one directory
 // line instead of the bucket index and a search.
@@ -2333,8 +2428,22 @@ __global__ __launch_bounds__(256) void k_gsib(const uint32_t *__restrict__ key,
   if (last) ((g & 1) ? fcN : fcS)[e] = r;
   uint32_t ns = first ? 0u : val[i - 1];
   if (first && !(g & 1)) {  // oldest special: the newest non-special of e follows its group
+    // The two groups of e are adjacent (keys g, g | 1), so the end of the
+    // second is near: gallop forward from i, then bisect the last step.  (A
+    // bisection over [i, n) was ~log2 n dependent cache misses for every
+    // special group head -- the kernel's whole time at 2e9 nodes.)
     const uint32_t want = g | 1u;
-    uint32_t lo = i, hi = n;  // first position with key > want
+    uint32_t lo = i + 1, hi = n, step = 1;  // invariant: key[< lo] <= want
+    while (lo < n) {
+      const uint32_t p = n - lo > step - 1 ? lo + step - 1 : n - 1;
+      if (key[p] <= want) {
+        lo = p + 1;
+        step <<= 1;
+      } else {
+        hi = p;
+        break;
+      }
+    }
     while (lo < hi) {
       const uint32_t m = lo + ((hi - lo) >> 1);
       if (key[m] <= want) lo = m + 1; else hi = m;
@@ -2422,8 +2531,10 @@ __global__ __launch_bounds__(1024) void k_walk(
     const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ doc_Wcap,
     const uint32_t *__restrict__ walk_first, const uint64_t *__restrict__ slot_first,
     uint32_t *__restrict__ slots, uint32_t *__restrict__ wcnt, uint32_t *__restrict__ wnext,
-    uint32_t *__restrict__ dyn_ctr, uint32_t *__restrict__ status, uint32_t walk_span) {
+    uint32_t *__restrict__ dyn_ctr, uint32_t *__restrict__ status, uint32_t walk_span,
+    unsigned long long *__restrict__ wprof) {
   __shared__ uint32_t next_walker;
+  uint32_t n_steps = 0, n_pend = 0, n_hops = 0;  // (wprof: CW_TREE_PROF diagnostics)
   const uint32_t b = xcd_tile(blockIdx.x, gridDim.x), d = wblk_doc[b];
   const uint32_t W = doc_W[d], Wcap = doc_Wcap[d];
   const uint32_t w0 = wblk_w0[b], w1 = min(w0 + walk_span, W);
@@ -2452,8 +2563,24 @@ __global__ __launch_bounds__(1024) void k_walk(
     ent = x | (L & LINK_VIS);
     return L & ~LINK_IDX;
   };
+  // a finished sublist's {node count, next sublist}: wide (the one-list path,
+  // ranked by k_lvl_walk's random reads) one u64 word in wcnt's room, so a
+  // ranking step reads one line; narrow two arrays
+  auto put_sub = [&](uint32_t x, uint32_t cnt, uint32_t next) {
+    if (WIDE) {
+      reinterpret_cast<uint64_t *>(wcnt)[f + x] = cnt | (uint64_t)next << 32;
+    } else {
+      wcnt[f + x] = cnt;
+      wnext[f + x] = next;
+    }
+  };
   if (threadIdx.x == 0) next_walker = w0 + blockDim.x;
   __syncthreads();
+  // (one walker a thread by default, walk_span == blockDim.x: a refilling
+  // loop -- a lane takes the next walker as soon as its own ends, in this
+  // block or from a grid-wide pool -- was measured slower, 1.8 -> 5.4 ms at
+  // 6.7e7 nodes for spans of 4,096: the walkers in flight spread over a wider
+  // range of the list, and the line reuse between neighbouring walkers drops)
   for (uint32_t lw = w0 + threadIdx.x; lw < w1; lw = atomicAdd(&next_walker, 1u)) {
     const uint32_t v = split_node(d, lw, log2k, n);
     uint32_t sv, ev;
@@ -2464,8 +2591,11 @@ __global__ __launch_bounds__(1024) void k_walk(
     uint4 q = make_uint4(ev, 0u, 0u, 0u);
     for (uint32_t steps = 0;; steps++) {
       uint32_t u = sv;
+      n_steps++;
+      n_pend += (L & LINK_PEND) ? 1u : 0u;
       if (L & LINK_PEND)  // the successor is the thread of an ancestor: chase it
         for (uint32_t hop = 0; hop <= n; hop++) {
+          n_hops++;
           const uint32_t tv = thr[base + (u < n ? u : 0u)];
           bool pend;
           if (WIDE) {
@@ -2503,8 +2633,7 @@ __global__ __launch_bounds__(1024) void k_walk(
           atomicOr(&status[d], (uint32_t)CW_STATUS_INTERNAL);
           break;
         }
-        wcnt[f + x] = cap;
-        wnext[f + x] = y;
+        put_sub(x, cap, y);
         x = y;
         cnt = 0;
       }
@@ -2531,8 +2660,12 @@ __global__ __launch_bounds__(1024) void k_walk(
       if ((cnt & 3) > 1) dst[1] = q.y;
       if ((cnt & 3) > 2) dst[2] = q.z;
     }
-    wcnt[f + x] = cnt;
-    wnext[f + x] = nextsub;
+    put_sub(x, cnt, nextsub);
+  }
+  if (wprof) {
+    atomicAdd(&wprof[0], (unsigned long long)n_steps);
+    atomicAdd(&wprof[1], (unsigned long long)n_pend);
+    atomicAdd(&wprof[2], (unsigned long long)n_hops);
   }
 }
 
@@ -2612,18 +2745,17 @@ __global__ __launch_bounds__(256) void k_rank(const uint32_t *__restrict__ wcnt,
 // --- multi-level sublist ranking (one giant document) ----------------------------
 // The sublists form one linked list.  A level: every K-th element below
 // Wsplit starts a walker that follows the links to the next such element,
-// recording for each element it passes its walker, and the prefix sums (a:
-// nodes, b: sublists) before it inside the walk; per walker the sums and the
-// next walker.  Levels repeat until <= 8192 walkers remain, which one
-// workgroup ranks in LDS (k_sup_rank); k_lvl_apply hands the bases back down.
-__global__ __launch_bounds__(256) void k_lvl_walk(const uint32_t *__restrict__ ca,
-                                                  const uint32_t *__restrict__ cb,
-                                                  const uint32_t *__restrict__ nxt, uint32_t Wsplit,
+// recording for each element it passes {its walker, the nodes and sublists
+// before it inside the walk}; per walker {nodes, sublists, next walker}.
+// Levels repeat until <= SUP_MAX walkers remain, which one workgroup ranks in
+// LDS (k_sup_rank); k_lvl_apply hands the bases back down.  Each record is one
+// word (the sublists: k_walk's u64 {nodes, next}; a level's walkers: uint4),
+// so a walker's step reads one random line and writes one: the 2e9-node list
+// has 1.25e8 sublists, and three separate arrays each way cost six.
+template <bool SUBL>
+__global__ __launch_bounds__(256) void k_lvl_walk(const void *__restrict__ in, uint32_t Wsplit,
                                                   uint32_t Wall, uint32_t K, uint32_t S,
-                                                  uint32_t *__restrict__ sup, uint32_t *__restrict__ pa,
-                                                  uint32_t *__restrict__ pb, uint32_t *__restrict__ sa,
-                                                  uint32_t *__restrict__ sb,
-                                                  uint32_t *__restrict__ snext,
+                                                  uint4 *__restrict__ pos, uint4 *__restrict__ wout,
                                                   uint32_t *__restrict__ status,
                                                   const uint32_t *__restrict__ dyn, uint32_t Wstat) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2633,12 +2765,21 @@ __global__ __launch_bounds__(256) void k_lvl_walk(const uint32_t *__restrict__ c
   if (dyn) Wall = min(Wstat + dyn[0], Wall);
   uint32_t x = q * K, acc = 0, cnt = 0, nq = NX_END;
   for (uint32_t steps = 0; steps <= Wall; steps++) {
-    sup[x] = q;
-    pa[x] = acc;
-    pb[x] = cnt;
-    acc += ca[x];
-    cnt += cb ? cb[x] : 1u;
-    const uint32_t nx = nxt[x];
+    uint32_t a, b, nx;
+    if (SUBL) {
+      const uint64_t v = static_cast<const uint64_t *>(in)[x];
+      a = (uint32_t)v;
+      b = 1;
+      nx = (uint32_t)(v >> 32);
+    } else {
+      const uint4 v = static_cast<const uint4 *>(in)[x];
+      a = v.x;
+      b = v.y;
+      nx = v.z;
+    }
+    pos[x] = make_uint4(q, acc, cnt, 0u);
+    acc += a;
+    cnt += b;
     if (nx == NX_END) break;
     if (nx >= Wall) {
       atomicOr(&status[0], (uint32_t)CW_STATUS_INTERNAL);
@@ -2650,30 +2791,44 @@ __global__ __launch_bounds__(256) void k_lvl_walk(const uint32_t *__restrict__ c
     }
     x = nx;
   }
-  sa[q] = acc;
-  sb[q] = cnt;
-  snext[q] = nq;
+  wout[q] = make_uint4(acc, cnt, nq, 0u);
 }
 
-// Bases of a level's elements from their walker's bases.  order != nullptr
-// (the sublist level): sbase = node base, order[sublist base] = element.
-__global__ __launch_bounds__(256) void k_lvl_apply(const uint32_t *__restrict__ sup,
-                                                   const uint32_t *__restrict__ pa,
-                                                   const uint32_t *__restrict__ pb,
-                                                   const uint32_t *__restrict__ ba,
-                                                   const uint32_t *__restrict__ bb, uint32_t Wall,
-                                                   uint32_t *__restrict__ oa, uint32_t *__restrict__ ob,
-                                                   uint32_t *__restrict__ order,
+// Bases of a level's elements from their walker's: walker q's {node base, tour
+// index} from `base` (uint2) or, for the top level, k_sup_rank's nb / tb.
+// pos == nullptr: the elements are the top level's walkers themselves.
+// erec != nullptr (the sublist level): erec[tour index] = {sublist, node base,
+// node count} -- what the emit reads, in tour order; otherwise out[x].
+__global__ __launch_bounds__(256) void k_lvl_apply(const uint4 *__restrict__ pos,
+                                                   const uint32_t *__restrict__ nb,
+                                                   const uint32_t *__restrict__ tb,
+                                                   const uint2 *__restrict__ base,
+                                                   const uint64_t *__restrict__ wl, uint32_t Wall,
+                                                   uint2 *__restrict__ out, uint4 *__restrict__ erec,
                                                    const uint32_t *__restrict__ dyn, uint32_t Wstat) {
   const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
   if (dyn) Wall = min(Wstat + dyn[0], Wall);  // walkers in use (Wall: the capacity)
   if (x >= Wall) return;
-  const uint32_t q = sup[x], va = ba[q] + pa[x], vb = bb[q] + pb[x];
-  oa[x] = va;
-  if (order) {
-    if (vb < Wall) order[vb] = x;
+  uint32_t q = x, pa = 0, pb = 0;
+  if (pos) {
+    const uint4 P = pos[x];
+    q = P.x;
+    pa = P.y;
+    pb = P.z;
+  }
+  uint32_t va, vb;
+  if (base) {
+    const uint2 B = base[q];
+    va = B.x + pa;
+    vb = B.y + pb;
   } else {
-    ob[x] = vb;
+    va = nb[q] + pa;
+    vb = tb[q] + pb;
+  }
+  if (erec) {
+    if (vb < Wall) erec[vb] = make_uint4(x, va, (uint32_t)wl[x], 0u);
+  } else {
+    out[x] = make_uint2(va, vb);
   }
 }
 
@@ -2681,7 +2836,8 @@ constexpr uint32_t SUP_MAX = 8192;  // elements k_sup_rank ranks in LDS (12 B ea
 
 __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ scnt,
                                                    const uint32_t *__restrict__ ssub,
-                                                   const uint32_t *__restrict__ snext, uint32_t S2,
+                                                   const uint32_t *__restrict__ snext, uint32_t stride,
+                                                   uint32_t S2,
                                                    uint32_t n, uint32_t Weff, uint32_t *__restrict__ nb,
                                                    uint32_t *__restrict__ tb,
                                                    uint32_t *__restrict__ status,
@@ -2703,9 +2859,9 @@ __global__ __launch_bounds__(1024) void k_sup_rank(const uint32_t *__restrict__ 
   }
   uint32_t *nx = sm, *cn = sm + S2, *sb = sm + 2 * S2;
   for (uint32_t i = threadIdx.x; i < S2; i += blockDim.x) {
-    nx[i] = snext[i];
-    cn[i] = scnt[i];
-    sb[i] = ssub ? ssub[i] : 1u;
+    nx[i] = snext[(size_t)i * stride];  // (stride: the fields of packed records)
+    cn[i] = scnt[(size_t)i * stride];
+    sb[i] = ssub ? ssub[(size_t)i * stride] : 1u;
   }
   __syncthreads();
   for (uint32_t round = 0; (1u << round) < 2 * S2; round++) {
@@ -2751,7 +2907,7 @@ __global__ __launch_bounds__(256) void k_emit(
     const uint32_t *__restrict__ slots, const uint64_t *__restrict__ slot_first,
     const uint32_t *__restrict__ wcnt, const uint32_t *__restrict__ sbase,
     const uint32_t *__restrict__ order, const uint32_t *__restrict__ sval,
-    const uint32_t *__restrict__ eblk_doc,
+    const uint4 *__restrict__ erec, const uint32_t *__restrict__ eblk_doc,
     const uint32_t *__restrict__ eblk_x0, const uint32_t *__restrict__ walk_first,
     const uint32_t *__restrict__ doc_W, const uint32_t *__restrict__ dyn_ctr,
     const uint32_t *__restrict__ doc_log2cap, const uint32_t *__restrict__ doc_off,
@@ -2771,12 +2927,16 @@ __global__ __launch_bounds__(256) void k_emit(
   const uint32_t ti = eblk_x0[b] + threadIdx.x;  // tour index
   uint32_t nvis = 0, cnt = 0, p0 = 0;
   bool bad = false;
-  const uint32_t x = ti < Weff ? order[f + ti] : 0u;
+  // erec (one giant document): {sublist, node base, count} in tour order, read
+  // coalesced; otherwise the sublist from order and its tables
+  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+  if (erec && ti < Weff) rec = erec[f + ti];
+  const uint32_t x = ti < Weff ? (erec ? rec.x : order[f + ti]) : 0u;
   const uint4 *sl4 = nullptr;
   if (ti < Weff) {
     if (x < Weff) {
-      cnt = wcnt[f + x];
-      p0 = sbase[f + x];
+      cnt = erec ? rec.z : wcnt[f + x];
+      p0 = erec ? rec.y : sbase[f + x];
       sl4 = reinterpret_cast<const uint4 *>(slots + slot_first[d] + ((size_t)x << log2cap));
       if (p0 + cnt > n || cnt > cap) bad = true;
     } else {
@@ -3819,7 +3979,7 @@ struct cw_ctx {
   bool tab_on_device = false;
   bool last_giant = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
-  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, min_log2k = 5,
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
@@ -4194,7 +4354,10 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
   const uint32_t D = (uint32_t)(t.doc_off.size() - 1);
   uint32_t shift = shift0;
   for (int p = 0; p < passes; p++) {
-    const uint32_t dbits = bits / passes + ((uint32_t)p < bits % passes ? 1u : 0u);
+    // the wider digits last: keys that arrive nearly sorted (the giant path's
+    // group keys, parent ~ rank) spread over every bin only in the low pass,
+    // whose tile runs are then longer (2 keys a bin and tile at 11 bits)
+    const uint32_t dbits = bits / passes + ((uint32_t)p >= passes - bits % passes ? 1u : 0u);
     const uint32_t nb = 1u << dbits;
     const uint32_t sub0 = dbits <= SUB_BITS ? dbits : (dbits + 1) / 2;
     snprintf(nm, sizeof nm, "%s_hist", tag);
@@ -4311,7 +4474,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   if (hbm_walk) {
     slots = scratch_t<uint32_t>(c, "slots", t.slots);
     dyn_ctr = scratch_t<uint32_t>(c, "dyn_ctr", D);
-    wcnt = scratch_t<uint32_t>(c, "wcnt", t.Wtot);
+    // (one giant document: u64 {count, next} words, see k_walk)
+    wcnt = scratch_t<uint32_t>(c, "wcnt", (giant ? 2 : 1) * (size_t)t.Wtot);
     wnext = scratch_t<uint32_t>(c, "wnext", t.Wtot);
     sbase = scratch_t<uint32_t>(c, "sbase", t.Wtot);
     order = scratch_t<uint32_t>(c, "order", t.Wtot);
@@ -4484,6 +4648,11 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   } else {
     // 6. walk: sublists of the preorder successor list
     if (!(giant && !linked)) HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));  // (k_geff did)
+    unsigned long long *wprof = nullptr;
+    if (c->tree_prof && giant) {
+      wprof = scratch_t<unsigned long long>(c, "wprof", 4);
+      HIPCHK(c, hipMemsetAsync(wprof, 0, 32, c->stream));
+    }
     {
       Launch L(c, "walk", (double)N * (4 + 4));
       hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
@@ -4491,52 +4660,90 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
                          dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
                          (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
-                         out->status, c->walk_span);
+                         out->status, c->walk_span, wprof);
     }
     if (check_launch(c, "walk")) return -1;
+    if (wprof) {
+      unsigned long long h[4];
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      HIPCHK(c, hipMemcpy(h, wprof, 32, hipMemcpyDeviceToHost));
+      fprintf(stderr, "walk profile: nodes %u steps %llu pending %llu thread hops %llu\n", N, h[0], h[1],
+              h[2]);
+    }
 
     // 7. rank sublists (+ max lamport-ts per document)
+    uint4 *erec = nullptr;
     if (giant) {
       // the walkers the walk added (pending threads) stay on the device: the
       // ranking kernels read W + dyn_ctr[0] themselves, no readback (sync) here
-      const uint32_t W = t.doc_W[0], Wcap = t.Wtot, Weff = Wcap;  // (Weff: an upper bound)
+      const uint32_t W = t.doc_W[0], Wcap = t.Wtot;
+      const uint64_t *wl = reinterpret_cast<const uint64_t *>(wcnt);  // k_walk<true>'s words
+      erec = scratch_t<uint4>(c, "g_erec", Wcap);
+      if (!erec) return fail(c, "out of device memory (rank)");
       if (Wcap <= SUP_MAX) {  // few sublists: one LDS ranking, no walk levels
-        Launch L(c, "rank", (double)Wcap * 20);
+        uint32_t *nbt = scratch_t<uint32_t>(c, "g_nbt", 2 * (size_t)Wcap);
+        if (!nbt) return fail(c, "out of device memory (rank)");
+        Launch L(c, "rank", (double)Wcap * 36);
         hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)Wcap * 12, c->stream, wcnt, nullptr,
-                           wnext, Wcap, N, Wcap, sbase, nullptr, out->status, order, dyn_ctr, W, Wcap);
+                           wcnt + 1, 2u, Wcap, N, Wcap, nbt, nbt + Wcap, out->status, nullptr, dyn_ctr, W,
+                           Wcap);
+        hipLaunchKernelGGL(k_lvl_apply, dim3((Wcap + 255) / 256), B256, 0, c->stream, nullptr, nbt,
+                           nbt + Wcap, nullptr, wl, Wcap, nullptr, erec, dyn_ctr, W);
       } else {
-      // level 2: every 16th static sublist; level 3 when more than 8192 walkers remain
-      const uint32_t K2 = 16, S2 = (W + K2 - 1) / K2;
-      uint32_t K3 = 1;
-      while ((S2 + K3 - 1) / K3 > SUP_MAX) K3 <<= 1;
-      const uint32_t S3 = (S2 + K3 - 1) / K3;
-      const bool three = K3 > 1;
-      uint32_t *sup2 = scratch_t<uint32_t>(c, "g_sup2", Weff), *pa2 = scratch_t<uint32_t>(c, "g_pa2", Weff);
-      uint32_t *pb2 = scratch_t<uint32_t>(c, "g_pb2", Weff), *l2 = scratch_t<uint32_t>(c, "g_l2", 6 * S2);
-      uint32_t *l3 = scratch_t<uint32_t>(c, "g_l3", 8 * S3 + 8 * S2);
-      if (!sup2 || !pa2 || !pb2 || !l2 || !l3) return fail(c, "out of device memory (multi-level rank)");
-      uint32_t *sa2 = l2, *sb2 = l2 + S2, *sn2 = l2 + 2 * S2, *ba2 = l2 + 3 * S2, *bb2 = l2 + 4 * S2;
-      uint32_t *sup3 = l3, *pa3 = l3 + S2, *pb3 = l3 + 2 * S2, *sa3 = l3 + 3 * S2,
-               *sb3 = sa3 + S3, *sn3 = sb3 + S3, *nb3 = sn3 + S3, *tb3 = nb3 + S3;
-      {
-        Launch L(c, "rank", (double)Weff * 24 + (double)S2 * 40);
-        hipLaunchKernelGGL(k_lvl_walk, dim3((S2 + 255) / 256), B256, 0, c->stream, wcnt, nullptr,
-                           wnext, W, Weff, K2, S2, sup2, pa2, pb2, sa2, sb2, sn2, out->status,
-                           dyn_ctr, W);
-        if (three) {
-          hipLaunchKernelGGL(k_lvl_walk, dim3((S3 + 255) / 256), B256, 0, c->stream, sa2, sb2, sn2,
-                             S2, S2, K3, S3, sup3, pa3, pb3, sa3, sb3, sn3, out->status, nullptr, 0u);
-          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S3 * 12, c->stream, sa3, sb3,
-                             sn3, S3, N, Weff, nb3, tb3, out->status, nullptr, dyn_ctr, W, Wcap);
-          hipLaunchKernelGGL(k_lvl_apply, dim3((S2 + 255) / 256), B256, 0, c->stream, sup3, pa3, pb3,
-                             nb3, tb3, S2, ba2, bb2, nullptr, nullptr, 0u);
-        } else {
-          hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)S2 * 12, c->stream, sa2, sb2,
-                             sn2, S2, N, Weff, ba2, bb2, out->status, nullptr, dyn_ctr, W, Wcap);
+        // levels: K = 16, until the walkers fit one LDS ranking; the last level
+        // takes a longer stride (<= 64) instead of one more level of launches
+        struct Lv { uint32_t E, Ws, K, S; size_t pos, wout, base; };
+        std::vector<Lv> lv;
+        size_t words = 0;  // (uint32 words of one scratch buffer, 16-byte units)
+        uint32_t E = Wcap, Ws = W;
+        while (lv.empty() || lv.back().S > SUP_MAX) {
+          const uint32_t need = (Ws + SUP_MAX - 1) / SUP_MAX;
+          uint32_t K = 16;
+          if (need <= 64) {
+            K = 1;
+            while (K < need) K <<= 1;
+          }
+          Lv v{E, Ws, K, (Ws + K - 1) / K, 0, 0, 0};
+          v.pos = words, words += 4 * (size_t)v.E;
+          v.wout = words, words += 4 * (size_t)v.S;
+          v.base = words, words += lv.empty() ? 0 : 4 * (((size_t)v.E + 1) / 2);
+          lv.push_back(v);
+          E = Ws = v.S;
         }
-        hipLaunchKernelGGL(k_lvl_apply, dim3((Weff + 255) / 256), B256, 0, c->stream, sup2, pa2, pb2,
-                           ba2, bb2, Weff, sbase, nullptr, order, dyn_ctr, W);
-      }
+        const size_t nbt_off = words;
+        words += 2 * (size_t)lv.back().S + 4;
+        uint32_t *lb = scratch_t<uint32_t>(c, "g_levels", words);
+        if (!lb) return fail(c, "out of device memory (multi-level rank)");
+        auto u4 = [&](size_t o) { return reinterpret_cast<uint4 *>(lb + o); };
+        auto u2 = [&](size_t o) { return reinterpret_cast<uint2 *>(lb + o); };
+        Launch L(c, "rank", (double)Wcap * 48 + (double)lv[0].S * 40);
+        for (size_t i = 0; i < lv.size(); i++) {
+          const Lv &v = lv[i];
+          if (i == 0)
+            hipLaunchKernelGGL(k_lvl_walk<true>, dim3((v.S + 255) / 256), B256, 0, c->stream,
+                               (const void *)wl, v.Ws, v.E, v.K, v.S, u4(v.pos), u4(v.wout), out->status,
+                               dyn_ctr, W);
+          else
+            hipLaunchKernelGGL(k_lvl_walk<false>, dim3((v.S + 255) / 256), B256, 0, c->stream,
+                               (const void *)u4(lv[i - 1].wout), v.Ws, v.E, v.K, v.S, u4(v.pos),
+                               u4(v.wout), out->status, nullptr, 0u);
+        }
+        const Lv &top = lv.back();
+        uint32_t *nb = lb + nbt_off, *tb = nb + top.S;
+        const uint32_t *tw = lb + top.wout;
+        hipLaunchKernelGGL(k_sup_rank, dim3(1), dim3(1024), (size_t)top.S * 12, c->stream, tw, tw + 1,
+                           tw + 2, 4u, top.S, N, Wcap, nb, tb, out->status, nullptr, dyn_ctr, W, Wcap);
+        for (size_t i = lv.size(); i-- > 0;) {
+          const Lv &v = lv[i];
+          const bool is_top = i + 1 == lv.size();
+          const uint2 *bq = is_top ? nullptr : u2(lv[i + 1].base);
+          if (i == 0)
+            hipLaunchKernelGGL(k_lvl_apply, dim3((v.E + 255) / 256), B256, 0, c->stream, u4(v.pos), nb,
+                               tb, bq, wl, v.E, nullptr, erec, dyn_ctr, W);
+          else
+            hipLaunchKernelGGL(k_lvl_apply, dim3((v.E + 255) / 256), B256, 0, c->stream, u4(v.pos), nb,
+                               tb, bq, nullptr, v.E, u2(v.base), nullptr, nullptr, 0u);
+        }
       }
       if (check_launch(c, "rank")) return -1;
     } else {
@@ -4553,7 +4760,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       // (giant: the slot entries hold the emitted values already, see k_walk)
       hipLaunchKernelGGL(k_emit, dim3(t.Be), B256, 0, c->stream, slots,
                          (const uint64_t *)c->bufs["t_slot_first"].p, wcnt, sbase, order,
-                         giant ? nullptr : sval,
+                         giant ? nullptr : sval, erec,
                          dev_tab(c, "t_eblk_doc"), dev_tab(c, "t_eblk_x0"), walk_first, doc_W,
                          dyn_ctr, dev_tab(c, "t_doc_log2cap"), doc_off, out->weave_perm, vis8,
                          out->visible_count, out->status);
@@ -4839,10 +5046,15 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     }
     if (gdir) {
       {
-        Launch L(c, "index", (double)N * 8 * 2 + (double)N / 15 * 64);
-        hipLaunchKernelGGL(k_gd_first, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir);
-        hipLaunchKernelGGL(k_gd_set_sorted, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir,
-                           out->status);
+        Launch L(c, "index", (double)N * 8 + (double)N / 15 * 64);
+        if (c->gd_build)
+          hipLaunchKernelGGL(k_gd_build, dim3((N + GDB_KEYS - 1) / GDB_KEYS), B256, 0, c->stream, skey, N,
+                             E, gdir, out->status);
+        else {
+          hipLaunchKernelGGL(k_gd_first, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir);
+          hipLaunchKernelGGL(k_gd_set_sorted, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E,
+                             gdir, out->status);
+        }
       }
       if (check_launch(c, "index")) return -1;
       // cause and kind packed in one word per input node when the ids leave
@@ -6203,6 +6415,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tl_mode = knob("CW_TL_MODE", 4);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
+  c->gd_build = knob("CW_GD_BUILD", 1);
   c->gpack = knob("CW_GPACK", 1);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);

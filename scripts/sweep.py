@@ -32,7 +32,9 @@ def main():
 
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
     lay = spec.layout()
+    t0 = time.time()
     off, idk, ck, kd = gen.generate(spec, 0, a.docs, nthreads=16)
+    print(f"generated {len(idk):,} nodes in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     N, D = len(idk), a.docs
     dev = torch.device("cuda", 0)
     g_id = torch.from_numpy(idk.view(np.int64)).to(dev)
@@ -75,6 +77,7 @@ def main():
                 torch.cuda.synchronize()
                 results[i].append(time.perf_counter() - t0)
             st = w.kernel_stats()
+            print(f"sweep {sweep} variant {i}: {min(results[i]) * 1e3:.2f} ms", file=sys.stderr, flush=True)
             for k, x in st.items():
                 stats.setdefault(i, {}).setdefault(k, []).append(x[1] / a.rounds)
             w.close()
