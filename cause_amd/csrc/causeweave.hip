@@ -430,7 +430,7 @@ __global__ __launch_bounds__(SORT_THREADS) void k_radix_scatter(
     const K kk = skey[j];
     const uint32_t d = (uint32_t)(kk >> shift) & dmask;
     const uint32_t dst = soff[d] + j - bstart[d];
-    keys_out[dst] = kk;
+    if (keys_out) keys_out[dst] = kk;  // (null: the caller wants the values only)
     vals_out[dst] = sval[j];
     if (inv) inv[s - lbase + sval[j]] = dst - (s - lbase);  // rank of each input node
   }
@@ -1557,10 +1557,22 @@ __device__ __forceinline__ bool front_doc(
   }
   __syncthreads();
   stamp(3);
-  for (uint32_t r = tid; r < n; r += NT) {
-    const uint32_t v = p16[r];
-    lane_at(svalD, r) = (VT)v;
-    if (skey) skey[base + r] = lane_at(idD, (v < n ? v : 0u));  // ids in rank order (yarns)
+  for (uint32_t r = tid; r < n; r += NT) lane_at(svalD, r) = (VT)p16[r];
+  if (skey) {
+    // the ids in rank order (the yarns sort by them) straight from the
+    // directory: group g's set bits are ids g * FR_GROUP_BITS + b, ranked from
+    // its word 0 on -- no gather of idD by input index (a random 8-byte read
+    // a node: the front end of a yarns call took 2.9x as long)
+    const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
+    for (uint32_t g = g0; g < g1; g++) {
+      const uint4 q = sdir[g];
+      uint32_t r = q.x;
+      const uint32_t wv[3] = {q.y, q.z, q.w};
+#pragma unroll
+      for (uint32_t k = 0; k < 3; k++)
+        for (uint32_t m = wv[k]; m != 0 && r < n; m &= m - 1)
+          skey[base + r++] = (uint64_t)g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
+    }
   }
   stamp(4);
   if (tprof && tid == 0)
@@ -4322,11 +4334,11 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 template <typename K>
 int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
-               K **kout, uint32_t **vout, uint32_t *inv = nullptr) {
+               K **kout, uint32_t **vout, uint32_t *inv = nullptr, uint32_t *vfinal = nullptr) {
   auto &t = c->tab;
   if (bits == 0) bits = 1;
   const uint32_t dbits_pack = ceil_log2(std::max(t.pack_dmax, 1u));
-  if (c->pack_sort && !inv && !t.pack_doc0.empty() && bits + dbits_pack <= 8 * sizeof(K)) {
+  if (c->pack_sort && !inv && !vfinal && !t.pack_doc0.empty() && bits + dbits_pack <= 8 * sizeof(K)) {
     // every document fits one tile: one in-LDS sort per pack of documents
     const uint32_t P = (uint32_t)t.pack_doc0.size() - 1;
     char nm[48];
@@ -4391,7 +4403,12 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     snprintf(nm, sizeof nm, "%s_scatter", tag);
     {
       const bool last = p + 1 == passes;
-      Launch L(c, nm, (double)N * (2 * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)) +
+      // vfinal: the last pass writes the values there and no keys
+      if (last && vfinal) {
+        ko = nullptr;
+        vo = vfinal;
+      }
+      Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)) +
                           (double)t.T * nb * 4);
       hipLaunchKernelGGL(k_radix_scatter<K>, dim3(t.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
                          ko, vo, dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
@@ -4880,9 +4897,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
                              out->visible_count, loc, tprof_f);
         };
-        if (tprof_f) {
-          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true, 4>, sval);
-          else launch(k_weave_doc<1024, 2048, uint16_t, true, 4>, sval16);
+        if (tprof_f) {  // (the default front-end depth, so the clocks are the product's)
+          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true, 4, 1>, sval);
+          else launch(k_weave_doc<1024, 2048, uint16_t, true, 4, 1>, sval16);
         } else if (c->tl_mode == 4) {
           auto fv = [&](auto fvc) {
             constexpr int F = decltype(fvc)::value;
@@ -5135,11 +5152,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       uint64_t *ykA = skey == skA ? skB : skA;
       uint32_t *yvA = sval == svA ? svB : svA;
       // (skey, sval) stay intact: ping-pong through the free id buffers + link/loc
+      // (the last pass writes yarn_perm itself, without the keys)
       if (radix_sort<uint64_t>(c, "yarns", skey, sval, ykA, yvA, link, nsc, bt->site_bits,
-                               bt->site_shift, N, &yk, &yv))
+                               bt->site_shift, N, &yk, &yv, nullptr, out->yarn_perm))
         return -1;
-      HIPCHK(c, hipMemcpyAsync(out->yarn_perm, yv, (size_t)N * 4, hipMemcpyDeviceToDevice,
-                               c->stream));
     }
     // ids of 64 significant bits: the documents with an id >= 2^63 (KEY_RANGE)
     if (key_bits >= 64) {
