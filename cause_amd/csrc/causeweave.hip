@@ -37,6 +37,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -2789,7 +2790,7 @@ __global__ __launch_bounds__(256) void k_lvl_walk(const void *__restrict__ in, u
       b = v.y;
       nx = v.z;
     }
-    pos[x] = make_uint4(q, acc, cnt, 0u);
+    if (pos) pos[x] = make_uint4(q, acc, cnt, 0u);  // (none on the sublist level: k_lvl_emit)
     acc += a;
     cnt += b;
     if (nx == NX_END) break;
@@ -2841,6 +2842,47 @@ __global__ __launch_bounds__(256) void k_lvl_apply(const uint4 *__restrict__ pos
     if (vb < Wall) erec[vb] = make_uint4(x, va, (uint32_t)wl[x], 0u);
   } else {
     out[x] = make_uint2(va, vb);
+  }
+}
+
+// The sublist level's emit records: each walker of the first level walks its
+// sublists a second time, now with its node base and tour index known (from
+// the level above, base, or the top level's nb / tb), and writes the record
+// of each sublist it passes -- {sublist, node base, node count} at tour index
+// base + k, consecutive for a walker.  A second pass of random 8-byte reads
+// instead of writing every sublist's {walker, offsets} to pos[x] and the
+// records from there: two scattered 16-byte stores a sublist, the slowest
+// access there is (k_lvl_walk's walkers pass a geometric number of sublists,
+// so per-walker slots overflow too often to be the alternative).
+__global__ __launch_bounds__(256) void k_lvl_emit(const uint64_t *__restrict__ wl, uint32_t Wsplit,
+                                                  uint32_t Wall, uint32_t K, uint32_t S,
+                                                  const uint32_t *__restrict__ nb,
+                                                  const uint32_t *__restrict__ tb,
+                                                  const uint2 *__restrict__ base,
+                                                  uint4 *__restrict__ erec,
+                                                  const uint32_t *__restrict__ dyn, uint32_t Wstat) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= S) return;
+  if (dyn) Wall = min(Wstat + dyn[0], Wall);
+  uint32_t va, vb;
+  if (base) {
+    const uint2 B = base[q];
+    va = B.x;
+    vb = B.y;
+  } else {
+    va = nb[q];
+    vb = tb[q];
+  }
+  uint32_t x = q * K;
+  for (uint32_t steps = 0; steps <= Wall; steps++) {
+    const uint64_t v = wl[x];
+    const uint32_t a = (uint32_t)v, nx = (uint32_t)(v >> 32);
+    if (vb < Wall) erec[vb] = make_uint4(x, va, a, 0u);
+    va += a;
+    vb++;
+    // (the first walk flagged a bad link; stop where it stopped)
+    if (nx == NX_END || nx >= Wall || (nx < Wsplit && nx % K == 0)) break;
+    x = nx;
   }
 }
 
@@ -3991,7 +4033,7 @@ struct cw_ctx {
   bool tab_on_device = false;
   bool last_giant = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
-  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, min_log2k = 5,
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, giant_log2cap = 5, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
@@ -4218,7 +4260,9 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     // one giant document: every slot overflow takes a sublist id from one
     // counter; 32-entry slots overflow ~8x less often (walk 2.8 -> 1.5 ms at
     // 6.7e7 nodes) for 8 more bytes a node, so below 2^30 nodes
-    if (giant && n < (1u << 30)) log2cap = std::max(log2cap, 5u);
+    // (CW_GIANT_LOG2CAP: the tests shrink it to send walks through many
+    // continuation sublists)
+    if (giant && n < (1u << 30)) log2cap = std::max(log2cap, c->giant_log2cap);
     // and 16-node splitter blocks: half the sublists to rank for a slightly
     // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8),
     // once there are walkers enough to fill the chip (config 1's 10^5 nodes:
@@ -4721,7 +4765,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
             while (K < need) K <<= 1;
           }
           Lv v{E, Ws, K, (Ws + K - 1) / K, 0, 0, 0};
-          v.pos = words, words += 4 * (size_t)v.E;
+          v.pos = words, words += lv.empty() ? 0 : 4 * (size_t)v.E;  // (sublist level: none)
           v.wout = words, words += 4 * (size_t)v.S;
           v.base = words, words += lv.empty() ? 0 : 4 * (((size_t)v.E + 1) / 2);
           lv.push_back(v);
@@ -4733,12 +4777,12 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
         if (!lb) return fail(c, "out of device memory (multi-level rank)");
         auto u4 = [&](size_t o) { return reinterpret_cast<uint4 *>(lb + o); };
         auto u2 = [&](size_t o) { return reinterpret_cast<uint2 *>(lb + o); };
-        Launch L(c, "rank", (double)Wcap * 48 + (double)lv[0].S * 40);
+        Launch L(c, "rank", (double)Wcap * 40 + (double)lv[0].S * 40);
         for (size_t i = 0; i < lv.size(); i++) {
           const Lv &v = lv[i];
-          if (i == 0)
+          if (i == 0)  // (no per-sublist records: k_lvl_emit walks again)
             hipLaunchKernelGGL(k_lvl_walk<true>, dim3((v.S + 255) / 256), B256, 0, c->stream,
-                               (const void *)wl, v.Ws, v.E, v.K, v.S, u4(v.pos), u4(v.wout), out->status,
+                               (const void *)wl, v.Ws, v.E, v.K, v.S, nullptr, u4(v.wout), out->status,
                                dyn_ctr, W);
           else
             hipLaunchKernelGGL(k_lvl_walk<false>, dim3((v.S + 255) / 256), B256, 0, c->stream,
@@ -4754,10 +4798,10 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
           const Lv &v = lv[i];
           const bool is_top = i + 1 == lv.size();
           const uint2 *bq = is_top ? nullptr : u2(lv[i + 1].base);
-          if (i == 0)
-            hipLaunchKernelGGL(k_lvl_apply, dim3((v.E + 255) / 256), B256, 0, c->stream, u4(v.pos), nb,
-                               tb, bq, wl, v.E, nullptr, erec, dyn_ctr, W);
-          else
+          if (i == 0) {
+            hipLaunchKernelGGL(k_lvl_emit, dim3((v.S + 255) / 256), B256, 0, c->stream, wl, v.Ws, v.E, v.K,
+                               v.S, nb, tb, bq, erec, dyn_ctr, W);
+          } else
             hipLaunchKernelGGL(k_lvl_apply, dim3((v.E + 255) / 256), B256, 0, c->stream, u4(v.pos), nb,
                                tb, bq, nullptr, v.E, u2(v.base), nullptr, nullptr, 0u);
         }
@@ -6444,6 +6488,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->front_fused = knob("CW_FRONT_FUSED", 1);
   c->tour_log2k = std::max(MIN_LOG2K, std::min(knob("CW_TOUR_LOG2K", 3), 12u));
   c->giant_log2k = std::max(MIN_LOG2K, std::min(knob("CW_GIANT_LOG2K", 4), 12u));
+  c->giant_log2cap = std::max(2u, std::min(knob("CW_GIANT_LOG2CAP", 5), 12u));
   c->fused = knob("CW_FUSED", 1);
   c->xfold = knob("CW_XFOLD", 0);
   c->front_u = knob("CW_FRONT_U", 1);

@@ -480,6 +480,22 @@ def test_giant_path_splitter_blocks(log2k, monkeypatch):
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
 
 
+def test_giant_path_many_continuation_sublists(monkeypatch):
+    """4-entry walk slots (CW_GIANT_LOG2CAP / CW_LOG2CAP = 2): every walk goes
+    on through several continuation sublists, so the first ranking level's
+    walkers pass more sublists than their 32-entry slots hold and the rest
+    take the overflow path (pos + the overflow list)."""
+    monkeypatch.setenv("CW_GIANT_MIN", "0")
+    monkeypatch.setenv("CW_GIANT_LOG2CAP", "2")
+    monkeypatch.setenv("CW_LOG2CAP", "2")
+    with abi.Weaver(0) as w:
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 1000)
+        off, idk, ck, kd = gen.generate(spec, 0, 1)
+        check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+        off, idk, ck, kd = gen.generate(gen.CONFIG1, 0, 1)
+        check_batch(w, off, idk, ck, kd, gen.CONFIG1.layout(), method=oracle.METHOD_LINKED)
+
+
 def test_few_large_documents_per_document_giant_path():
     """A batch of a few large documents goes through the giant path one
     document at a time (render bits merged at unaligned offsets); a small one
