@@ -370,10 +370,12 @@ def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
 # ------------------------------------------------- one giant document (config 5)
 # Giant-path front ends: the directory over the whole key range
 # (k_gd_place, small key ranges: the default here), the sorted-id directory
-# join (CW_GDIR=0: k_gd_first / k_gd_set_sorted / k_gpack / k_gjoin, config
-# 5's default), without the packed cause + kind word (CW_GPACK=0), and the
-# bucket index + searching join (CW_GJOIN=0).
+# join (CW_GDIR=0: k_gd_build / k_gpack / k_gjoin, config 5's default), the
+# same with the two-pass directory build (CW_GD_BUILD=0: k_gd_first /
+# k_gd_set_sorted), without the packed cause + kind word (CW_GPACK=0), and
+# the bucket index + searching join (CW_GJOIN=0).
 GIANT_FRONTS = {"gdplace": {}, "gjoin": {"CW_GDIR": "0"},
+                "gjoin-2pass-dir": {"CW_GDIR": "0", "CW_GD_BUILD": "0"},
                 "gjoin-unpacked": {"CW_GDIR": "0", "CW_GPACK": "0"},
                 "bucket": {"CW_GDIR": "0", "CW_GJOIN": "0"}}
 
