@@ -2401,31 +2401,204 @@ __global__ __launch_bounds__(NT) void k_tree_l(
 //            leaves the tile is left to the walk (LINK_PEND: thr[x] is chased).
 // (also clears k_gsib's last-child tables and zeroes two counters at r == 0:
 // fewer launches on the one-list path, where each costs a visible share)
+// tcnt != nullptr (the tile-local sibling links, k_glocal): per GL_TILE-rank
+// tile, the children whose effective parent lies in an earlier tile ("cross"
+// children, counted into tcnt), and no clearing of fcS / fcN (k_glocal writes
+// every entry).
+constexpr uint32_t GL_TILE = 2048;
 __global__ __launch_bounds__(256) void k_geff(const uint32_t *__restrict__ par,
                                               const uint8_t *__restrict__ skind, uint32_t n,
                                               uint32_t root_key, uint32_t *__restrict__ gk,
                                               uint32_t *__restrict__ fcS, uint32_t *__restrict__ fcN,
                                               uint32_t *__restrict__ zero_a,
-                                              uint32_t *__restrict__ zero_b) {
+                                              uint32_t *__restrict__ zero_b,
+                                              uint32_t *__restrict__ tcnt) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  fcS[r] = 0;
-  fcN[r] = 0;
-  if (r == 0) {
-    gk[0] = root_key;  // the root has no group: it sorts last
-    if (zero_a) *zero_a = 0;
-    if (zero_b) *zero_b = 0;
-    return;
-  }
-  const bool sp = is_special(skind[r]);
-  uint32_t c = par[r];
-  c = c < r ? c : 0u;  // clamps keep out-of-domain documents in bounds
-  if (!sp)
-    while (c != 0 && is_special(skind[c])) {
-      const uint32_t pc = par[c];
-      c = pc < c ? pc : 0u;
+  bool cross = false;
+  if (r < n) {
+    if (!tcnt) {
+      fcS[r] = 0;
+      fcN[r] = 0;
     }
-  gk[r] = (c << 1) | (sp ? 0u : 1u);
+    if (r == 0) {
+      gk[0] = root_key;  // the root has no group: it sorts last
+      if (zero_a) *zero_a = 0;
+      if (zero_b) *zero_b = 0;
+    } else {
+      const bool sp = is_special(skind[r]);
+      uint32_t c = par[r];
+      c = c < r ? c : 0u;  // clamps keep out-of-domain documents in bounds
+      if (!sp)
+        while (c != 0 && is_special(skind[c])) {
+          const uint32_t pc = par[c];
+          c = pc < c ? pc : 0u;
+        }
+      gk[r] = (c << 1) | (sp ? 0u : 1u);
+      cross = c < (r & ~(GL_TILE - 1));
+    }
+  }
+  if (tcnt) {  // (a block lies inside one tile: 256 | GL_TILE)
+    const uint64_t m = __ballot(cross);
+    __shared__ uint32_t bc;
+    if (threadIdx.x == 0) bc = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(&bc, (uint32_t)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x == 0 && bc) atomicAdd(&tcnt[blockIdx.x * blockDim.x / GL_TILE], bc);
+  }
+}
+
+// --- the tree's sibling links without sorting every node (round 4) ----------------
+// Two thirds of config-2/5 nodes have their effective parent inside their own
+// GL_TILE-rank tile.  A group (parent e, class) lists its members in rank
+// order: first the ones in e's own tile ("local", all in that one tile), then
+// the ones in later tiles ("cross").  So:
+//   k_glocal   per tile, in LDS: the local children sorted by (e - r0, class)
+//              (a 13-bit stable sort, cross children and the root last): each
+//              local child's next sibling = the previous local member (final:
+//              local members come first), each local group's last member into
+//              fcS / fcN (every entry of the tile written); the cross children
+//              compacted, in rank order, at the tile's offset (k_geff counted
+//              them, a scan placed them);
+//   sort       the cross children only, by group key (stable in rank);
+//   k_gcross_ns  a cross child's next sibling: the previous cross member of its
+//              group, or for the first one the group's last local member
+//              (fcS / fcN as k_glocal left them);
+//   k_gcross_fc  the last cross member of a group becomes its last child.
+// The oldest special's next sibling (the newest non-special of its parent,
+// weave-later?) is read by k_gthr from the final fcN.  Replaces the sort of all
+// group keys and k_gsib.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_glocal(const uint32_t *__restrict__ gk, uint32_t n,
+                                               const uint32_t *__restrict__ toff,
+                                               uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
+                                               uint32_t *__restrict__ fcN, uint32_t *__restrict__ ckey,
+                                               uint32_t *__restrict__ cval, uint32_t *__restrict__ mtot) {
+  constexpr uint32_t IT = GL_TILE / NT, SENT = 2 * GL_TILE;  // key 13 bits: SENT = not local
+  __shared__ uint16_t tkey[GL_TILE], tj[GL_TILE];
+  __shared__ uint32_t nsv[GL_TILE], fcl[2][GL_TILE];
+  __shared__ uint32_t wcnt[NT / 64][SUB_BINS], run[64];
+  const uint32_t t = blockIdx.x, r0 = t * GL_TILE, tid = threadIdx.x;
+  const uint32_t len = min(GL_TILE, n - r0);
+  for (uint32_t j = tid; j < GL_TILE; j += NT) fcl[0][j] = fcl[1][j] = 0;
+  uint32_t key[IT], val[IT], sd[IT], pos[IT], g[IT];
+  uint32_t ncross = 0;
+  bool crs[IT];
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = wb_elem<IT>(k), r = r0 + j;
+    g[k] = j < len ? gk[r] : 0xFFFFFFFFu;
+    const uint32_t e = g[k] >> 1;
+    const bool node = j < len && r > 0 && (uint64_t)g[k] < 2ull * n;
+    const bool loc = node && e >= r0;
+    crs[k] = node && !loc;
+    ncross += crs[k] ? 1u : 0u;
+    key[k] = loc ? (((e - r0) << 1) | (g[k] & 1u)) : SENT;
+    val[k] = j;
+  }
+  // the cross children, compacted in rank order: element j of the tile is
+  // item k of lane l of wave w with j = (w IT + k) 64 + l (wb_elem), so the
+  // 64-lane slots w IT + k are in element order -- a ballot a slot, a scan over
+  // the (GL_TILE / 64) slots
+  {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      // cross items before this one: all items of earlier (wave, k') slots plus
+      // the lanes below in this slot
+      const uint64_t m = __ballot(crs[k]);
+      const uint32_t lane = tid & 63, w = tid >> 6;
+      if (lane == 0) run[(w * IT + k) & 63] = (uint32_t)__popcll(m);  // (NT / 64 * IT <= 64)
+      pos[k] = lanes_below(m);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan over the slots in element order
+      const uint32_t v = tid < (NT / 64) * IT ? run[tid] : 0u;
+      uint32_t x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (tid >= (uint32_t)o) x += y;
+      }
+      run[tid] = x - v;
+      if (tid == 63 && t == gridDim.x - 1 && mtot) *mtot = toff[t] + x;
+    }
+    __syncthreads();
+    const uint32_t base = toff[t], w = tid >> 6;
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++)
+      if (crs[k]) {
+        const uint32_t o = base + run[w * IT + k] + pos[k];
+        ckey[o] = g[k];
+        cval[o] = r0 + wb_elem<IT>(k);
+      }
+    __syncthreads();
+  }
+  // stable sort of the tile by key (13 bits: 6 + 6 + 1)
+  for (uint32_t sh = 0; sh < 13; sh += SUB_BITS) {
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) sd[k] = (key[k] >> sh) & (SUB_BINS - 1);
+    rank_subdigit<NT, IT>(sd, len, min(SUB_BITS, 13u - sh), pos, wcnt, run);
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++)
+      if (wb_elem<IT>(k) < len) {
+        tkey[pos[k]] = (uint16_t)key[k];
+        tj[pos[k]] = (uint16_t)val[k];
+      }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      const uint32_t j = wb_elem<IT>(k);
+      if (j < len) {
+        key[k] = tkey[j];
+        val[k] = tj[j];
+      }
+    }
+    __syncthreads();
+  }
+  // sorted: tkey / tj hold the tile in (key, rank) order
+  for (uint32_t p = tid; p < len; p += NT) {
+    const uint32_t kk = tkey[p];
+    if (kk >= SENT) continue;
+    const uint32_t j = tj[p], e = r0 + (kk >> 1);
+    const bool first = p == 0 || tkey[p - 1] != kk, last = p + 1 == len || tkey[p + 1] != kk;
+    nsv[j] = first ? (NSC_UP | e) : r0 + tj[p - 1];
+    if (last) fcl[kk & 1][kk >> 1] = r0 + j;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < len; j += NT) {
+    const uint32_t r = r0 + j, gg = gk[r];  // (cached: this block read it)
+    const bool node = r > 0 && (uint64_t)gg < 2ull * n;
+    if (node && (gg >> 1) >= r0) nsc[r] = nsv[j];  // (cross children: k_gcross_ns)
+    fcS[r] = fcl[0][j];
+    fcN[r] = fcl[1][j];
+  }
+}
+
+// next sibling of each cross child (sorted by group key, stable in rank)
+__global__ __launch_bounds__(256) void k_gcross_ns(const uint32_t *__restrict__ key,
+                                                   const uint32_t *__restrict__ val,
+                                                   const uint32_t *__restrict__ mtot,
+                                                   uint32_t *__restrict__ nsc,
+                                                   const uint32_t *__restrict__ fcS,
+                                                   const uint32_t *__restrict__ fcN) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, m = *mtot;
+  if (i >= m) return;
+  const uint32_t g = key[i], r = val[i], e = g >> 1;
+  uint32_t ns;
+  if (i > 0 && key[i - 1] == g) ns = val[i - 1];
+  else ns = ((g & 1) ? fcN : fcS)[e];  // the group's last local member (or none)
+  nsc[r] = ns ? ns : (NSC_UP | e);
+}
+
+// ... and the last cross member of each group: its parent's last child
+__global__ __launch_bounds__(256) void k_gcross_fc(const uint32_t *__restrict__ key,
+                                                   const uint32_t *__restrict__ val,
+                                                   const uint32_t *__restrict__ mtot,
+                                                   uint32_t *__restrict__ fcS, uint32_t *__restrict__ fcN) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, m = *mtot;
+  if (i >= m) return;
+  const uint32_t g = key[i];
+  if (i + 1 == m || key[i + 1] != g) ((g & 1) ? fcN : fcS)[g >> 1] = val[i];
 }
 
 __global__ __launch_bounds__(256) void k_gsib(const uint32_t *__restrict__ key,
@@ -2486,8 +2659,16 @@ __global__ __launch_bounds__(NT) void k_gthr(const uint32_t *__restrict__ nsc,
     const uint32_t j = k * NT + tid, r = r0 + j;
     fcr[k] = flg[k] = 0;
     if (j >= len) continue;
-    const uint32_t fs = fcS[r], fn = fcN[r], ns = nsc[r];
+    const uint32_t fs = fcS[r], fn = fcN[r];
+    uint32_t ns = nsc[r];
     const bool sp = is_special(skind[r]);
+    // the oldest special child (no earlier special sibling) is followed by its
+    // parent's newest non-special (weave-later?); k_gsib patched it already,
+    // the tile-local links (k_glocal) leave it to this final fcN
+    if (sp && r != 0 && (ns & NSC_UP)) {
+      const uint32_t f = fcN[ns & ~NSC_UP];
+      if (f) ns = f;
+    }
     fcr[k] = fs ? fs : fn;
     uint64_t tv;
     if (r == 0) tv = RES | SUCCW_END;
@@ -4033,7 +4214,7 @@ struct cw_ctx {
   bool tab_on_device = false;
   bool last_giant = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
-  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, giant_log2cap = 5, min_log2k = 5,
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, giant_log2cap = 5, glocal = 1, glocal_min = 1u << 20, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
@@ -4375,14 +4556,26 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 // <= MAX_DIGIT bits (at least one pass).  Pass 0 reads (kin, vin) -- vin ==
 // nullptr means identity values -- and the passes ping-pong between (kA,vA)
 // and (kB,vB).
+// rt: the tiles of another array than the batch's (one device-sized list, the
+// giant tree's cross-tile children), instead of c->tab's
+struct RSTab {
+  uint32_t T, D;
+  const uint32_t *tile_start, *tile_doc, *doc_off, *tile_first;
+};
+
 template <typename K>
 int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
-               K **kout, uint32_t **vout, uint32_t *inv = nullptr, uint32_t *vfinal = nullptr) {
+               K **kout, uint32_t **vout, uint32_t *inv = nullptr, uint32_t *vfinal = nullptr,
+               const RSTab *rt = nullptr) {
   auto &t = c->tab;
+  const RSTab tt = rt ? *rt
+                      : RSTab{t.T, (uint32_t)(t.doc_off.size() - 1), dev_tab(c, "t_tile_start"),
+                              dev_tab(c, "t_tile_doc"), dev_tab(c, "t_doc_off"),
+                              dev_tab(c, "t_tile_first")};
   if (bits == 0) bits = 1;
   const uint32_t dbits_pack = ceil_log2(std::max(t.pack_dmax, 1u));
-  if (c->pack_sort && !inv && !vfinal && !t.pack_doc0.empty() && bits + dbits_pack <= 8 * sizeof(K)) {
+  if (c->pack_sort && !inv && !vfinal && !rt && !t.pack_doc0.empty() && bits + dbits_pack <= 8 * sizeof(K)) {
     // every document fits one tile: one in-LDS sort per pack of documents
     const uint32_t P = (uint32_t)t.pack_doc0.size() - 1;
     char nm[48];
@@ -4400,14 +4593,14 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
   }
   const uint32_t maxd = std::min<uint32_t>(c->max_digit, MAX_DIGIT);
   const int passes = (int)((bits + maxd - 1) / maxd);
-  uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)t.T * (1u << ((bits + passes - 1) / passes)));
+  uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)tt.T * (1u << ((bits + passes - 1) / passes)));
   if (!hist) return fail(c, "out of device memory (hist)");
   const K *ki = kin;
   const uint32_t *vi = vin;
   K *ko = kA;
   uint32_t *vo = vA;
   char nm[48];
-  const uint32_t D = (uint32_t)(t.doc_off.size() - 1);
+  const uint32_t D = tt.D;
   uint32_t shift = shift0;
   for (int p = 0; p < passes; p++) {
     // the wider digits last: keys that arrive nearly sorted (the giant path's
@@ -4418,30 +4611,30 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     const uint32_t sub0 = dbits <= SUB_BITS ? dbits : (dbits + 1) / 2;
     snprintf(nm, sizeof nm, "%s_hist", tag);
     {
-      Launch L(c, nm, (double)N * sizeof(K) + (double)t.T * nb * 4);
-      hipLaunchKernelGGL(k_radix_hist<K>, dim3(t.T), dim3(256), 0, c->stream, ki,
-                         dev_tab(c, "t_tile_start"), shift, dbits, hist);
+      Launch L(c, nm, (double)N * sizeof(K) + (double)tt.T * nb * 4);
+      hipLaunchKernelGGL(k_radix_hist<K>, dim3(tt.T), dim3(256), 0, c->stream, ki,
+                         tt.tile_start, shift, dbits, hist);
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scan", tag);
-    if (D == 1 && t.T > GSCAN_CHUNK) {
+    if (D == 1 && tt.T > GSCAN_CHUNK) {
       // one document of many tiles: chunked scan over all workgroups (up to
       // one chunk of tiles, the one-workgroup scan is a single launch instead
       // of four)
-      const uint32_t nc = (t.T + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
+      const uint32_t nc = (tt.T + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
       uint32_t *cs = scratch_t<uint32_t>(c, "gscan_cs", (size_t)nc * nb);
       uint32_t *tot = scratch_t<uint32_t>(c, "gscan_tot", nb);
       if (!cs || !tot) return fail(c, "out of device memory (scan)");
-      Launch L(c, nm, (double)t.T * nb * 12);
-      hipLaunchKernelGGL(k_gscan_colsum, dim3(nc), dim3(1024), 0, c->stream, hist, t.T, nb, cs);
+      Launch L(c, nm, (double)tt.T * nb * 12);
+      hipLaunchKernelGGL(k_gscan_colsum, dim3(nc), dim3(1024), 0, c->stream, hist, tt.T, nb, cs);
       hipLaunchKernelGGL(k_gscan_chunks, dim3((nb + 1023) / 1024), dim3(1024), 0, c->stream, cs, nc,
                          nb, tot);
       hipLaunchKernelGGL(k_gscan_bins, dim3(1), dim3(1024), 0, c->stream, tot, nb, 0u);
-      hipLaunchKernelGGL(k_gscan_apply, dim3(nc), dim3(1024), 0, c->stream, hist, t.T, nb, cs, tot);
+      hipLaunchKernelGGL(k_gscan_apply, dim3(nc), dim3(1024), 0, c->stream, hist, tt.T, nb, cs, tot);
     } else {
-      Launch L(c, nm, (double)t.T * nb * 8);
+      Launch L(c, nm, (double)tt.T * nb * 8);
       hipLaunchKernelGGL(k_radix_scan, dim3(D), dim3(1024), 0, c->stream, hist,
-                         dev_tab(c, "t_tile_first"), dev_tab(c, "t_doc_off"), dbits);
+                         tt.tile_first, tt.doc_off, dbits);
     }
     if (check_launch(c, nm)) return -1;
     snprintf(nm, sizeof nm, "%s_scatter", tag);
@@ -4453,10 +4646,10 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
         vo = vfinal;
       }
       Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)) +
-                          (double)t.T * nb * 4);
-      hipLaunchKernelGGL(k_radix_scatter<K>, dim3(t.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
-                         ko, vo, dev_tab(c, "t_tile_start"), dev_tab(c, "t_tile_doc"),
-                         dev_tab(c, "t_doc_off"), hist, shift, dbits, sub0,
+                          (double)tt.T * nb * 4);
+      hipLaunchKernelGGL(k_radix_scatter<K>, dim3(tt.T), dim3(SORT_THREADS), 0, c->stream, ki, vi,
+                         ko, vo, tt.tile_start, tt.tile_doc,
+                         tt.doc_off, hist, shift, dbits, sub0,
                          last ? inv : nullptr);
     }
     if (check_launch(c, nm)) return -1;
@@ -4564,21 +4757,78 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     }
     if (!gkA || !gkB || !gvA || !gvB || !gk) return fail(c, "out of device memory (giant tree)");
     const dim3 GN((N + 255) / 256);
+    const bool glocal = c->glocal && N >= c->glocal_min;
+    const uint32_t TL = (N + GL_TILE - 1) / GL_TILE;
+    uint32_t *tcnt = nullptr;
+    if (glocal) {
+      tcnt = scratch_t<uint32_t>(c, "gl_tcnt", (size_t)TL + 1);
+      if (!tcnt) return fail(c, "out of device memory (giant tree)");
+      HIPCHK(c, hipMemsetAsync(tcnt, 0, ((size_t)TL + 1) * 4, c->stream));
+    }
     {
-      Launch L(c, "geff", (double)N * (4 + 1 + 4));
+      Launch L(c, "geff", (double)N * (4 + 1 + 4) + (glocal ? 0.0 : (double)N * 8));
       // (the walk's counter and the emit's rendered count zeroed here)
       hipLaunchKernelGGL(k_geff, GN, B256, 0, c->stream, par, skind, N, root_key, gk, fcS, fcN,
-                         hbm_walk ? dyn_ctr : nullptr, out->visible_count);
+                         hbm_walk ? dyn_ctr : nullptr, out->visible_count, tcnt);
     }
     if (check_launch(c, "geff")) return -1;
-    uint32_t *gks, *gvs;
-    if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
-      return -1;
-    {
-      Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
-      hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
+    if (glocal) {
+      // cross children's offsets: an exclusive scan of the tile counts in place
+      // (the sort's chunked scan with one bin)
+      const uint32_t nc = (TL + GSCAN_CHUNK - 1) / GSCAN_CHUNK;
+      uint32_t *cs = scratch_t<uint32_t>(c, "gl_cs", (size_t)nc + 1);
+      uint32_t *aux = scratch_t<uint32_t>(c, "gl_aux", 4);
+      if (!cs || !aux) return fail(c, "out of device memory (giant tree)");
+      uint32_t *mtot = aux + 1;
+      {
+        Launch L(c, "glocal", (double)N * (4 + 4 + 8 + 4 + 8 * 0.34));
+        hipLaunchKernelGGL(k_gscan_colsum, dim3(nc), dim3(1024), 0, c->stream, tcnt, TL, 1u, cs);
+        hipLaunchKernelGGL(k_gscan_chunks, dim3(1), dim3(1024), 0, c->stream, cs, nc, 1u, aux);
+        hipLaunchKernelGGL(k_gscan_bins, dim3(1), dim3(1024), 0, c->stream, aux, 1u, 0u);
+        hipLaunchKernelGGL(k_gscan_apply, dim3(nc), dim3(1024), 0, c->stream, tcnt, TL, 1u, cs, aux);
+        hipLaunchKernelGGL(k_glocal<512>, dim3(TL), dim3(512), 0, c->stream, gk, N, tcnt, nsc, fcS, fcN,
+                           gkA, gvA, mtot);
+      }
+      if (check_launch(c, "glocal")) return -1;
+      // the cross children's count sizes their sort (one readback)
+      if (!c->pin_small) HIPCHK(c, hipHostMalloc((void **)&c->pin_small, 64, hipHostMallocDefault));
+      HIPCHK(c, hipMemcpyAsync(c->pin_small, mtot, 4, hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      const uint32_t M = c->pin_small[0];
+      if (M > N) return fail(c, "cross children %u > %u", M, N);
+      if (M) {
+        const uint32_t TR = (M + TILE - 1) / TILE;
+        std::vector<uint32_t> h((size_t)TR + 1 + TR + 2 + 2);
+        for (uint32_t i = 0; i <= TR; i++) h[i] = std::min(i * TILE, M);  // tile_start
+        for (uint32_t i = 0; i < TR; i++) h[TR + 1 + i] = 0;                // tile_doc
+        h[2 * TR + 1] = 0, h[2 * TR + 2] = M;                               // doc_off
+        h[2 * TR + 3] = 0, h[2 * TR + 4] = TR;                              // tile_first
+        uint32_t *dt = scratch_t<uint32_t>(c, "gl_rtab", h.size());
+        if (!dt) return fail(c, "out of device memory (giant tree)");
+        HIPCHK(c, hipMemcpy(dt, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+        const RSTab rt{TR, 1u, dt, dt + TR + 1, dt + 2 * TR + 1, dt + 2 * TR + 3};
+        uint32_t *gks, *gvs;  // (ping-pong through the input pair itself)
+        if (radix_sort<uint32_t>(c, "gsort", gkA, gvA, gkB, gvB, gkA, gvA, gbits, 0, M, &gks, &gvs,
+                                 nullptr, nullptr, &rt))
+          return -1;
+        {
+          Launch L(c, "gcross", (double)M * (8 + 4 + 4 + 8));
+          const dim3 GM((M + 255) / 256);
+          hipLaunchKernelGGL(k_gcross_ns, GM, B256, 0, c->stream, gks, gvs, mtot, nsc, fcS, fcN);
+          hipLaunchKernelGGL(k_gcross_fc, GM, B256, 0, c->stream, gks, gvs, mtot, fcS, fcN);
+        }
+        if (check_launch(c, "gcross")) return -1;
+      }
+    } else {
+      uint32_t *gks, *gvs;
+      if (radix_sort<uint32_t>(c, "gsort", gk, nullptr, gkA, gvA, gkB, gvB, gbits, 0, N, &gks, &gvs))
+        return -1;
+      {
+        Launch L(c, "gsib", (double)N * (4 + 4 + 4 + 4));
+        hipLaunchKernelGGL(k_gsib, GN, B256, 0, c->stream, gks, gvs, N, nsc, fcS, fcN);
+      }
+      if (check_launch(c, "gsib")) return -1;
     }
-    if (check_launch(c, "gsib")) return -1;
     {
       Launch L(c, "gthr", (double)N * (4 + 4 + 4 + 1 + 4 + 4));
       hipLaunchKernelGGL((k_gthr<256, 1024>), dim3((N + 1023) / 1024), B256, 0, c->stream, nsc,
@@ -6476,6 +6726,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
   c->gd_build = knob("CW_GD_BUILD", 1);
+  c->glocal = knob("CW_GLOCAL", 1);
+  c->glocal_min = knob("CW_GLOCAL_MIN", 1u << 20);
   c->gpack = knob("CW_GPACK", 1);
   c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);

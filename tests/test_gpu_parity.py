@@ -377,7 +377,9 @@ def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
 GIANT_FRONTS = {"gdplace": {}, "gjoin": {"CW_GDIR": "0"},
                 "gjoin-2pass-dir": {"CW_GDIR": "0", "CW_GD_BUILD": "0"},
                 "gjoin-unpacked": {"CW_GDIR": "0", "CW_GPACK": "0"},
-                "bucket": {"CW_GDIR": "0", "CW_GJOIN": "0"}}
+                "bucket": {"CW_GDIR": "0", "CW_GJOIN": "0"},
+                # the tile-local sibling links (k_glocal) at every size
+                "glocal": {"CW_GDIR": "0", "CW_GLOCAL_MIN": "0"}}
 
 
 def _weaver_with(env):
