@@ -33,7 +33,16 @@ def main():
     spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=a.nodes)
     lay = spec.layout()
     t0 = time.time()
+    import threading
+    done = threading.Event()
+
+    def beat():  # (a long generation must not look hung to the box's silence limit)
+        while not done.wait(30):
+            print(f"generating: {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     off, idk, ck, kd = gen.generate(spec, 0, a.docs, nthreads=16)
+    done.set()
     print(f"generated {len(idk):,} nodes in {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
     N, D = len(idk), a.docs
     dev = torch.device("cuda", 0)
