@@ -22,7 +22,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # k_tree_l is the library's "tree" stat, k_weave_doc its "weave", k_map_pack its "m_pack"
 ALIAS = {"pack_bits": "packbits", "tree_l": "tree", "weave_doc": "weave", "map_pack": "m_pack",
-         "gjoin": "join", "lvl_walk": "rank", "sup_rank": "rank", "lvl_apply": "rank"}
+         "gjoin": "join", "lvl_walk": "rank", "sup_rank": "rank", "lvl_apply": "rank",
+         "lvl_emit": "rank", "gd_build": "index", "gcross_ns": "gcross", "gcross_fc": "gcross"}
 
 
 def stat_name(sym):
