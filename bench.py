@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="budget of the cpu_baseline sample (rank 0, N=1)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-refresh", action="store_true",
+                    help="skip the refresh_caches (yarns) steps: PMC passes count the weave alone")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive pass")
     ap.add_argument("--config", type=int, default=2, choices=[1, 2, 3, 4, 5],
                     help="BASELINE.json configs[config-1]: 2 = the headline batch "
@@ -818,7 +820,7 @@ def main():
     # refresh-ts -> weave-fn): the same steps with the yarns (yarn_perm, the id
     # order partitioned by site) asked for as well; `value` stays the weave's
     refresh = None
-    if a.config in (2, 5) and not k32:
+    if a.config in (2, 5) and not k32 and not a.no_refresh:
         yarn = torch.empty(N, dtype=torch.int32, device=dev)
         outs_y = dict(outs, yarn_perm=yarn.data_ptr())
 

@@ -17,7 +17,7 @@ for cfg in 2 4 5; do
     t=$(echo $pass | tr ' ' '_' | cut -c1-40)
     (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 400 rocprofv3 --kernel-trace --pmc $pass \
        --output-format csv -d "$R/$d/pmc_$t" -o run -- \
-       python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu --no-h2d --config $cfg > "$R/$d/pmc_$t.log" 2>&1) \
+       python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu --no-h2d --no-refresh --config $cfg > "$R/$d/pmc_$t.log" 2>&1) \
        || { echo "config $cfg pass $pass failed"; tail -5 "$R/$d/pmc_$t.log"; exit 1; }
     echo "config $cfg pass $t ok"
   done
