@@ -1370,7 +1370,8 @@ __device__ __forceinline__ bool front_doc(
     uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t d, uint4 *sdir) {
+    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t d, uint4 *sdir,
+    uint32_t *__restrict__ yarn = nullptr, uint32_t site_shift = 0, uint32_t site_bits = 0) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (tprof) {
@@ -1573,6 +1574,74 @@ __device__ __forceinline__ bool front_doc(
       for (uint32_t k = 0; k < 3; k++)
         for (uint32_t m = wv[k]; m != 0 && r < n; m &= m - 1)
           skey[base + r++] = (uint64_t)g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
+    }
+  }
+  if (yarn) {
+    // the yarns (spin: the id order partitioned by site, id-ascending inside a
+    // site) from the same directory walk: a thread's groups are a contiguous
+    // range of ranks, so per-site counts, block prefix sums over the threads
+    // and the site totals place every rank's input index (p16, by rank) -- no
+    // id sort by site afterwards.  Eight sites a round (8 x 16-bit counters
+    // in 4 words: more spill the fused kernel's registers), site_bits <= 4.
+    constexpr uint32_t YB = 8, YW = YB / 2;
+    const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
+    const uint32_t smask = (1u << site_bits) - 1;
+    auto site_of = [&](uint32_t g, uint32_t k, uint32_t m) {
+      const uint32_t id = g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
+      return (id >> site_shift) & smask;
+    };
+    uint32_t *const yD = yarn + base;
+    uint32_t off = 0;  // the sites of earlier rounds
+    bool hi = false, more = false;  // a site past the first round's (config 2: 8 of 16 used)
+#pragma unroll 1
+    for (uint32_t s0 = 0; s0 <= smask; s0 += YB) {
+      if (s0 > 0 && !more) break;
+      uint32_t cw[YW];
+#pragma unroll
+      for (uint32_t w = 0; w < YW; w++) cw[w] = 0;
+      for (uint32_t g = g0; g < g1; g++) {
+        const uint4 q = sdir[g];
+#pragma unroll 1
+        for (uint32_t k = 0; k < 3; k++)
+          for (uint32_t m = k == 0 ? q.y : k == 1 ? q.z : q.w; m != 0; m &= m - 1) {
+            const uint32_t st = site_of(g, k, m) - s0;  // (wraps when below this round)
+            hi |= st >= YB && st < 0x80000000u;
+#pragma unroll
+            for (uint32_t w = 0; w < YW; w++)  // (no run-time index: the counters stay in VGPRs)
+              if (w == (st >> 1)) cw[w] += 1u << ((st & 1) * 16);
+          }
+      }
+      if (s0 == 0) more = __syncthreads_or(hi);
+      // site s0 + 2 w + h: its prefix over the threads and its total are half
+      // h of word w's scan; the sites in order give the bases, packed in cw
+#pragma unroll
+      for (uint32_t w = 0; w < YW; w++) {
+        uint32_t tot;
+        const uint32_t pre = block_exscan<NT>(cw[w], wtot, &tot);
+        const uint32_t b0 = off + (pre & 0xFFFFu);
+        off += tot & 0xFFFFu;
+        const uint32_t b1 = off + (pre >> 16);
+        off += tot >> 16;
+        cw[w] = (b0 & 0xFFFFu) | (b1 << 16);
+      }
+      for (uint32_t g = g0; g < g1; g++) {
+        const uint4 q = sdir[g];
+        uint32_t r = q.x;
+#pragma unroll 1
+        for (uint32_t k = 0; k < 3; k++)
+          for (uint32_t m = k == 0 ? q.y : k == 1 ? q.z : q.w; m != 0 && r < n; m &= m - 1, r++) {
+            const uint32_t st = site_of(g, k, m) - s0, sh = (st & 1) * 16;
+            if (st >= YB) continue;
+            uint32_t p = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < YW; w++)
+              if (w == (st >> 1)) {
+                p = (cw[w] >> sh) & 0xFFFFu;
+                cw[w] += 1u << sh;
+              }
+            if (p < n) yD[p] = p16[r];
+          }
+      }
     }
   }
   stamp(4);
@@ -3469,7 +3538,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 // there is one tail instead of three.  A document whose ids leave the front
 // end's directory counts itself in big[0] and stops: the host then weaves the
 // batch with the separate kernels.
-template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0, int FV = 0>
+template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0, int FV = 0, bool YF = false>
 __global__ __launch_bounds__(NT) void k_weave_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
@@ -3480,8 +3549,10 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
     uint32_t kbits, uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp, uint32_t *__restrict__ perm,
     uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc,
-    unsigned long long *__restrict__ tprof) {
+    unsigned long long *__restrict__ tprof, uint32_t *__restrict__ yarn, uint32_t site_sb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
+  // (site_sb: the yarns' site field, shift | bits << 8 -- one argument: the
+  // kernel is at its SGPR limit)
   const uint32_t d = blockIdx.x;
   // (tprof, CW_TREE_PROF: the three phases' clocks per document)
   const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -3490,7 +3561,8 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
   if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, 0u, d,
-                     reinterpret_cast<uint4 *>(lds_w)))
+                     reinterpret_cast<uint4 *>(lds_w), YF ? yarn : nullptr, site_sb & 0xFFu,
+                     site_sb >> 8))  // (YF = false: the yarn code compiles away)
     return;
   __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
   const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -4214,7 +4286,7 @@ struct cw_ctx {
   bool tab_on_device = false;
   bool last_giant = false;
   // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
-  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, giant_log2cap = 5, glocal = 1, glocal_min = 1u << 20, min_log2k = 5,
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, yarn_fused = 1, giant_log2cap = 5, glocal = 1, glocal_min = 1u << 20, min_log2k = 5,
            max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
@@ -5134,7 +5206,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     uint32_t *sval = nullptr;
     const bool want_yarns = out->yarn_perm && bt->site_bits;
     // 1-2 (dense ids). id order and join through per-document rank directories
-    bool front_done = false, fused_done = false;
+    bool front_done = false, fused_done = false, yarns_fused = false;
     uint32_t *kbm = nullptr;  // special / hide bitmaps per tile (front end -> tree)
     // fused front end: documents of < 2^16 nodes whose ids fit a 40 KiB directory
     if (c->front && c->front_fused && N >= (uint64_t)c->front_min_avg * D &&
@@ -5146,7 +5218,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       if (!big || !rank16 || !kbm) return fail(c, "out of device memory (front)");
       HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
       sval = svA;
-      skey = want_yarns ? skA : nullptr;
+      // the yarns inside the fused kernel (site fields of <= 4 bits): no ids
+      // in rank order written, no sort by site afterwards
+      yarns_fused = want_yarns && c->yarn_fused && bt->site_bits <= 4;  // (<= 2 rounds of 8 sites)
       unsigned long long *tprof_f = nullptr;
       if (c->tree_prof) {
         tprof_f = scratch_t<unsigned long long>(c, "tprof3", (size_t)D * 8);
@@ -5165,6 +5239,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                    !c->front_eff && (c->tl_mode == 0 || c->tl_mode == 4) &&
                    (!c->tree_prof || c->tl_mode == 4) && tl_lds + 64 * 4 + 4 <= c->lds_max &&
                    wd_lds + 1024 <= c->lds_max && to_lds <= TOUR_LDS_MAX;
+      // (k_front writes the ids for the yarn sort; CW_TREE_PROF's kernels have no yarn code)
+      yarns_fused = yarns_fused && fused_done && !c->tree_prof;
+      skey = want_yarns && !yarns_fused ? skA : nullptr;
       if (fused_done) {
         uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *thr = scratch_t<uint32_t>(c, "thr", N);
         uint32_t *loc = scratch_t<uint32_t>(c, "tour_loc", N);
@@ -5173,8 +5250,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         const uint32_t kbits_t = ceil_log2((uint64_t)t.nmax + 1) + 1;
         // par and (without yarns, which sort by it) sval as u16, no skind
         uint16_t *par16 = scratch_t<uint16_t>(c, "par16", N);
-        uint16_t *sval16 = want_yarns ? nullptr : scratch_t<uint16_t>(c, "sval16", N);
-        if (!par16 || (!want_yarns && !sval16)) return fail(c, "out of device memory (fused weave)");
+        uint16_t *sval16 = want_yarns && !yarns_fused ? nullptr : scratch_t<uint16_t>(c, "sval16", N);
+        if (!par16 || (!(want_yarns && !yarns_fused) && !sval16))
+          return fail(c, "out of device memory (fused weave)");
         // algorithmic bytes: front end (ids twice, causes, kinds, the rank scratch
         // out and back, par 2, sval 2 or 4, class bitmaps), tree (par 2, kind bits;
         // fcS clear 4, nsc 4; fcS + nsc back 8, link 4), tour (link 4, sval, the
@@ -5189,21 +5267,25 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              nullptr, sv_ptr, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status,
                              big, dev_tab(c, "t_doc_log2k"), kbits_t, (t.nmax + 31) / 32, nsc, fcS,
                              (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
-                             out->visible_count, loc, tprof_f);
+                             out->visible_count, loc, tprof_f, yarns_fused ? out->yarn_perm : nullptr,
+                             bt->site_shift | bt->site_bits << 8);
         };
+        const bool wy = want_yarns && !yarns_fused;  // (u32 sval: the yarn sort's values)
         if (tprof_f) {  // (the default front-end depth, so the clocks are the product's)
-          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, true, 4, 1>, sval);
+          if (wy) launch(k_weave_doc<1024, 2048, uint32_t, true, 4, 1>, sval);
           else launch(k_weave_doc<1024, 2048, uint16_t, true, 4, 1>, sval16);
         } else if (c->tl_mode == 4) {
           auto fv = [&](auto fvc) {
             constexpr int F = decltype(fvc)::value;
-            if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, F>, sval);
+            if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, F>, sval);
+            else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 4, F, true>, sval16);
             else launch(k_weave_doc<1024, 2048, uint16_t, false, 4, F>, sval16);
           };
           if (c->front_u) fv(std::integral_constant<int, 1>());
           else fv(std::integral_constant<int, 0>());
         } else {
-          if (want_yarns) launch(k_weave_doc<1024, 2048, uint32_t, false>, sval);
+          if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false>, sval);
+          else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 0, 0, true>, sval16);
           else launch(k_weave_doc<1024, 2048, uint16_t, false>, sval16);
         }
       } else {
@@ -5439,8 +5521,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                    spare ? skB : nullptr))
       return -1;
 
-    // 10. yarns: stable partition of the id order by site rank
-    if (want_yarns && !flagged) {
+    // 10. yarns: stable partition of the id order by site rank (unless the
+    // fused kernel wrote them)
+    if (want_yarns && !flagged && !(fused_done && yarns_fused)) {
       uint64_t *yk;
       uint32_t *yv;
       uint64_t *ykA = skey == skA ? skB : skA;
@@ -6726,6 +6809,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
   c->gd_build = knob("CW_GD_BUILD", 1);
+  c->yarn_fused = knob("CW_YARN_FUSED", 1);
   c->glocal = knob("CW_GLOCAL", 1);
   c->glocal_min = knob("CW_GLOCAL_MIN", 1u << 20);
   c->gpack = knob("CW_GPACK", 1);
