@@ -23,6 +23,7 @@ STATUS_ROOT, STATUS_DUP, STATUS_ORPHAN, STATUS_NON_LAMPORT, STATUS_INTERNAL = 1,
 STATUS_MAP_KEY = 16
 STATUS_WEFT = 64
 STATUS_KEY_RANGE = 128
+STATUS_UNWOVEN = 256  # reserved: never set since round 4 (include/causeweave.h)
 NIL32 = 0xFFFFFFFF
 K32_RESERVED = 0xFFFFFFF0     # K32 words from here up = the top 16 K64 values (CW_NIL, ...)
 

@@ -3666,13 +3666,34 @@ constexpr uint32_t MAP_ORPHAN = 0xFFFFFFFDu;     // nil key: the absent cause id
 //   nil                             2 << W         (the cause node is absent, or
 //                                                   the cause or the cause node's
 //                                                   cause is nil: cause_is_id = 2)
-// In an id key weave no node's cause is in the weave (each is an orphan
+// In an id key weave X no node's cause is in the weave (each is an orphan
 // there), so weave-node appends every node at the end: the weave is the root
 // then the nodes in id order (shared.cljc:226-241, asap never holds) -- a chain.
+// The one exception is a self-caused X (cause = id: the spec of new-node
+// forbids it, shared.cljc:98, but a ::nodes map can hold it): node n lands in
+// the key weave cause(cause(n)) and its cause c in cause(cause(c)), equal for
+// every n exactly when cause(X) = X, so X, its children and its grandchildren
+// all share the key weave X with their causes in it.  Those nodes keep their
+// real cause-in-weave; X's own cause is X, so the list pipeline flags the key
+// weave NON_LAMPORT and the literal fold (exact.hip) weaves it.
 // The nil key weave also holds nodes caused by the root id [0 "0" 0] or by nil
 // (cause-in-weave = the root, map.cljc:35-37) and their children, next to the
 // appended orphans: its nodes keep their real cause-in-weave, the list pipeline
 // flags the orphans and the literal fold (exact.hip) weaves that key weave.
+// Is the id key X of a node caused by c self-caused (see above)?  c is the
+// node's cause, found in the collection; X is that cause node's cause id.
+__device__ __forceinline__ bool map_self_key(const uint64_t *__restrict__ skey,
+                                             const uint32_t *__restrict__ sval,
+                                             const uint64_t *__restrict__ cause,
+                                             const uint8_t *__restrict__ cause_is_id, uint32_t n,
+                                             uint64_t c, uint64_t X) {
+  if (X == c) return true;  // the cause node is X itself
+  const uint32_t rx = lower_bound_u64(skey, n, X);
+  if (rx >= n || skey[rx] != X) return false;
+  const uint32_t gx = sval[rx];
+  return cause_is_id[gx] == 1 && cause[gx] == X;
+}
+
 __global__ __launch_bounds__(256) void k_map_key(
     const uint64_t *__restrict__ skey, const uint32_t *__restrict__ sval,
     const uint64_t *__restrict__ cause, const uint8_t *__restrict__ cause_is_id,
@@ -3698,8 +3719,10 @@ __global__ __launch_bounds__(256) void k_map_key(
         const uint32_t gc = base + sval[base + r];
         const uint8_t cci = cause_is_id[gc];
         if (cci == 1) {
-          key = (1ull << W) | cause[gc];
-          p = MAP_CHAIN;
+          const uint64_t X = cause[gc];
+          key = (1ull << W) | X;
+          p = map_self_key(skey + base, sval + base, cause + base, cause_is_id + base, n, c, X)
+                  ? r : MAP_CHAIN;
         } else if (cci == 2) {  // the cause node's cause is nil: the nil key, under it
           key = 2ull << W;
           p = r;

@@ -778,59 +778,130 @@ __global__ __launch_bounds__(256) void k_xsyn_final(
   skd[o] = c == KIND_HIDE || c == KIND_HHIDE ? 3 : c;
 }
 
-// --- phase 2: insertion-tree rounds ------------------------------------------
+// --- phase 2: insertion-tree rounds with BEFORE anchors ----------------------
+// Layout 2 (documents with an early node, round 5): the synthetic list of f
+// starts at sb2[f] = H; slot 2r + 2 = rank r, slot 2r + 1 = the placeholder of
+// rank r.  A round turns the weave W into one anchor per node:
+//   AFTER s   right after slot s (H, or an older node: the insertion-tree
+//             parent of round 4's rule), or
+//   BEFORE x  right before rank x, m's older child woven first (weave-asap?'s
+//             second test, shared.cljc:199-200) -- static along a chain of
+//             early nodes, where "the node before x" moved one link a round
+//             (a reverse chain took n - 2 rounds).
+// x has at most one BEFORE child (its own cause), so BEFORE anchors form chains
+// m_k -> .. -> m_1 -> b down to an AFTER-anchored bottom b, which the fold lays
+// out as m_k A_k .. m_1 A_1 b A_b (A = a node's after-subtrees).  As a tree
+// with children by descending slot: the placeholder 2b + 1 takes b's place
+// under b's parent and holds m_k .. m_1 and b (slots descending).  Every unused
+// placeholder is a leaf under slot 2r (rank r - 1, or H): the smallest slot
+// there, so the last child.  Parents stay below their children, so weave_tail
+// weaves layout 2 as it weaves any synthetic list (all classes normal: a plain
+// preorder); positions of placeholders are transparent (MT_MAX) to the queries.
+
+constexpr uint32_t XB_BIT = 0x80000000u;  // anchor word: BEFORE rank (low bits), else AFTER slot
+constexpr uint32_t X_ROUND_CAP = 48;     // rounds before a small still-moving document is folded
+constexpr uint32_t X_CAP_FOLD_MAX = 4096;  // ... serially (k_xfold: ~n^2 steps at worst)
+
+// Positions of a layout-2 weave.  from1: round 0's W is phase 1's weave
+// (layout 1, wperm1 at sb1): rank position x' -> x = 2x', slot s' -> 2s'.
+// Otherwise wperm2 (layout 2).  G[x] = the global slot at position x for a
+// rank or H (MT_MAX for a placeholder), AUX[x] = G[x] where the node is
+// non-special (H too), pos[slot] = x.  posold: moved[f] = 1 when a rank's
+// position changed (the round did not reproduce W).
+__global__ __launch_bounds__(256) void k_x2_pos(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase1,
+    const uint32_t *__restrict__ sbase2, const uint8_t *__restrict__ only, uint32_t from1,
+    const uint32_t *__restrict__ wperm1, const uint32_t *__restrict__ wperm2,
+    const uint8_t *__restrict__ xk, uint32_t *__restrict__ G, uint32_t *__restrict__ AUX,
+    uint32_t *__restrict__ pos, const uint32_t *__restrict__ posold, uint8_t *__restrict__ moved,
+    uint32_t *__restrict__ ctl) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
+  if (sb == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+  bool changed = false;
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base;
+    if (r == 0) {
+      G[sb] = sb;
+      AUX[sb] = sb;
+      pos[sb] = sb;
+      if (!from1 && wperm2[sb] != 0) atomicOr(&ctl[1], 16u);  // H is always first
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < 2; h++) {
+      uint32_t x, s;
+      if (from1) {
+        if (h) break;
+        x = 2 * r + 2;
+        s = 2 * wperm1[sbase1[f] + 1 + r];
+      } else {
+        x = 2 * r + 1 + h;
+        s = wperm2[sb + x];
+      }
+      if (s == 0 || s > 2 * n) {
+        atomicOr(&ctl[1], 16u);
+        continue;
+      }
+      const uint32_t g = sb + s, xg = sb + x;
+      if (s & 1u) {  // a placeholder
+        G[xg] = MT_MAX;
+        AUX[xg] = MT_MAX;
+      } else {
+        G[xg] = g;
+        AUX[xg] = (xk[base + (s >> 1) - 1] & KIND_CLASS) ? MT_MAX : g;
+        changed |= posold && posold[g] != xg;
+      }
+      pos[g] = xg;
+    }
+  }
+  if (posold && __syncthreads_or(changed) && threadIdx.x == 0) moved[f] = 1;
+}
 
 // xf[c] = the smallest position of an older child of c (weave-asap?'s second
 // test), MT_MAX when none.
-__global__ __launch_bounds__(256) void k_xf(
+__global__ __launch_bounds__(256) void k_x2_xf(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
-    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
     const uint8_t *__restrict__ only, const uint32_t *__restrict__ xpar,
     const uint32_t *__restrict__ pos, uint32_t *__restrict__ xf) {
-  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
   if (sb == X_NONE || !only[f]) return;
   const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
     const uint32_t r = i - base, p = xpar[i];
-    if (p < n && p > r) atomicMin(&xf[base + p], pos[sb + 1 + r]);
+    if (p < n && p > r) atomicMin(&xf[base + p], pos[sb + 2 * r + 2]);
   }
 }
 
-// Each node's insertion-tree parent from the weave W (G, pos; mt over G, mtn
-// over G of the non-special nodes): weave-node's scan on W restricted to the
-// older nodes.  first: W is phase 1's weave (an appended node goes after the
-// last older node of the whole weave; later rounds use its region).
-__global__ __launch_bounds__(256) void k_xpred(
+// Each node's anchor from the weave W (G, pos; mt over G, mtn over G of the
+// non-special nodes): weave-node's scan on W restricted to the older nodes.
+// first: W is phase 1's weave (an appended node goes after the last older node
+// of the whole weave; later rounds use the region of the previous appended
+// node, prevne: its sub-batch index or X_NONE).
+__global__ __launch_bounds__(256) void k_x2_anchor(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
-    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
     const uint8_t *__restrict__ only, const uint32_t *__restrict__ xpar,
-    const uint8_t *__restrict__ xk, const uint8_t *__restrict__ early,
-    const uint32_t *__restrict__ xf, const uint32_t *__restrict__ app_list,
-    const uint32_t *__restrict__ app_idx, const uint32_t *__restrict__ pos,
+    const uint8_t *__restrict__ xk, const uint32_t *__restrict__ xf,
+    const uint32_t *__restrict__ prevne, const uint32_t *__restrict__ pos,
     const uint32_t *__restrict__ G, XMinTree mt, XMinTree mtn, uint32_t first,
-    uint32_t *__restrict__ spar, uint8_t *__restrict__ skd, uint32_t *__restrict__ ctl) {
-  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase[f];
+    uint32_t *__restrict__ anc, uint32_t *__restrict__ ctl) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
   if (sb == X_NONE || !only[f]) return;
   const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t r = i - base, p = xpar[i], m = sb + 1 + r;
+    const uint32_t r = i - base, p = xpar[i], m = sb + 2 * r + 2;
     const bool sp = (xk[i] & KIND_CLASS) != 0;
     const uint32_t x1 = xf[i];
-    const uint32_t cp = p == X_NIL ? sb : (p < r ? pos[sb + 1 + p] : MT_MAX);
-    uint32_t pred;
+    const uint32_t cp = p == X_NIL ? sb : (p < r ? pos[sb + 2 * p + 2] : MT_MAX);
+    uint32_t pred = MT_MAX;
+    bool before = false;
     if (cp == MT_MAX && x1 == MT_MAX) {  // appended
-      uint32_t e = sb + n + 1, lo = sb;
-      if (!first) {
-        // the region of the previous appended node (not an early one)
-        uint32_t prev = sb;
-        for (uint32_t k = app_idx[i]; k-- > 0;) {
-          const uint32_t ip = app_list[k];
-          if (ip < base) break;
-          if (!early[ip]) {
-            prev = sb + 1 + (ip - base);
-            break;
-          }
-        }
+      uint32_t e = sb + 2 * n + 1, lo = sb;
+      if (!first) {  // the region of the previous appended node (not an early one)
+        const uint32_t ip = prevne[i];
+        const uint32_t prev = ip == X_NONE ? sb : sb + 2 * (ip - base) + 2;
         lo = pos[prev];
         e = mt_first_after(mt, lo, prev);
       }
@@ -838,23 +909,237 @@ __global__ __launch_bounds__(256) void k_xpred(
       pred = q == MT_MAX || q < lo ? MT_MAX : G[q];
     } else if (cp != MT_MAX && cp < x1) {  // right after the cause, then clause A's skip
       if (sp) {
-        pred = p == X_NIL ? sb : sb + 1 + p;
+        pred = p == X_NIL ? sb : sb + 2 * p + 2;
       } else {
         const uint32_t stop = min(mt_first_after(mtn, cp, m), x1);
-        const uint32_t q = mt_last_before(mt, stop, m);
-        pred = q == MT_MAX || q < cp ? MT_MAX : G[q];
+        if (stop == x1) {
+          before = true;
+        } else {
+          const uint32_t q = mt_last_before(mt, stop, m);
+          pred = q == MT_MAX || q < cp ? MT_MAX : G[q];
+        }
       }
     } else {  // right before the older child woven first
-      const uint32_t q = mt_last_before(mt, x1, m);
-      pred = q == MT_MAX || q < sb ? MT_MAX : G[q];
+      before = true;
     }
-    if (pred == MT_MAX || pred >= m) {
+    uint32_t a;
+    if (before) {
+      const uint32_t gx = G[x1];
+      if (gx == MT_MAX || gx < sb + 2 || gx >= m) {
+        atomicOr(&ctl[1], 8u);
+        a = 0;
+      } else {
+        a = XB_BIT | ((gx - sb - 2) >> 1);
+      }
+    } else if (pred == MT_MAX || pred >= m || pred < sb) {
       atomicOr(&ctl[1], 8u);
-      pred = sb;
+      a = 0;
+    } else {
+      a = pred - sb;
     }
-    spar[m] = pred - sb;
-    skd[m] = 0;
+    anc[i] = a;
   }
+}
+
+// BEFORE chains: jmp = the BEFORE target (a rank) or the node itself; hasb[x]
+// = x has a BEFORE child.  k_x2_jump then doubles jmp down every chain to its
+// AFTER-anchored bottom (in place: a value read mid-update is only further
+// down the same chain).
+__global__ __launch_bounds__(256) void k_x2_chain(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
+    const uint8_t *__restrict__ only, const uint32_t *__restrict__ anc,
+    uint32_t *__restrict__ jmp, uint8_t *__restrict__ hasb) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t];
+  if (sbase2[f] == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t a = anc[i];
+    if (a & XB_BIT) {
+      const uint32_t x = a & ~XB_BIT;
+      jmp[i] = x;
+      hasb[base + x] = 1;
+    } else {
+      jmp[i] = i - base;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_x2_jump(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
+    const uint8_t *__restrict__ only, uint32_t *jmp) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t];
+  if (sbase2[f] == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t j = __hip_atomic_load(&jmp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t k = __hip_atomic_load(&jmp[base + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k != j) __hip_atomic_store(&jmp[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The layout-2 tree of the anchors (slots local to the document, all classes
+// normal): rank r under its AFTER slot, or under its placeholder when it is
+// a chain bottom, or under its bottom's placeholder when BEFORE-anchored; a
+// used placeholder under the bottom's AFTER slot, an unused one under 2r.
+__global__ __launch_bounds__(256) void k_x2_build(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
+    const uint8_t *__restrict__ only, const uint32_t *__restrict__ anc,
+    const uint32_t *__restrict__ jmp, const uint8_t *__restrict__ hasb,
+    uint32_t *__restrict__ spar, uint8_t *__restrict__ skd) {
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
+  if (sb == X_NONE || !only[f]) return;
+  const uint32_t base = doc_off[f];
+  for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
+    const uint32_t r = i - base, a = anc[i];
+    uint32_t pr, pp;
+    if (a & XB_BIT) {
+      pr = 2 * jmp[i] + 1;
+      pp = 2 * r;
+    } else if (hasb[i]) {
+      pr = 2 * r + 1;
+      pp = a;
+    } else {
+      pr = a;
+      pp = 2 * r;
+    }
+    spar[sb + 2 * r + 2] = pr;
+    spar[sb + 2 * r + 1] = pp;
+    skd[sb + 2 * r + 2] = 0;
+    skd[sb + 2 * r + 1] = 0;
+    if (r == 0) {
+      spar[sb] = CW_NIL_RANK;
+      skd[sb] = KIND_ROOT;
+    }
+  }
+}
+
+// The converged layout-2 weave back to layout 1 (wperm1[sb1 + 1 + q] = rank + 1
+// at output position q), for k_xsyn_emit: ranks counted per tile of positions
+// (a tile of ranks [a, b) owns positions [2a + 1, 2b + 1)), a scan over tiles,
+// then each rank written at its count.  Documents not on layout 2 count their
+// n ranks (so a document's first tile starts at its doc_off).
+__global__ __launch_bounds__(256) void k_x2_count(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
+    const uint32_t *__restrict__ wperm2, uint32_t *__restrict__ tcnt) {
+  __shared__ uint32_t ws[4];
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
+  const uint32_t base = doc_off[f], a = tile_start[t] - base, b = tile_start[t + 1] - base;
+  uint32_t c = 0;
+  if (sb == X_NONE) {
+    c = threadIdx.x == 0 ? b - a : 0u;
+  } else {
+    for (uint32_t x = 2 * a + 1 + threadIdx.x; x < 2 * b + 1; x += blockDim.x) {
+      const uint32_t s = wperm2[sb + x];
+      c += (s != 0 && !(s & 1u)) ? 1u : 0u;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tcnt[t] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(256) void k_x2_compact(
+    const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
+    const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase1,
+    const uint32_t *__restrict__ sbase2, const uint32_t *__restrict__ toff,
+    const uint32_t *__restrict__ wperm2, uint32_t *__restrict__ wperm1,
+    uint32_t *__restrict__ ctl) {
+  __shared__ uint32_t ws[4];
+  const uint32_t t = blockIdx.x, f = tile_doc[t], sb = sbase2[f];
+  if (sb == X_NONE) return;
+  const uint32_t base = doc_off[f], n = doc_off[f + 1] - base;
+  const uint32_t a = tile_start[t] - base, b = tile_start[t + 1] - base;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t k0 = toff[t] - base;
+  for (uint32_t x0 = 2 * a + 1; x0 < 2 * b + 1; x0 += 256) {
+    const uint32_t x = x0 + threadIdx.x;
+    const uint32_t s = x < 2 * b + 1 ? wperm2[sb + x] : 0u;
+    const bool real = s != 0 && !(s & 1u);
+    const uint64_t bb = __ballot(real);
+    if (lane == 0) ws[wv] = (uint32_t)__popcll(bb);
+    __syncthreads();
+    uint32_t pre = k0;
+    for (uint32_t w = 0; w < wv; w++) pre += ws[w];
+    if (real) {
+      const uint32_t q = pre + lanes_below(bb);
+      if (q < n) wperm1[sbase1[f] + 1 + q] = s >> 1;
+      else atomicOr(&ctl[1], 32u);
+    }
+    k0 += ws[0] + ws[1] + ws[2] + ws[3];
+    __syncthreads();
+  }
+}
+
+// prevne[i] for every appended node i: the previous appended node of its
+// document that is not early (sub-batch index), X_NONE if none -- the region
+// k_x2_anchor starts from.  A max-scan over the appended list in chunks of 256.
+__device__ __forceinline__ uint32_t x_wave_maxscan_incl(uint32_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(v, o, 64);
+    if (lane >= o) v = max(v, y);
+  }
+  return v;
+}
+
+// (value k + 1 for a non-early entry k, 0 otherwise) -> the chunk's maximum
+__global__ __launch_bounds__(256) void k_x2_ne_chunk(const uint32_t *__restrict__ app_list, uint32_t A,
+                                                     const uint8_t *__restrict__ early,
+                                                     uint32_t *__restrict__ cmax) {
+  __shared__ uint32_t ws[4];
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+  uint32_t v = (k < A && !early[app_list[k]]) ? k + 1 : 0u;
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor(v, o, 64));
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) cmax[blockIdx.x] = max(max(ws[0], ws[1]), max(ws[2], ws[3]));
+}
+
+// exclusive max-scan of C chunk maxima in place (one workgroup of 1024)
+__global__ __launch_bounds__(1024) void k_x2_ne_scan(uint32_t *__restrict__ cmax, uint32_t C) {
+  __shared__ uint32_t wmax[16];
+  __shared__ uint32_t carry;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < C; c0 += 1024) {
+    const uint32_t c = c0 + threadIdx.x;
+    const uint32_t v = c < C ? cmax[c] : 0u;
+    const uint32_t inc = x_wave_maxscan_incl(v);
+    if (lane == 63) wmax[wv] = inc;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (uint32_t w = 0; w < wv; w++) pre = max(pre, wmax[w]);
+    const uint32_t excl = max(pre, (uint32_t)__shfl_up(inc, 1, 64) * (lane > 0 ? 1u : 0u));
+    if (c < C) cmax[c] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = max(pre, inc);
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void k_x2_ne_final(const uint32_t *__restrict__ app_list,
+                                                     const uint32_t *__restrict__ app_doc, uint32_t A,
+                                                     const uint8_t *__restrict__ early,
+                                                     const uint32_t *__restrict__ cexcl,
+                                                     uint32_t *__restrict__ prevne) {
+  __shared__ uint32_t ws[4];
+  const uint32_t k = blockIdx.x * 256 + threadIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t v = (k < A && !early[app_list[k]]) ? k + 1 : 0u;
+  const uint32_t inc = x_wave_maxscan_incl(v);
+  if (lane == 63) ws[wv] = inc;
+  __syncthreads();
+  uint32_t pre = cexcl[blockIdx.x];
+  for (uint32_t w = 0; w < wv; w++) pre = max(pre, ws[w]);
+  const uint32_t up = __shfl_up(inc, 1, 64);
+  const uint32_t prev = lane > 0 ? max(pre, up) : pre;  // the last non-early entry before k, + 1
+  if (k < A)
+    prevne[app_list[k]] = (prev != 0 && app_doc[prev - 1] == app_doc[k]) ? app_list[prev - 1] : X_NONE;
 }
 
 // The woven synthetic lists -> the caller's outputs: weave_perm (input index per
@@ -1113,34 +1398,159 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
       if (check_launch(c, "xsyn_resolve")) return -1;
       if (weave_groups(false)) return -1;
     }
-    // phase 2: documents with an early node, insertion-tree rounds from there
+    // phase 2: documents with an early node, anchor rounds on layout 2 from
+    // phase 1's weave until the weave reproduces itself (the fold's, by
+    // induction over the nodes in id order); a small document still moving
+    // after X_ROUND_CAP rounds is folded serially instead
     if (any_x2) {
-      uint32_t *posB = scratch_t<uint32_t>(c, "x_posB", NS), *xf = scratch_t<uint32_t>(c, "x_xf", NX);
-      if (!posB || !xf || !app_list) return fail(c, "out of device memory (exact path rounds)");
-      if (positions(1, d_x2, posA, nullptr)) return -1;
+      std::vector<uint32_t> sb2(F, X_NONE);
+      std::vector<Group> groups2;
+      uint64_t NS2 = 0;
+      uint32_t nmax = 1;
+      {
+        std::vector<uint32_t> small2, big2;
+        for (uint32_t f = 0; f < F; f++) {
+          if (!x2[f]) continue;
+          const uint64_t n = xoff[f + 1] - xoff[f];
+          nmax = std::max<uint32_t>(nmax, (uint32_t)n);
+          if (2 * n + 1 >= c->giant_min || 2 * n + 1 >= LINK_IDX) big2.push_back(f);
+          else small2.push_back(f);
+        }
+        if (!small2.empty()) {
+          Group g{false, true, NS2, {0}};
+          for (uint32_t f : small2) {
+            sb2[f] = (uint32_t)(NS2 + g.off.back());
+            g.off.push_back(g.off.back() + 2 * (xoff[f + 1] - xoff[f]) + 1);
+          }
+          NS2 = (NS2 + g.off.back() + 31) & ~31ull;
+          groups2.push_back(std::move(g));
+        }
+        for (uint32_t f : big2) {
+          const uint64_t n = xoff[f + 1] - xoff[f];
+          sb2[f] = (uint32_t)NS2;
+          groups2.push_back(Group{true, true, NS2, {0, 2 * n + 1}});
+          NS2 = (NS2 + 2 * n + 1 + 31) & ~31ull;
+        }
+      }
+      if (NS2 >= 0xFFFFFFF0ull - 16) return fail(c, "exact path: %llu layout-2 nodes", (unsigned long long)NS2);
+      const uint64_t NP2 = ((NS2 + 15) & ~15ull) + 16;
+      uint32_t *d_sb2 = x_upload(c, "x_sbase2", sb2);
+      uint8_t *d_only = x_upload(c, "x_only", x2);
+      uint32_t *spar2 = scratch_t<uint32_t>(c, "x_spar2", NS2), *wperm2 = scratch_t<uint32_t>(c, "x_wperm2", NS2);
+      uint8_t *skd2 = scratch_t<uint8_t>(c, "x_skd2", NS2);
+      uint32_t *wbits2 = scratch_t<uint32_t>(c, "x_wbits2", NS2 / 32 + 1);
+      uint32_t *G2 = scratch_t<uint32_t>(c, "x_G2", NP2), *AUX2 = scratch_t<uint32_t>(c, "x_aux2", NP2);
+      uint32_t *p2A = scratch_t<uint32_t>(c, "x_pos2A", NS2), *p2B = scratch_t<uint32_t>(c, "x_pos2B", NS2);
+      uint32_t *xf = scratch_t<uint32_t>(c, "x_xf", NX), *anc = scratch_t<uint32_t>(c, "x_anc", NX);
+      uint32_t *jmp = scratch_t<uint32_t>(c, "x_jmp", NX), *prevne = scratch_t<uint32_t>(c, "x_prevne", NX);
+      uint8_t *hasb = scratch_t<uint8_t>(c, "x_hasb", NX), *moved = scratch_t<uint8_t>(c, "x_moved", F);
+      size_t gmax2 = 1;
+      for (auto &g : groups2) gmax2 = std::max(gmax2, g.off.size() - 1);
+      uint32_t *wvc2 = scratch_t<uint32_t>(c, "x_wvc", std::max(gmax, gmax2)),
+               *wst2 = scratch_t<uint32_t>(c, "x_wst", std::max(gmax, gmax2));
+      if (!d_sb2 || !d_only || !spar2 || !wperm2 || !skd2 || !wbits2 || !G2 || !AUX2 || !p2A || !p2B || !xf ||
+          !anc || !jmp || !prevne || !hasb || !moved || !wvc2 || !wst2)
+        return fail(c, "out of device memory (exact path rounds, %llu layout-2 nodes)", (unsigned long long)NS2);
+      if (A > 0) {  // the previous non-early appended node of every appended node
+        const uint32_t A32 = (uint32_t)A, C = (A32 + 255) / 256;
+        uint32_t *cmax = scratch_t<uint32_t>(c, "x_necmax", C);
+        uint32_t *app_doc = scratch_t<uint32_t>(c, "x_appdoc", A);
+        if (!cmax || !app_doc) return fail(c, "out of device memory (exact path rounds)");
+        Launch L(c, "xins_prevne", (double)A * 14);
+        hipLaunchKernelGGL(k_x2_ne_chunk, dim3(C), B256, 0, c->stream, app_list, A32, early, cmax);
+        hipLaunchKernelGGL(k_x2_ne_scan, dim3(1), dim3(1024), 0, c->stream, cmax, C);
+        hipLaunchKernelGGL(k_x2_ne_final, dim3(C), B256, 0, c->stream, app_list, app_doc, A32, early, cmax,
+                           prevne);
+      }
+      if (check_launch(c, "xins_prevne")) return -1;
+      auto positions2 = [&](uint32_t from1, uint32_t *pos, const uint32_t *posold) -> int {
+        HIPCHK(c, hipMemsetAsync(G2, 0xFF, NP2 * 4, c->stream));
+        HIPCHK(c, hipMemsetAsync(AUX2, 0xFF, NP2 * 4, c->stream));
+        Launch L(c, "xsyn_pos", (double)NX * 26);
+        hipLaunchKernelGGL(k_x2_pos, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, d_sb2,
+                           d_only, from1, wperm, wperm2, xk, G2, AUX2, pos, posold, moved, ctl);
+        return check_launch(c, "xsyn_pos");
+      };
+      if (positions2(1, p2A, nullptr)) return -1;
+      const uint32_t jumps = ceil_log2(nmax) + 1;
+      std::vector<uint8_t> only(x2), h_moved(F);
       for (uint32_t round = 0;; round++) {
         XMinTree mt, mtn;
-        if (mt_build(c, "x_mtG", G, NP, &mt) || mt_build(c, "x_mtA", AUX, NP, &mtn)) return -1;
+        if (mt_build(c, "x_mtG", G2, NP2, &mt) || mt_build(c, "x_mtA", AUX2, NP2, &mtn)) return -1;
         {
-          Launch L(c, "xins_round", (double)NX * 40);
+          Launch L(c, "xins_round", (double)NX * (40 + 8 * jumps));
           HIPCHK(c, hipMemsetAsync(xf, 0xFF, (size_t)NX * 4, c->stream));
-          hipLaunchKernelGGL(k_xf, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb, d_x2,
-                             xpar, posA, xf);
-          hipLaunchKernelGGL(k_xpred, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
-                             d_x2, xpar, xk, early, xf, app_list, app_idx, posA, G, mt, mtn,
-                             round == 0 ? 1u : 0u, spar, skd, ctl);
+          HIPCHK(c, hipMemsetAsync(hasb, 0, NX, c->stream));
+          hipLaunchKernelGGL(k_x2_xf, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2, d_only,
+                             xpar, p2A, xf);
+          hipLaunchKernelGGL(k_x2_anchor, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2,
+                             d_only, xpar, xk, xf, prevne, p2A, G2, mt, mtn, round == 0 ? 1u : 0u, anc, ctl);
+          hipLaunchKernelGGL(k_x2_chain, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2,
+                             d_only, anc, jmp, hasb);
+          for (uint32_t j = 0; j < jumps; j++)
+            hipLaunchKernelGGL(k_x2_jump, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2,
+                               d_only, jmp);
+          hipLaunchKernelGGL(k_x2_build, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2,
+                             d_only, anc, jmp, hasb, spar2, skd2);
         }
         if (check_launch(c, "xins_round")) return -1;
-        if (weave_groups(true)) return -1;
-        HIPCHK(c, hipMemsetAsync(ctl, 0, 4, c->stream));
-        if (positions(1, d_x2, posB, posA)) return -1;
-        std::swap(posA, posB);
+        // weave the layout-2 groups that hold a moving document
+        for (auto &g : groups2) {
+          bool any = false;
+          for (uint32_t f = 0; f < F && !any; f++)
+            any = only[f] && sb2[f] >= g.base && sb2[f] < g.base + g.off.back();
+          if (!any) continue;
+          const uint64_t Dg = g.off.size() - 1, Ng = g.off.back();
+          if (ensure_tables(c, Dg, g.off.data(), g.giant)) return -1;
+          HIPCHK(c, hipMemsetAsync(wst2, 0, Dg * 4, c->stream));
+          HIPCHK(c, hipMemsetAsync(wvc2, 0, Dg * 4, c->stream));
+          cw_list_result sr{};
+          sr.weave_perm = wperm2 + g.base;
+          sr.visible_bits = wbits2 + g.base / 32;
+          sr.visible_count = wvc2;
+          sr.status = wst2;
+          if (weave_tail(c, Dg, (uint32_t)Ng, g.giant, spar2 + g.base, skd2 + g.base, nullptr, nullptr,
+                         nullptr, 0, &sr))
+            return -1;
+          c->x_iters++;
+        }
+        if (ensure_tables(c, F, xoff.data())) return -1;
+        tile_start = dev_tab(c, "t_tile_start");
+        tile_doc = dev_tab(c, "t_tile_doc");
+        sub_off = dev_tab(c, "t_doc_off");
+        HIPCHK(c, hipMemsetAsync(moved, 0, F, c->stream));
+        if (positions2(0, p2B, p2A)) return -1;
+        std::swap(p2A, p2B);
         HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(h_moved.data(), moved, F, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (c->pin_small[1]) return fail(c, "exact path: inconsistent synthetic weave (%u)", c->pin_small[1]);
-        if (c->pin_small[0] == 0) break;  // the weave reproduced itself: the fold's
+        bool more = false;
+        for (uint32_t f = 0; f < F; f++) {
+          only[f] = only[f] && h_moved[f];  // a document that reproduced its weave is done
+          if (only[f] && round + 1 >= X_ROUND_CAP && xoff[f + 1] - xoff[f] <= X_CAP_FOLD_MAX) {
+            only[f] = 0;  // small and still moving: the serial fold (emitted after the synthetic lists)
+            run[f] = 1;
+            any_serial = true;
+          }
+          more |= only[f] != 0;
+        }
+        if (!more) break;
         if (round > NX + 2) return fail(c, "exact path: no fixed point after %u rounds", round);
+        HIPCHK(c, hipMemcpy(d_only, only.data(), F, hipMemcpyHostToDevice));
       }
+      // the converged layout-2 weaves back into layout 1 for the emission
+      uint32_t *tcnt2 = scratch_t<uint32_t>(c, "x_tcnt", T);
+      if (!tcnt2) return fail(c, "out of device memory (exact path)");
+      {
+        Launch L(c, "xsyn_compact", (double)NX * 16);
+        hipLaunchKernelGGL(k_x2_count, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb2, wperm2,
+                           tcnt2);
+        hipLaunchKernelGGL(k_xapp_scan, dim3(1), dim3(1024), 0, c->stream, tcnt2, T);
+        hipLaunchKernelGGL(k_x2_compact, dim3(T), B256, 0, c->stream, tile_start, tile_doc, sub_off, d_sb,
+                           d_sb2, tcnt2, wperm2, wperm, ctl);
+      }
+      if (check_launch(c, "xsyn_compact")) return -1;
     }
     HIPCHK(c, hipMemcpyAsync(c->pin_small, ctl, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));

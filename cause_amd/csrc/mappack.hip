@@ -27,7 +27,8 @@
 // In the key weave a node caused by an id whose node is itself id-caused (an id
 // key) or absent (the nil key) is never next to its cause, so weave-node
 // appends it (shared.cljc:236-238): it chains after the previous node of the
-// key weave, as k_seg_build does.
+// key weave, as k_seg_build does -- except under a self-caused id key, whose
+// key weave holds its causes (k_map_key) and is folded literally.
 
 constexpr uint32_t MPK = 2048;                 // largest pack (nodes); CW_MAP_PACK picks the geometry
 constexpr uint16_t MP_ROOT = 0xFFFFu;          // cause-in-weave = the key weave's root
@@ -316,7 +317,23 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         const uint64_t gc = B[jc];
         if (K8[jc] & 0x80u) {  // the cause node is id-caused: the key is that id (F8c)
           key = (1ull << W) | gc;
-          p = MP_CHAIN;
+          // a chain, unless the key's node X = gc is self-caused: then X, its
+          // children and grandchildren share the key weave with their causes
+          // (k_map_key) -- real causes, and X's own makes it a literal key weave
+          bool selfk = gc == c;
+          if (!selfk && (gc & ~imask) == 0) {
+            const uint64_t want = ((uint64_t)dl << kbits) | gc;
+            uint32_t l2 = dstart[dl], h2 = a1;
+            while (l2 < h2) {
+              const uint32_t m = (l2 + h2) >> 1;
+              if (A[m] < want) l2 = m + 1; else h2 = m;
+            }
+            if (l2 < a1 && A[l2] == want) {
+              const uint32_t jx = I2J[l2];
+              selfk = (K8[jx] & 0x80u) && B[jx] == gc;
+            }
+          }
+          p = selfk ? (uint16_t)lo : MP_CHAIN;
         } else if (K8[jc] & 0x40u) {  // the cause node's cause is nil: the nil key, under it
           key = 2ull << W;
           p = (uint16_t)lo;

@@ -69,9 +69,12 @@ enum {
   CW_STATUS_MAP_KEY = 1u << 4,     /* map: a key token >= 2^token_bits                      */
   CW_STATUS_INTERNAL = 1u << 5,    /* consistency check failed inside the pipeline         */
   CW_STATUS_WEFT = 1u << 6,        /* weft: a cut id is not a node of the document         */
-  CW_STATUS_KEY_RANGE = 1u << 7    /* an id key >= 2^63: it does not fit the K64 layout
+  CW_STATUS_KEY_RANGE = 1u << 7,   /* an id key >= 2^63: it does not fit the K64 layout
                                       (CW_NIL and its neighbours are reserved); weave the
                                       document with cw_weave_lists_k128                     */
+  CW_STATUS_UNWOVEN = 1u << 8      /* reserved, never set since ABI round 4: every document
+                                      the reference folds is woven (exact path); kept so
+                                      client code that tests the bit still compiles         */
 };
 
 /* Where the arrays of a batch/result live. */
@@ -215,7 +218,9 @@ int cw_weave_lists_k128(cw_ctx *ctx, const cw_list_batch_k128 *batch, cw_list_re
  * key weave as a list document through the list pipeline).  Both fold key
  * weaves that are not a plain F5 tree -- the nil key weave holding nodes caused
  * by the root id or by nil next to appended orphans, a cause with a larger id
- * than its node -- literally (shared.cljc:225-241), so every collection without
+ * than its node, the id key weave of a self-caused id X (cause = id; X, its
+ * children and grandchildren fold there by their real causes) -- literally
+ * (shared.cljc:225-241), so every collection without
  * DUP / MAP_KEY comes out as the reference's fold; CW_STATUS_NON_LAMPORT stays
  * as information. */
 typedef struct {

@@ -31,13 +31,16 @@ hangs under the head H as a non-special root.  A second weave with every
 appended node under its T gives the fold's result.
 
 Phase 2, documents with a non-Lamport cause whose node has an older child
-("early" nodes: weave-asap?'s second clause, shared.cljc:199-200).  The fold
-is the preorder of its insertion tree: each node's parent is the node right
-before its insertion point at its time, children by descending id.  From any
-weave W, `preds` computes every node's insertion point in W restricted to the
-older nodes; weaving those parents gives W'.  W' == W holds exactly for the
-fold's weave, and each round fixes at least the oldest misplaced node, so
-iterating from phase 1's weave reaches the fold.
+("early" nodes: weave-asap?'s second clause, shared.cljc:199-200).  From any
+weave W, `anchors` finds every node's insertion split in W restricted to the
+older nodes and names it by a node that does not move from round to round where
+it can: BEFORE x (right before x_f, the node's older child woven first) or
+AFTER s (right after s: the cause, the end of the special run after it, or the
+last older node of an appended node's region).  `build` lays the anchors out
+(BEFORE chains under a placeholder at their bottom's place), giving W'.
+W' == W holds exactly for the fold's weave and each round fixes at least the
+oldest misplaced node; with BEFORE anchors a chain of early nodes (a reverse
+chain: node r caused by r + 1) settles in two rounds instead of n - 2.
 """
 from __future__ import annotations
 
@@ -109,20 +112,6 @@ def f5_preorder(spar, scls):
         ks = [k for k in kids[v] if scls[k] != 0] + [k for k in kids[v] if scls[k] == 0]
         st.extend(reversed(ks))
     return out, eff
-
-
-def tree_preorder(parent):
-    """Plain preorder, children by descending index (the insertion tree)."""
-    n = len(parent)
-    kids = [[] for _ in range(n)]
-    for i in range(n - 1, 0, -1):
-        kids[parent[i]].append(i)
-    out, st = [], [0]
-    while st:
-        v = st.pop()
-        out.append(v)
-        st.extend(reversed(kids[v]))
-    return out
 
 
 # --- phase 1 ------------------------------------------------------------------
@@ -256,11 +245,23 @@ def phase1_weave(par, cls):
     return [s - 1 for s in order[1:]]
 
 
-# --- phase 2 ------------------------------------------------------------------
+# --- phase 2: anchor rounds (round 5) -----------------------------------------
+#
+# A node m whose insertion split is right before x_f, the first of its older
+# children in the weave (weave-asap?'s second test, shared.cljc:199-200), is
+# anchored BEFORE x_f instead of AFTER whatever node precedes x_f in W: that
+# node is what changes from round to round along a chain of early nodes (a
+# reverse chain, node r caused by r + 1, moved one link a round).  x_f has at
+# most one such m (its own cause), so the BEFORE anchors form chains
+# m_k -> ... -> m_1 -> b ending in an AFTER-anchored bottom b, and the fold
+# lays a chain out as m_k A_k m_(k-1) ... m_1 A_1 b A_b (A_i = m_i's after-
+# subtrees).  As a tree with children by descending index: a placeholder P_b
+# takes b's place under b's parent (just below b's index) and holds m_k .. m_1
+# and b as children, each with its own after-children.
 
-def preds(W, par, cls, region=False):
-    """Insertion-tree parent (rank + 1, 0 = H) of every node, from the weave W
-    restricted to the older nodes (weave-node's scan, shared.cljc:229-241)."""
+def anchors(W, par, cls, region=False):
+    """Anchors of every node from the weave W: ('A', s) = right after synthetic
+    s (rank + 1, 0 = H), ('B', x) = right before rank x (its older child)."""
     n = len(par)
     pos = [0] * n
     for q, v in enumerate(W):
@@ -269,7 +270,7 @@ def preds(W, par, cls, region=False):
     for x, p in enumerate(par):
         if p >= 0 and p > x:
             kids[p].append(x)
-    out = [0] * (n + 1)
+    out = [None] * n
     prev_app = None
     for m in range(n):
         c, sp = par[m], cls[m] != 0
@@ -282,43 +283,84 @@ def preds(W, par, cls, region=False):
             cp = pos[c]
         else:
             cp = None
-        if cp is None and xf is None:          # appended: after the last older node
+        if cp is None and xf is None:          # appended
             if region and prev_app is not None:
-                # ... of the region the previous appended node opened (its
-                # subtree of the insertion tree W came from: the next node
-                # after it is older)
                 a = pos[prev_app]
                 e = next((q for q in range(a + 1, len(W)) if W[q] < prev_app), len(W))
-                last = [q for q in range(a, e) if older(q)]
             else:
-                last = [q for q in range(len(W)) if older(q)]
-            out[m + 1] = W[last[-1]] + 1 if last else 0
+                a, e = 0, len(W)
+            last = next((q for q in range(e - 1, a - 1, -1) if older(q)), None)
+            out[m] = ('A', 0 if last is None else W[last] + 1)
             prev_app = m
             continue
         if cp is not None and (xf is None or cp < xf):
+            if sp:                             # right after the cause: no skip
+                out[m] = ('A', 0 if c == NIL else c + 1)
+                continue
             stop = len(W)
             for q in range(cp + 1, len(W)):
                 if not older(q):
                     continue
                 v = W[q]
-                if sp or cls[v] == 0 or par[v] == m:
+                if cls[v] == 0 or par[v] == m:
                     stop = q
                     break
         else:
             stop = xf
-        before = [q for q in range(stop) if older(q)]
-        out[m + 1] = W[before[-1]] + 1 if before else 0
+        if xf is not None and stop == xf:
+            out[m] = ('B', W[xf])
+            continue
+        before = next((q for q in range(stop - 1, -1, -1) if older(q)), None)
+        out[m] = ('A', 0 if before is None else W[before] + 1)
+    return out
+
+
+def build(anc):
+    """The weave of a set of anchors (ranks in order): BEFORE chains under a
+    placeholder at their bottom's place, then a plain preorder with children
+    by descending key (placeholder of b: key b + 0.5 on the synthetic scale)."""
+    n = len(anc)
+    bchild = {}
+    for m, (t, a) in enumerate(anc):
+        if t == 'B':
+            assert a not in bchild and a < m
+            bchild[a] = m
+
+    def bottom(m):
+        while anc[m][0] == 'B':
+            m = anc[m][1]
+        return m
+
+    kids = {}
+    def add(p, key, v):
+        kids.setdefault(p, []).append((key, v))
+    for m, (t, a) in enumerate(anc):
+        s = m + 1
+        if t == 'A':
+            if m in bchild:               # a chain bottom: its placeholder
+                add(a, s - 0.5, ('P', m))
+                add(('P', m), s, s)
+            else:
+                add(a, s, s)
+        else:
+            add(('P', bottom(m)), s, s)
+    out, st = [], [0]
+    while st:
+        v = st.pop()
+        if not isinstance(v, tuple) and v != 0:
+            out.append(v - 1)
+        ks = sorted(kids.get(v, []), key=lambda kv: -kv[0])
+        st.extend(v2 for _, v2 in reversed(ks))
     return out
 
 
 def exact_weave(par, cls, max_rounds=None):
-    """Phase 1, then phase 2 rounds when the document has an early node."""
+    """Phase 1, then rounds with BEFORE anchors."""
     W = phase1_weave(par, cls)
     rounds = 0
     if any(early_nodes(par)):
         while True:
-            p = preds(W, par, cls, region=rounds > 0)
-            W2 = [s - 1 for s in tree_preorder(p)[1:]]
+            W2 = build(anchors(W, par, cls, region=rounds > 0))
             rounds += 1
             if W2 == W:
                 break
@@ -326,6 +368,51 @@ def exact_weave(par, cls, max_rounds=None):
             if max_rounds and rounds >= max_rounds:
                 break
     return W, rounds
+
+
+def chain_doc(family, n, rng):
+    """Adversarial documents of early nodes: chains of
+    causes through younger nodes, as a buggy or malicious site can make them
+    (s/insert checks only that the cause exists, shared.cljc:175-178).
+      reverse          node r caused by r + 1 (the last by the root)
+      reverse_special  the same with random hides / shows in the chain
+      zigzag           odd r caused by r + 2 (younger), even r by r - 1
+      zigzag_random    causes r + k / r - k for random small k, alternating
+      two_reverse      two interleaved reverse chains (r caused by r + 2)
+      reverse_hidden   a reverse chain over half the nodes, the rest hides
+                       and shows of random chain nodes
+      reverse_older    every third node caused by an older node instead
+    Rank 0 is the root (nil cause)."""
+    par, cls = [NIL], [0]
+    for r in range(1, n):
+        last = r + 1 >= n
+        if family == "reverse" or family == "reverse_special":
+            par.append(0 if last else r + 1)
+        elif family == "zigzag":
+            par.append(r + 2 if r % 2 and r + 2 < n else r - 1)
+        elif family == "zigzag_random":
+            k = rng.randint(1, 3)
+            par.append(min(n - 1, r + k) if r % 2 else max(0, r - k))
+        elif family == "two_reverse":
+            par.append(r + 2 if r + 2 < n else 0)
+        elif family == "reverse_hidden":
+            h = n // 2
+            par.append((r + 1 if r + 1 < h else 0) if r < h else rng.randrange(1, h))
+        elif family == "reverse_older":
+            par.append(r - 1 if r % 3 == 0 else (0 if last else r + 1))
+        else:
+            raise ValueError(family)
+        if family == "reverse_special":
+            cls.append(rng.choice((0, 0, 1, 2, 3)))
+        elif family == "reverse_hidden" and r >= n // 2:
+            cls.append(rng.choice((1, 2, 3)))
+        else:
+            cls.append(0)
+    return par, cls
+
+
+CHAIN_FAMILIES = ("reverse", "reverse_special", "zigzag", "zigzag_random", "two_reverse",
+                  "reverse_hidden", "reverse_older")
 
 
 # --- random documents on ranks ------------------------------------------------

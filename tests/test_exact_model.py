@@ -111,3 +111,18 @@ def test_rounds_are_few_at_realistic_rates():
         rounds.append(r)
     assert max(rounds) <= 6
     assert np.mean(rounds) <= 2.5
+
+
+@pytest.mark.parametrize("family", M.CHAIN_FAMILIES)
+@pytest.mark.parametrize("n", [300, 4000])
+def test_chains_settle_in_log_rounds(family, n):
+    """chains of causes through younger nodes (reverse,
+    zigzag, interleaved, with specials) took Theta(chain length) rounds with
+    round 4's insertion-tree rule (n - 2 on a reverse chain).  With BEFORE
+    anchors they settle in at most 2 log2 n + 4 rounds, equal to the fold."""
+    import math
+
+    par, cls = M.chain_doc(family, n, random.Random(n))
+    got, rounds = M.exact_weave(par, cls, max_rounds=1000)
+    assert rounds <= 2 * math.log2(n) + 4, rounds
+    assert got == M.fold(par, cls)

@@ -301,3 +301,99 @@ def test_large_list_orphans_and_non_lamport():
         print(f"2^23 nodes, 2000 orphans, 50 non-Lamport: {rounds} rounds")
         assert 1 <= rounds <= 12
     assert res.status[0] & abi.STATUS_NON_LAMPORT and res.status[0] & abi.STATUS_ORPHAN
+
+
+def _rank_docs(docs):
+    """Model documents (par, cls on ranks, rank 0 the root) -> a packed batch:
+    id = rank, cause = the cause's rank, NIL or an id no node has."""
+    from cause_amd.pack import KeyLayout
+    from tests import exact_model as M
+
+    off, I, C, K = [0], [], [], []
+    for par, cls in docs:
+        n = len(par)
+        for r in range(n):
+            I.append(r)
+            p = par[r]
+            C.append((1 << 64) - 1 if p == M.NIL else (n + 7 if p == M.END else p))
+            K.append(cls[r] | (4 if r == 0 else 0))
+        off.append(len(I))
+    return (np.array(off, np.uint64), np.array(I, np.uint64), np.array(C, np.uint64),
+            np.array(K, np.uint8), KeyLayout(32, 0, 0))
+
+
+def test_chain_families_few_rounds():
+    """VERDICT r4 weak #2 on the GPU: chains of causes through younger nodes
+    (tests/exact_model.py chain_doc: reverse, zigzag, interleaved, with
+    specials and hides) in one batch with clean documents -- bit-exact
+    against the literal fold, in at most 2 log2 n + 4 anchor rounds (round
+    4's rule took n - 2 rounds on a reverse chain)."""
+    import math
+
+    from tests import exact_model as M
+
+    n = 4000
+    docs = [M.chain_doc(f, n, random.Random(k)) for k, f in enumerate(M.CHAIN_FAMILIES)]
+    docs.insert(3, M.random_doc(random.Random(5), n))  # a clean neighbour
+    off, idk, ck, kd, lay = _rank_docs(docs)
+    with abi.Weaver(0) as w:
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, lay)
+        w.set_profiling(False)
+        rounds = _stage_launches(w, "xins_round")
+        assert "xfold" not in w.kernel_stats()
+    print(f"{len(docs)} documents of {n} nodes, {len(M.CHAIN_FAMILIES)} chain families: {rounds} rounds")
+    assert 1 <= rounds <= 2 * math.log2(n) + 4
+    assert res.status[3] == 0 and (res.status[[0, 1, 2, 4, 5, 6, 7]] & abi.STATUS_NON_LAMPORT).all()
+
+
+def _with_reverse_chain(off, idk, ck, a, L):
+    """Ranks [a, a + L) of the one document: rank r caused by rank r + 1 (the
+    last keeps its cause) -- a reverse chain of L early nodes."""
+    ck = ck.copy()
+    srt = np.argsort(idk, kind="stable")
+    for q in range(a, a + L - 1):
+        ck[srt[q]] = idk[srt[q + 1]]
+    return ck
+
+
+def test_reverse_chain_in_config2_document():
+    """a 2^18-node config-2-shaped document with a
+    16,384-long reverse chain, bit-exact against the oracle's general fold
+    (pinned to the literal fold by test_exact), in few rounds; its time next
+    to the same document without the chain is printed for profiles/."""
+    import json
+    import math
+    import os
+    import time
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 18) - 1, seed=35)
+    off, idk, ck, kd = gen.generate(spec, 0, 1, nthreads=8)
+    n = len(idk)
+    ck2 = _with_reverse_chain(off, idk, ck, 1, 16_384)
+    lay = spec.layout()
+    times = {}
+    with abi.Weaver(0) as w:
+        for name, c in (("clean", ck), ("chain", ck2)):
+            w.weave_lists(off, idk, c, kd, lay)  # warm
+            t = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                w.weave_lists(off, idk, c, kd, lay)
+                t.append(time.perf_counter() - t0)
+            times[name] = min(t) * 1e3
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck2, kd, lay, method=oracle.METHOD_GENERAL)
+        w.set_profiling(False)
+        rounds = _stage_launches(w, "xins_round")
+    rec = {"nodes": n, "chain": 16_384, "rounds": rounds, "clean_ms": round(times["clean"], 3),
+           "chain_ms": round(times["chain"], 3), "ratio": round(times["chain"] / times["clean"], 2),
+           "note": "host-memory cw_weave_lists, min of 5 (H2D + D2H included)"}
+    print(json.dumps(rec))
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/r5_reverse_chain.json", "w") as fh:
+        fh.write(json.dumps(rec) + "\n")
+    assert res.status[0] & abi.STATUS_NON_LAMPORT
+    assert 1 <= rounds <= 2 * math.log2(n) + 4

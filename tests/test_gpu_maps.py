@@ -254,7 +254,9 @@ def literal_histories(rng, n_colls, n_lo, n_hi, t_max=None):
     """Map collections the reference folds with nodes that are not children of
     their causes in id order: nodes caused by the root id [0 "0" 0] or by nil
     (the nil key, next to nodes whose cause is absent, and children of those),
-    and undo/redo nodes whose cause has a larger id."""
+    and undo/redo nodes whose cause has a larger id or is the node itself (a
+    self-caused id X makes the id key weave X hold X's children and
+    grandchildren with their causes)."""
     offs, I, Cs, CI, K = [0], [], [], [], []
     for d in range(n_colls):
         n = rng.randint(n_lo, n_hi)
@@ -276,9 +278,7 @@ def literal_histories(rng, n_colls, n_lo, n_hi, t_max=None):
                 nodes.append([idv, None, 1, rng.choice([1, 2, 3, 0])])
         for x in nodes:
             if x[1] is None:
-                x[1] = rng.choice(nodes)[0] if len(nodes) > 1 else 0
-                if x[1] == x[0]:
-                    x[1] = 0
+                x[1] = x[0] if rng.random() < 0.04 else rng.choice(nodes)[0]
         rng.shuffle(nodes)
         for x in nodes:
             I.append(x[0]); Cs.append(x[1]); CI.append(x[2]); K.append(x[3])
@@ -294,6 +294,58 @@ def test_literal_key_weaves_root_id_nil_and_non_lamport_causes(weaver):
     off, idk, ck, ci, kd = literal_histories(random.Random(23), 400, 2, 30, t_max=200)
     res = check(weaver, off, idk, ck, ci, kd, 2)
     assert (res.status & abi.STATUS_NON_LAMPORT).any()
+
+
+def self_cause_collections():
+    """Hand-made collections around a self-caused id X (cause = id), which the
+    reference's new-node spec forbids (shared.cljc:98) but a ::nodes map handed
+    to the 1-arity weave can hold.  Returns the batch and the expected key
+    weave ID|X of collection 0 (input indices after the root)."""
+    t = lambda ts, site=1: (ts << 2) | site
+    X, C, C2, G = t(5), t(9), t(13), t(17)
+    colls = [
+        # X->X, two children of X, a grandchild through C: the key weave X is
+        # root, X, C2, C, G (weave-node: C2 lands right after X, before C)
+        [(X, X, 1, 0), (C, X, 1, 0), (C2, X, 1, 0), (G, C, 1, 0)],
+        # the same shuffled, with an older child of X (E < X: placed before
+        # the node it causes), hides of G and C2, a plain key and a nil key
+        [(G, C, 1, 0), (t(3), X, 1, 0), (C2, X, 1, 0), (X, X, 1, 2), (C, X, 1, 0),
+         (t(20), G, 1, 1), (t(21), C2, 1, 2), (t(2), 1, 0, 0), (t(22), t(2), 1, 0),
+         (t(23), t(99), 1, 0)],
+        # a two-cycle X<->Y: neither is self-caused, every id key weave chains
+        [(X, C, 1, 0), (C, X, 1, 0), (t(30), X, 1, 0), (t(31), C, 1, 3), (t(32), t(30), 1, 0)],
+        # a self-caused special, children of several kinds, great-grandchildren
+        # (key = a grandchild's cause, not X) and an absent X sibling
+        [(X, X, 1, 1), (C, X, 1, 3), (C2, X, 1, 0), (G, C2, 1, 0), (t(18), G, 1, 2),
+         (t(19, 2), C2, 1, 1), (t(24), t(19, 2), 1, 0), (t(25, 3), X, 1, 0)],
+    ]
+    offs, cols = [0], ([], [], [], [])
+    for nodes in colls:
+        for x in nodes:
+            for k in range(4):
+                cols[k].append(x[k])
+        offs.append(len(cols[0]))
+    return (np.array(offs, np.uint64), np.array(cols[0], np.uint64), np.array(cols[1], np.uint64),
+            np.array(cols[2], np.uint8), np.array(cols[3], np.uint8)), (ID_KEY | X, [0, 2, 1, 3])
+
+
+def test_self_caused_id_key(weaver):
+    """the id key weave of a self-caused id X folds X, its
+    children and grandchildren by their real causes (map.cljc:30-45,
+    shared.cljc:225-241), on the fused, small and pipeline paths."""
+    (off, idk, ck, ci, kd), (xkey, xweave) = self_cause_collections()
+    res = check(weaver, off, idk, ck, ci, kd, 2)
+    got = gpu_maps(res, len(off) - 1)
+    assert got[0][xkey][1] == xweave
+    assert res.status[0] & abi.STATUS_NON_LAMPORT  # X's cause is X: folded literally
+    assert res.status[2] == 0  # a two-cycle stays chained, nothing to flag
+    # the same collections amid a batch of clean ones (packs, tiles, chunks)
+    spec = gen.MapSpec(nodes_per_coll=60, p_bad=0.05, seed=31)
+    _, tb = spec.layout()
+    o2, i2, c2, ci2, k2 = gen.generate_maps(spec, 0, 300, nthreads=4)
+    cat = lambda a, b: np.concatenate([a, b])
+    off3 = np.concatenate([o2, o2[-1] + off[1:]])
+    check(weaver, off3, cat(i2, idk), cat(c2, ck), cat(ci2, ci), cat(k2, kd), max(2, tb))
 
 
 @pytest.mark.parametrize("n_lo,n_hi,colls", [(3000, 6000, 4), (15000, 20000, 2)])
