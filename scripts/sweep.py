@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--nodes", type=int, default=50_000)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--check", action="store_true", help="compare outputs across variants")
+    ap.add_argument("--yarns", action="store_true", help="ask for yarn_perm too (refresh-caches)")
     a = ap.parse_args()
     variants = json.loads(a.variants)
     import torch
@@ -54,6 +55,8 @@ def main():
          "visible_count": torch.empty(D, dtype=torch.int32, device=dev),
          "max_ts": torch.empty(D, dtype=torch.int64, device=dev),
          "status": torch.empty(D, dtype=torch.int32, device=dev)}
+    if a.yarns:
+        o["yarn_perm"] = torch.empty(N, dtype=torch.int32, device=dev)
     ptrs = {k: t.data_ptr() for k, t in o.items()}
     ref = None
     results = {i: [] for i in range(len(variants))}
@@ -72,9 +75,10 @@ def main():
             torch.cuda.synchronize()
             if a.check:
                 if ref is None:
-                    ref = (o["weave_perm"].clone(), o["visible_bits"].clone())
+                    ref = {k: t.clone() for k, t in o.items()}
                 else:
-                    assert torch.equal(o["weave_perm"], ref[0]) and torch.equal(o["visible_bits"], ref[1])
+                    for k, t in o.items():
+                        assert torch.equal(t, ref[k]), f"{k} differs from variant 0"
                 assert int(o["status"].max()) == 0
             w.set_profiling(True)
             w.reset_kernel_stats()

@@ -2,11 +2,13 @@
   "Drop-in weave-fns for CausalList and CausalMap on the MI355X.
 
   `weave` has the arities and contract of c.list/weave (list.cljc:20-34):
-  (weave ct) is the full reweave; (weave ct node) and (weave ct node more)
-  return ct unchanged when (first node) is not in ::nodes and otherwise give
-  the same weave as the full reweave (incremental insertion in any causal order
-  equals it, SURVEY F7), so every arity is one GPU call.  `map-weave` is the
-  same for c.map/weave (map.cljc:21-45).  Neither throws for a ::nodes map the
+  (weave ct) is the full reweave, one GPU call; (weave ct node) and
+  (weave ct node more) are the reference's own incremental weave-node step
+  (list.cljc:29-34: O(n) on the host, no marshalling), captured before
+  install! rebinds the var -- a single insert never pays for a whole-document
+  round trip.  The GPU weave is bit-exact with the fold, so the incremental
+  steps continue from it unchanged.  `map-weave` is the same for c.map/weave
+  (map.cljc:21-45).  The full reweave never throws for a ::nodes map the
   reference accepts: orphans, non-Lamport and nil causes are rewoven by the
   library's literal fold (exact path).
 
@@ -18,6 +20,11 @@
             [clojure.spec.alpha :as spec])
   (:import (causal.gpu CauseWeave CauseWeave$Node CauseWeave$ListResult CauseWeave$MapResult)
            (java.util.function Supplier)))
+
+;; The reference's weave-fns as loaded, before install! rebinds the vars: the
+;; incremental arities (one node, or one tx run) stay on the host.
+(defonce ^:private ref-list-weave c.list/weave)
+(defonce ^:private ref-map-weave c.map/weave)
 
 ;; One context per thread: a cw_ctx is not thread-safe (include/causeweave.h),
 ;; and swap! may call a weave-fn from several threads at once.
@@ -69,11 +76,9 @@
 (defn weave
   "c.list/weave (list.cljc:20-34) on the GPU."
   ([causal-tree] (assoc causal-tree ::s/weave (::s/weave (first (weave-batch [causal-tree])))))
-  ([causal-tree node] (weave causal-tree node nil))
+  ([causal-tree node] (ref-list-weave causal-tree node nil))
   ([causal-tree node more-consecutive-nodes-in-same-tx]
-   (if (not (get-in causal-tree [::s/nodes (first node)]))
-     causal-tree
-     (weave causal-tree))))
+   (ref-list-weave causal-tree node more-consecutive-nodes-in-same-tx)))
 
 (defn refresh-caches
   "s/refresh-caches with this weave: spin, refresh-ts and the weave from one call."
@@ -126,11 +131,8 @@
 (defn map-weave
   "c.map/weave (map.cljc:21-45) on the GPU."
   ([causal-tree] (first (map-weave-batch [causal-tree])))
-  ([causal-tree node] (map-weave causal-tree node nil))
-  ([causal-tree [id] more-nodes]
-   (if (not (get-in causal-tree [::s/nodes id]))
-     causal-tree
-     (map-weave causal-tree))))
+  ([causal-tree node] (ref-map-weave causal-tree node nil))
+  ([causal-tree node more-nodes] (ref-map-weave causal-tree node more-nodes)))
 
 (defn install!
   "Route CausalList and CausalMap through the GPU: their protocol methods pass

@@ -279,6 +279,14 @@ public final class CauseWeave implements AutoCloseable {
     public int status;
   }
 
+  /** A map id packed as ts | site rank | tx; the root id [0 "0" 0] is 0 whatever
+   *  rank "0" has (cause_amd/pack.py pack_maps). */
+  static long packMapId(String[] ranks, long ts, String site, long tx, int siteBits, int txBits) {
+    if (ts == 0 && tx == 0 && site.equals("0")) return 0L;
+    long rank = Arrays.binarySearch(ranks, site);
+    return (ts << (siteBits + txBits)) | (rank << txBits) | tx;
+  }
+
   /** c.map/weave 1-arity (map.cljc:21-45) + active-node (:47-59) for a batch of
    *  collections; keyToken[j] = the key token of node j when causeKind is 2. */
   public MapResult[] weaveMaps(List<List<Node>> colls, List<long[]> keyTokens, int tokenBits)
@@ -291,8 +299,14 @@ public final class CauseWeave implements AutoCloseable {
       List<Node> withRoot = new ArrayList<>(d);
       withRoot.add(new Node(0, "0", 0, 1, 0, null, 0, KIND_ROOT));
       String[] r = internSites(withRoot);
-      if (!r[0].equals("0"))
-        throw new IllegalArgumentException("a site-id sorts before \"0\" (the virtual root must pack to 0)");
+      // site-ids may sort before "0" (String.compareTo, e.g. " a ", list_test.cljc:85-96):
+      // the virtual root [0 "0" 0] still packs to 0 and so does a cause naming it; an
+      // id with ts >= 1 packs above 0 whatever its site's rank.  Only a node id that
+      // itself sorts before the root id (ts 0) is refused -- as cause_amd/pack.py does.
+      for (Node n : d)
+        if (n.ts == 0 && n.site.compareTo("0") < 0)
+          throw new IllegalArgumentException("map node id [0 \"" + n.site + "\" " + n.tx
+              + "] sorts before the root id");
       ranks.add(r);
       msite = Math.max(msite, r.length - 1);
       for (Node n : d) {
@@ -316,11 +330,9 @@ public final class CauseWeave implements AutoCloseable {
         long[] tok = keyTokens.get(d);
         int k = 0;
         for (Node n : colls.get(d)) {
-          long site = Arrays.binarySearch(r, n.site);
-          id.setAtIndex(JAVA_LONG, j, (n.ts << (siteBits + txBits)) | (site << txBits) | n.tx);
+          id.setAtIndex(JAVA_LONG, j, packMapId(r, n.ts, n.site, n.tx, siteBits, txBits));
           if (n.causeKind == 0) {
-            long cs = Arrays.binarySearch(r, n.csite);
-            cause.setAtIndex(JAVA_LONG, j, (n.cts << (siteBits + txBits)) | (cs << txBits) | n.ctx);
+            cause.setAtIndex(JAVA_LONG, j, packMapId(r, n.cts, n.csite, n.ctx, siteBits, txBits));
             isId.set(JAVA_BYTE, j, (byte) 1);
           } else if (n.causeKind == 1) {  // nil: the nil key (cause_is_id = 2)
             cause.setAtIndex(JAVA_LONG, j, 0L);
