@@ -897,7 +897,16 @@ def main():
     # inside the timed region
     name = dom
     launches, ms, by = stats_dom[dom]
-    achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    achieved_kernel = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    # SURVEY 8(d)'s headline algorithmic bytes: B_io per node = id + cause +
+    # kind in, weave_perm + one visible bit out (21.125 B with u64 keys, 13.125
+    # with u32).  The fused per-document kernel does the whole weave, so its
+    # algorithmic bytes are B_io x the nodes of a launch; its own scratch
+    # handoffs (achieved_kernel_scratch) are not algorithmic bytes.
+    b_io = (4 + 4 + 1 + 4 + 1 / 8) if k32 else (8 + 8 + 1 + 4 + 1 / 8)
+    whole = name == "weave"
+    by_io = N * b_io * launches / a.steps if whole else by
+    achieved = by_io / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     kernel_ms_total = sum(v[1] for v in stats.values())
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
@@ -927,9 +936,17 @@ def main():
                                        else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "frac_io": achieved / HBM_PEAK_GBS,
+                         "bytes_alg_per_node": b_io if whole else by / launches / N,
+                         "bytes_alg_note": ("B_io (SURVEY 8d): id + cause + kind in, weave_perm + "
+                                            "visible bit out, per node of the launch" if whole else
+                                            "the kernel's algorithmic bytes (DESIGN 5)"),
+                         "achieved_kernel_scratch": achieved_kernel,
+                         "frac_kernel_scratch": achieved_kernel / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_note": tnote,
                          "launches_per_step": launches / a.steps,
                          "kernel_ms_per_step": ms / a.steps},
+            "frac_step_io": value * b_io / 1e9 / HBM_PEAK_GBS / world,
             "cpu_baseline": cpu,
             "kernels_ms_per_step": {k: round(v[1] / a.steps, 4) for k, v in
                                     sorted(stats.items(), key=lambda kv: -kv[1][1])},

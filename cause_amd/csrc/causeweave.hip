@@ -767,76 +767,16 @@ __global__ __launch_bounds__(1024) void k_gd_add(uint32_t *__restrict__ dir, uin
   if (e < E) dir[e * GD_WORDS] += sums[blockIdx.x];
 }
 
-// The same directory from the SORTED ids (the giant path after its id sort):
-// neighbouring lanes set bits of the same or the next words, so the atomics
-// stay in L2; a repeated id shows as two equal neighbours.
-__global__ __launch_bounds__(256) void k_gd_set_sorted(const uint64_t *__restrict__ skey, uint32_t n,
-                                                       uint64_t E, uint32_t *__restrict__ dir,
-                                                       uint32_t *__restrict__ status) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
-  bool dup = false, out = false;
-  uint64_t w = ~0ull;  // word index (the ids are sorted: equal words are neighbouring lanes)
-  uint32_t v = 0;
-  if (i < n) {
-    const uint64_t x = skey[i];
-    dup = i > 0 && skey[i - 1] == x;
-    uint64_t e;
-    uint32_t b;
-    gd_split(x, e, b);
-    if (e < E) {
-      w = e * GD_WORDS + 1 + (b >> 5);
-      v = 1u << (b & 31);
-    } else {
-      out = true;
-    }
-  }
-  // OR of each run of lanes with the same word; the run's first lane writes it
-  // (a plain store; atomically only for runs that may continue in the
-  // neighbouring waves)
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = __shfl_down(v, o, 64);
-    const uint64_t wy = __shfl_down(w, o, 64);
-    if (lane + o < 64 && wy == w) v |= y;
-  }
-  const uint64_t wp = __shfl_up(w, 1, 64);
-  const uint64_t wlast = __shfl(w, 63, 64);
-  if (w != ~0ull && (lane == 0 || wp != w)) {
-    if (lane == 0 || w == wlast) atomicOr(&dir[w], v);
-    else dir[w] = v;
-  }
-  const uint64_t d = __ballot(dup), o = __ballot(out);
-  if ((threadIdx.x & 63) == 0 && (d | o))
-    atomicOr(status, (d ? (uint32_t)CW_STATUS_DUP : 0u) | (o ? (uint32_t)CW_STATUS_INTERNAL : 0u));
-}
-
-// Word 0 of each directory entry from the sorted ids, no scan: the ones before
-// entry e are the rank of the first id at or above its range (like k_index_flat's
-// buckets, 480 keys wide); the entries a thread starts are zeroed for
-// k_gd_set_sorted.  Entries past the largest id are never read.
-__global__ __launch_bounds__(256) void k_gd_first(const uint64_t *__restrict__ skey, uint32_t n,
-                                                  uint64_t E, uint32_t *__restrict__ dir) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t e = min(skey[i] / GD_KEYS, E - 1);
-  const uint64_t e0 = i > 0 ? min(skey[i - 1] / GD_KEYS, E - 1) + 1 : 0;
-  for (uint64_t x = e0; x <= e; x++) {
-    uint4 *q = reinterpret_cast<uint4 *>(dir + x * GD_WORDS);
-    q[0] = make_uint4(i, 0, 0, 0);
-    q[1] = q[2] = q[3] = make_uint4(0, 0, 0, 0);
-  }
-}
-
-// The same directory in ONE pass over the sorted ids (k_gd_first +
-// k_gd_set_sorted read them twice and wrote every entry twice, the second time
-// as scattered 4-byte words: 28 ms at 2e9 nodes).  A block takes GDB_KEYS
+// The directory in ONE pass over the sorted ids (round 3's two kernels read
+// them twice and wrote every entry twice, the second time as scattered 4-byte
+// words: 28 ms at 2e9 nodes).  A block takes GDB_KEYS
 // consecutive sorted ids and builds the entries they fall in in LDS -- one
 // slot per distinct entry, bits by LDS atomics, word 0 = the index of the
 // entry's first id -- then writes each as a whole 64-byte line.  Every entry
 // has one writer, the block holding its first id ("lead"): ids at the start
 // of a block that continue the previous block's entry are left to that block,
 // which reads ahead for them (<= GD_KEYS ids).  Entries between two ids get
-// word 0 = the next id's index from that id's thread, as in k_gd_first.
+// word 0 = the next id's index from that id's thread.
 constexpr uint32_t GDB_KEYS = 512;
 __global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ skey, uint32_t n,
                                                   uint64_t E, uint32_t *__restrict__ dir,
@@ -926,7 +866,7 @@ __global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ s
 // gathered by input index (as k_join), the cause's rank from one directory
 // line instead of the bucket index and a search.
 constexpr int GJOIN_ITEMS = 4;
-// ckk (CW_GPACK): cause | kind << 56 in one word per input node (k_gpack), so
+// ckk: cause | kind << 56 in one word per input node (k_gpack), so
 // the gather by input index is one random line a node instead of two
 __global__ __launch_bounds__(256) void k_gpack(const uint64_t *__restrict__ cause_key,
                                                const uint8_t *__restrict__ kind, uint32_t n,
@@ -952,7 +892,7 @@ __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey
   const uint32_t i0 = blockIdx.x * (256 * GJOIN_ITEMS) + threadIdx.x;
   // causes are looked up only up to the largest id the directory holds: ids
   // past its E entries (a key_bits too small for the batch) were flagged
-  // INTERNAL by k_gd_set_sorted and must not be read
+  // INTERNAL by the directory build and must not be read
   const uint64_t kmax = min(skey[n - 1], E * GD_KEYS - 1);
   uint32_t gi[GJOIN_ITEMS];
   uint64_t ck[GJOIN_ITEMS];
@@ -1355,6 +1295,210 @@ __host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) 
   return sg * 16 + 4 * ((nmax + 1) / 2) + 8 * ((nmax + 31) / 32);
 }
 
+// Index of the o-th set bit (0-based) of w (o < popc(w)).
+__device__ __forceinline__ uint32_t select_bit(uint32_t w, uint32_t o) {
+  uint32_t pos = 0, c;
+  c = __popc(w & 0xFFFFu);
+  if (o >= c) { o -= c; w >>= 16; pos += 16; }
+  c = __popc(w & 0xFFu);
+  if (o >= c) { o -= c; w >>= 8; pos += 8; }
+  c = __popc(w & 0xFu);
+  if (o >= c) { o -= c; w >>= 4; pos += 4; }
+  c = __popc(w & 0x3u);
+  if (o >= c) { o -= c; w >>= 2; pos += 2; }
+  return pos + ((o >= (w & 1u)) ? 1u : 0u);
+}
+
+// Ordering LDS accesses of one wave across its lanes (a wave's LDS operations
+// run in order: only the compiler has to keep them so).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// The yarns of one document (spin 1-arity, shared.cljc:121-132: the id order
+// partitioned by site, id-ascending inside a site) written as whole runs
+// (round 5; the per-thread version scattered each node's 4 bytes over up to
+// 16 site streams: 3.9 ms of a config-2 step).  The directory (sdir: groups of
+// 96 id bits, x = the rank of the group's first id) and p16 (input index by
+// rank) are the front end's.  The site of an id repeats within a directory
+// word (site_shift + site_bits <= 5): a word's ids of site s are the bits of
+// a fixed mask.
+//   1. per wave (its threads' groups, a contiguous rank range): site counts
+//      by masked popcounts -> per-wave, per-site output cursors;
+//   2. per wave, rounds of 64 x K consecutive ranks: each lane takes K ranks
+//      (its start found by a binary search over the groups' ranks and a bit
+//      select), the wave ranks its elements by site (packed 16-bit counters,
+//      wave scans), stages them in LDS site by site, and writes each site's
+//      run of the round to its cursor: consecutive lanes, consecutive words.
+// stage: the free LDS after p16 (>= NT * K u16 entries; its first 1 KiB also
+// holds the per-wave counts of step 1).
+template <int NT>
+__device__ __forceinline__ void yarn_staged(const uint4 *sdir, uint32_t G, uint32_t n,
+                                         const uint16_t *p16, uint16_t *stage, uint32_t K,
+                                         uint32_t *__restrict__ yD, uint32_t site_shift,
+                                         uint32_t site_bits, uint32_t *wtot) {
+  constexpr uint32_t NW = NT / 64;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t S = 1u << site_bits, smask = S - 1;
+  const uint32_t per = (G + NT - 1) / NT;
+  const uint32_t gw0 = min(G, wv * 64 * per), gw1 = min(G, (wv + 1) * 64 * per);
+  // (the ids the directory holds: fewer than n when an id repeats -- a DUP
+  // document, whose outputs are unspecified but whose walk must stay inside)
+  uint32_t nid = 0;
+  if (G) {
+    const uint4 ql = sdir[G - 1];
+    nid = min(n, ql.x + __popc(ql.y) + __popc(ql.z) + __popc(ql.w));
+  }
+  const uint32_t rw0 = gw0 < G ? min(nid, sdir[gw0].x) : nid;
+  const uint32_t rw1 = gw1 < G ? min(nid, sdir[gw1].x) : nid;
+  // the mask of site s inside a 32-bit word
+  const uint32_t bw = 1u << site_shift, P = 1u << (site_shift + site_bits);
+  const uint32_t blk = bw >= 32 ? 0xFFFFFFFFu : (1u << bw) - 1u;
+  auto smask_of = [&](uint32_t s) {
+    uint32_t m = 0;
+    for (uint32_t o = 0; o < 32; o += P) m |= (blk << (s * bw)) << o;
+    return m;
+  };
+  // 1. per-wave site counts: lane s counts site s over the wave's groups
+  // (the mask lives in the lane: wave-uniform masks would spill SGPRs)
+  uint32_t *tab = reinterpret_cast<uint32_t *>(stage);  // [NW][16] counts
+  {
+    const uint32_t msk = lane < S ? smask_of(lane) : 0u;
+    uint32_t mine = 0;
+    for (uint32_t g = gw0; g < gw1; g++) {
+      const uint4 q = sdir[g];
+      mine += __popc(q.y & msk) + __popc(q.z & msk) + __popc(q.w & msk);
+    }
+    if (lane < 16) tab[wv * 16 + lane] = mine;
+  }
+  __syncthreads();
+  // lane s: this wave's cursor for site s = (sites before s, whole document)
+  // + (site s in earlier waves)
+  uint32_t cur = 0;
+  {
+    uint32_t tot = 0, before = 0;
+    if (lane < S)
+      for (uint32_t w = 0; w < NW; w++) {
+        const uint32_t v = tab[w * 16 + lane];
+        tot += v;
+        before += w < wv ? v : 0u;
+      }
+    uint32_t inc = tot;  // exclusive scan of the site totals over lanes 0..15
+    for (uint32_t o = 1; o < 16; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    cur = inc - tot + before;
+  }
+  __syncthreads();  // (the count table is staging from here on)
+  uint16_t *const stw = stage + wv * 64 * K;
+  for (uint32_t R = rw0; R < rw1; R += 64 * K) {
+    const uint32_t t = R + K * lane;
+    const uint32_t cnt = t < rw1 ? min(K, rw1 - t) : 0u;
+    uint32_t sites[8], vals[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) sites[j] = vals[j] = 0;
+    if (cnt) {
+      // the group holding rank t: the last with x <= t
+      uint32_t lo = gw0, hi = gw1;  // x(lo) <= t < x(hi)
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sdir[mid].x <= t) lo = mid; else hi = mid;
+      }
+      uint32_t g = lo, k;
+      uint4 q = sdir[g];
+      uint32_t o = t - q.x, m;
+      const uint32_t p0 = __popc(q.y), p1 = __popc(q.z);
+      if (o < p0) { k = 0; m = q.y; }
+      else if (o < p0 + p1) { k = 1; m = q.z; o -= p0; }
+      else { k = 2; m = q.w; o -= p0 + p1; }
+      m &= 0xFFFFFFFFu << select_bit(m, o);
+#pragma unroll
+      for (uint32_t j = 0; j < 8; j++) {
+        if (j >= cnt) break;
+        while (m == 0 && g < G) {
+          if (++k == 3) {
+            if (++g == G) break;
+            q = sdir[g];
+            k = 0;
+          }
+          m = k == 0 ? q.y : k == 1 ? q.z : q.w;
+        }
+        const uint32_t b = (uint32_t)__ffs(m) - 1;
+        m &= m - 1;
+        sites[j] = (b >> site_shift) & smask;
+        vals[j] = p16[t + j];
+      }
+    }
+    // the wave's elements of this round ranked by site
+    uint32_t own[8], ex[8];
+#pragma unroll
+    for (uint32_t w = 0; w < 8; w++) own[w] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+      if (j >= cnt) break;
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++)
+        if (w == (sites[j] >> 1)) own[w] += 1u << ((sites[j] & 1) * 16);
+    }
+    // lane s (< 16): the round's count of site s and its exclusive prefix over
+    // the sites (kept lane by lane: wave-uniform tables would spill SGPRs)
+    uint32_t tl = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 8; w++) {
+      uint32_t inc = own[w];
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      ex[w] = inc - own[w];
+      const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);  // (a VGPR broadcast, no SGPR)
+      if (w == (lane >> 1)) tl = (tot >> ((lane & 1) * 16)) & 0xFFFFu;
+    }
+    if (lane >= 16) tl = 0;
+    uint32_t offl = tl;  // exclusive scan over lanes 0..15
+    for (uint32_t o = 1; o < 16; o <<= 1) {
+      const uint32_t y = __shfl_up(offl, o, 64);
+      if (lane >= o) offl += y;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)offl, 15, 64);
+    offl -= tl;
+    // stage site by site
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+      const bool on = j < cnt;
+      const uint32_t s = sites[j], sh = (s & 1) * 16;
+      uint32_t e = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++)
+        if (on && w == (s >> 1)) {
+          e = (ex[w] >> sh) & 0xFFFFu;
+          ex[w] += 1u << sh;
+        }
+      const uint32_t base_s = (uint32_t)__shfl((int)offl, (int)s, 64);  // (every lane takes part)
+      if (on) stw[base_s + e] = (uint16_t)vals[j];
+    }
+    wave_lds_sync();
+    // each site's run of this round to its cursor
+    for (uint32_t i0 = 0; i0 < total; i0 += 64) {  // (wave-uniform: the shuffles see every lane)
+      const uint32_t i = i0 + lane;
+      uint32_t s = 0;  // the last site whose run starts at or before i
+#pragma unroll
+      for (uint32_t step = 8; step > 0; step >>= 1) {
+        const uint32_t o = (uint32_t)__shfl((int)offl, (int)(s + step), 64);
+        if (s + step < 16 && o <= i) s += step;
+      }
+      const uint32_t o0 = (uint32_t)__shfl((int)offl, (int)s, 64);
+      const uint32_t c = (uint32_t)__shfl((int)cur, (int)s, 64) + i - o0;
+      if (i < total && c < n) yD[c] = stw[i];
+    }
+    cur += tl;  // lane s's cursor moves past site s's run
+    wave_lds_sync();
+  }
+}
+
 // one document d (the whole workgroup); lds: the dynamic LDS.  Returns false
 // when the document's ids leave the directory (big[0] counts it).  PT / VT:
 // the width of par / sval (u16 inside k_weave_doc: n < 2^16); skind may be
@@ -1370,8 +1514,9 @@ __device__ __forceinline__ bool front_doc(
     uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t d, uint4 *sdir,
-    uint32_t *__restrict__ yarn = nullptr, uint32_t site_shift = 0, uint32_t site_bits = 0) {
+    unsigned long long *__restrict__ tprof, uint32_t d, uint4 *sdir,
+    uint32_t *__restrict__ yarn = nullptr, uint32_t site_shift = 0, uint32_t site_bits = 0,
+    uint32_t lds_total = 0) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (tprof) {
@@ -1514,19 +1659,8 @@ __device__ __forceinline__ bool front_doc(
   __syncthreads();
   stamp(1);
   // par, skind, special/hide bitmaps per 4096-rank tile, coalesced
-  // eff: a non-special's parent goes out as its effective parent (SURVEY F5:
-  // it climbs through special causes, here in LDS), so the tree need not climb
-  auto spec = [&](uint32_t x) { return ((clsA[x >> 5] | clsB[x >> 5]) >> (x & 31)) & 1u; };
   for (uint32_t r = tid; r < n; r += NT) {
-    uint32_t p = p16[r];
-    if (eff) {
-      p = p < r ? p : 0u;
-      if (!spec(r))
-        while (p != 0 && spec(p)) {
-          const uint32_t pp = p16[p];
-          p = pp < p ? pp : 0u;
-        }
-    }
+    const uint32_t p = p16[r];
     lane_at(parD, r) = (PT)p;
     const uint32_t a = (clsA[r >> 5] >> (r & 31)) & 1u, b = (clsB[r >> 5] >> (r & 31)) & 1u;
     if (skindD) lane_at(skindD, r) = (uint8_t)(a | (b << 1));  // the class, as k_fplace writes it
@@ -1576,7 +1710,16 @@ __device__ __forceinline__ bool front_doc(
           skey[base + r++] = (uint64_t)g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
     }
   }
-  if (yarn) {
+  // the yarns through per-wave LDS staging (round 5): the site pattern of an id
+  // repeats within a 32-bit directory word (site_shift + site_bits <= 5), and
+  // the free LDS after p16 (at least the class bitmaps, dead by now) holds a
+  // staging run of >= 2 ranks per lane
+  const uint32_t y_used = sg * 16 + 4 * ((n + 1) / 2);
+  const uint32_t y_lanes_k = lds_total > y_used ? (lds_total - y_used) / (NT * 2) : 0u;
+  if (yarn && site_shift + site_bits <= 5 && y_lanes_k >= 2) {
+    yarn_staged<NT>(sdir, G, n, p16, reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(sdir) + y_used),
+                    min(y_lanes_k, 8u), yarn + base, site_shift, site_bits, wtot);
+  } else if (yarn) {
     // the yarns (spin: the id order partitioned by site, id-ascending inside a
     // site) from the same directory walk: a thread's groups are a contiguous
     // range of ranks, so per-site counts, block prefix sums over the threads
@@ -1658,10 +1801,10 @@ __global__ __launch_bounds__(NT) void k_front(
     uint8_t *__restrict__ skind, uint32_t *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t eff, uint32_t doc0 = 0) {
+    unsigned long long *__restrict__ tprof, uint32_t doc0 = 0) {
   extern __shared__ __attribute__((aligned(16))) uint4 lds_fr[];
   front_doc<NT>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey, rank16,
-                max_ts, ts_shift, status, big, tprof, eff, doc0 + blockIdx.x, lds_fr);
+                max_ts, ts_shift, status, big, tprof, doc0 + blockIdx.x, lds_fr);
 }
 
 // dst bits [off, off + nbits) |= src bits [0, nbits) (dst zeroed beforehand).
@@ -2026,11 +2169,10 @@ __host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
   return ((nmax + 31) / 32) * 8 + ((nmax + 1) / 2) * 4;  // two bitmaps + u16 table
 }
 
-// MODE (A/B knob CW_TL_MODE): bit 0 = one CAS per insert (else CAS + exchange),
-// bit 1 = the special-table reads and the next parents go out before the keys,
-// bit 2 = a group whose parent lies in the tile (69% of config-2 nodes) keeps
-// its list head in a direct table indexed by (class, parent - tile start): one
-// exchange instead of a claiming CAS + exchange (with bit 0 clear)
+// MODE 4 (the one built; round 3's A/B variants 0-3 lost and are gone): a
+// group whose parent lies in the tile (69% of config-2 nodes) keeps its list
+// head in a direct table indexed by (class, parent - tile start): one exchange
+// instead of a claiming CAS + exchange; other groups go through the hash
 // one document d (the whole workgroup); lds: the dynamic LDS (16-byte aligned)
 template <int NT, int TILE_T, bool PROF, int MODE, typename PT = uint32_t>
 __device__ __forceinline__ void tree_l_doc(
@@ -2052,10 +2194,11 @@ __device__ __forceinline__ void tree_l_doc(
   };
   stamp(-1);
   // one tile's group-key hash: hk[slot] = group key (0 = empty), hh[slot] =
-  // the head of the slot's member list (a tile index; MODE bit 0 packs both
-  // into hw[slot] = key << HB | head); nxt: next member, TL_END ends.  The
-  // fallback sort's tkey/trank/tns and sweep 2's T live in the same buffer.
-  constexpr bool DH = (MODE & 4) && !(MODE & 1);
+  // the head of the slot's member list (a tile index); nxt: next member,
+  // TL_END ends.  The fallback sort's tkey/trank/tns and sweep 2's T live in
+  // the same buffer.
+  static_assert(MODE == 4, "k_tree_l is built with direct list heads only");
+  constexpr bool DH = true;
   constexpr uint32_t HS = DH ? TILE_T : 2 * TILE_T, GMAX = 16, HB = TILE_T <= 2048 ? 11 : 12;
   static_assert(TILE_T <= (1u << HB) && 17 + HB <= 32, "slot word layout");
   static_assert(2 * HS + (DH ? 2 * TILE_T : 0) == 4 * TILE_T, "hash (+ direct heads) = 4 TILE_T words");
@@ -2063,7 +2206,7 @@ __device__ __forceinline__ void tree_l_doc(
   uint32_t(*const wcnt)[SUB_BINS] = reinterpret_cast<uint32_t(*)[SUB_BINS]>(lds + 4 * TILE_T);
   uint16_t *const nxt = reinterpret_cast<uint16_t *>(lds + 4 * TILE_T + (NT / 64) * SUB_BINS);
   uint32_t *const bm = lds + tree_l_tile_bytes(NT, TILE_T) / 4;
-  uint32_t *const hw = hbuf, *const hk = hbuf, *const hh = hbuf + HS;  // MODE 1 / MODE 0
+  uint32_t *const hw = hbuf, *const hk = hbuf, *const hh = hbuf + HS;
   uint32_t *const tkey = hbuf, *const trank = hbuf + TILE_T, *const tns = hbuf + 2 * TILE_T;
   uint32_t *const ptab = tns;
   __shared__ uint32_t run[64];
@@ -2122,7 +2265,7 @@ __device__ __forceinline__ void tree_l_doc(
   auto clear_hash = [&]() {
     for (uint32_t i = tid; i < HS; i += NT) {
       hw[i] = 0;
-      if (!(MODE & 1)) hh[i] = TL_END;
+      hh[i] = TL_END;
     }
     if (DH)
       for (uint32_t i = tid; i < 2 * TILE_T; i += NT) hbuf[2 * HS + i] = TL_END;
@@ -2154,7 +2297,6 @@ __device__ __forceinline__ void tree_l_doc(
     };
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) ptv[k] = 0;
-    if (MODE & 2) load_ptvS();
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = wb_elem<IT>(k), r = r0 + j;
@@ -2177,7 +2319,7 @@ __device__ __forceinline__ void tree_l_doc(
       }
     }
     stamp(9);
-    if (!(MODE & 2)) load_ptvS();
+    load_ptvS();
     stamp(10);
     // insert: claim the key's slot (linear probing), push onto its list
 #pragma unroll
@@ -2185,7 +2327,7 @@ __device__ __forceinline__ void tree_l_doc(
       const uint32_t j = wb_elem<IT>(k), kk = key[k];
       slot[k] = 0;
       if (j < len && kk) {
-        uint32_t h = (kk * 0x9E3779B1u) >> (32 - __builtin_ctz(HS)), cmp = 0u;
+        uint32_t h = (kk * 0x9E3779B1u) >> (32 - __builtin_ctz(HS));
         const uint32_t e = (kk >> 1) - 1;
         if (DH && e >= r0) {  // slot = the head's word in hbuf
           const uint32_t s = 2 * HS + (kk & 1) * TILE_T + (e - r0);
@@ -2193,28 +2335,12 @@ __device__ __forceinline__ void tree_l_doc(
           slot[k] = s;
           continue;
         }
-        if (MODE & 1) {
-          for (;;) {  // one CAS for a new group; pushes onto a group's list retry
-            const uint32_t old = atomicCAS(&hw[h], cmp, (kk << HB) | j);
-            if (old == cmp) {
-              nxt[j] = (uint16_t)(cmp ? (cmp & ((1u << HB) - 1)) : TL_END);
-              break;
-            }
-            if ((old >> HB) == kk) {
-              cmp = old;
-            } else {
-              h = (h + 1) & (HS - 1);
-              cmp = 0u;
-            }
-          }
-        } else {
-          for (;;) {  // claim the key (hk), then push (exchange on hh)
-            const uint32_t old = atomicCAS(&hk[h], 0u, kk);
-            if (old == 0u || old == kk) break;
-            h = (h + 1) & (HS - 1);
-          }
-          nxt[j] = (uint16_t)atomicExch(&hh[h], j);
+        for (;;) {  // claim the key (hk), then push (exchange on hh)
+          const uint32_t old = atomicCAS(&hk[h], 0u, kk);
+          if (old == 0u || old == kk) break;
+          h = (h + 1) & (HS - 1);
         }
+        nxt[j] = (uint16_t)atomicExch(&hh[h], j);
         slot[k] = DH ? HS + h : h;
       }
     }
@@ -2228,7 +2354,6 @@ __device__ __forceinline__ void tree_l_doc(
     for (uint32_t k = 0; k < IT; k++) {
       const uint32_t j = wb_elem<IT>(k);
       uint32_t x = !(j < len && key[k]) ? TL_END
-                   : (MODE & 1) ? (hw[slot[k]] & ((1u << HB) - 1))
                    : DH ? hbuf[slot[k]] : hh[slot[k]];
       uint32_t p1 = 0, steps = 0;
       bool ls = true;
@@ -2324,7 +2449,7 @@ __device__ __forceinline__ void tree_l_doc(
           hbuf[slot[k]] = TL_END;
         } else if (kk) {
           hw[slot[k]] = 0;
-          if (!(MODE & 1)) hh[slot[k]] = TL_END;
+          hh[slot[k]] = TL_END;
         }
       }
       __syncthreads();
@@ -3560,9 +3685,11 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   // and input-index passes (1: 16, 0: 4 as in k_front)
   constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
   if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
-                     rank16, max_ts, ts_shift, status, big, nullptr, 0u, d,
+                     rank16, max_ts, ts_shift, status, big, nullptr, d,
                      reinterpret_cast<uint4 *>(lds_w), YF ? yarn : nullptr, site_sb & 0xFFu,
-                     site_sb >> 8))  // (YF = false: the yarn code compiles away)
+                     site_sb >> 8,  // (YF = false: the yarn code compiles away)
+                     // (a lower bound of the dynamic LDS: the largest document's front end)
+                     front_lds_bytes(32 * (bm_words - 1) + 1, sg)))
     return;
   __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
   const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -4308,20 +4435,16 @@ struct cw_ctx {
   } tab;
   bool tab_on_device = false;
   bool last_giant = false;
-  // launch geometry knobs (CW_TB, CW_WALK_THREADS, CW_WALK_SPAN, CW_WALK_LDS, CW_LOG2K)
-  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, walk_lds = 0, gd_build = 1, yarn_fused = 1, giant_log2cap = 5, glocal = 1, glocal_min = 1u << 20, min_log2k = 5,
-           max_digit = MAX_DIGIT, min_log2cap = 4, tree_cfg = 0;
+  // launch geometry (fixed at cw_ctx_create)
+  uint32_t tb = 1024, walk_threads = 1024, walk_span = 1024, giant_log2cap = 5, glocal = 1, glocal_min = 1u << 20, min_log2k = 5,
+           max_digit = MAX_DIGIT, min_log2cap = 4;
   // rank-directory front end (CW_FRONT, CW_FRONT_SLOT bytes per document)
   uint32_t front = 1, front_slot_groups = 4096, front_min_avg = 1024;
   uint32_t *pin_small = nullptr;  // pinned 16-byte readback
   uint32_t tree_prof = 0;          // CW_TREE_PROF: diagnostic phase stamps
-  uint32_t tree_pad = 0;           // CW_TREE_PAD: extra LDS bytes (occupancy experiments)
   uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
-  uint32_t tl_mode = 4;            // CW_TL_MODE: k_tree_l variant bits (A/B; 4 = direct list heads)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
-  uint32_t gpack = 1;              // CW_GPACK: ... gathering cause and kind as one packed word
-  uint32_t front_eff = 0;          // CW_FRONT_EFF: k_front writes effective parents (A/B)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
@@ -4332,10 +4455,6 @@ struct cw_ctx {
   uint32_t tour_log2k = 3;         // CW_TOUR_LOG2K: nodes per splitter block on that path
   uint32_t giant_log2k = 4;        // CW_GIANT_LOG2K: least splitter block of a giant document
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
-  uint32_t front_u = 1;            // CW_FRONT_U: k_weave_doc's front end keeps 16 ids a thread in
-                                   // flight in its directory and input-index passes (0: 4)
-  uint32_t map_flags = 1 | 4 | 8 | 16;  // k_map_pack variants: CW_MAP_DIR (bit 0), CW_MAP_LBW (bit 1),
-                                   // CW_MAP_RELAXED (bit 2), CW_MAP_DIRJOIN (bit 3), CW_MAP_EARLY (bit 4)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
   uint32_t x_iters = 0;            // synthetic-list weaves of the last exact path (exact.hip)
   uint32_t xfold = 0;              // CW_XFOLD: documents with an early node take the serial fold
@@ -4363,9 +4482,6 @@ struct cw_ctx {
     bool same = false;             // this call's coll_offsets equal off (set by cw_weave_maps)
     bool verify = false;           // ... taken on trust: compared while the kernel runs
   } mpack;
-  uint32_t map_pack = 0;           // CW_MAP_PACK: 0 = the smallest pack that holds the largest
-                                   // collection (512 / 128 threads, 1024 / 256, else 2048 / 512),
-                                   // 1 = 1024 / 256, 2 = 2048 / 1024, 3 = 2048 / 512, 4 = 512 / 128
 };
 
 namespace {
@@ -4945,7 +5061,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     constexpr uint32_t TL_NT = 1024;
     const uint32_t tl_dyn = tree_l_lds_bytes(t.nmax);
     // k_tree_l with 2,048-rank tiles, or 1,024 when the document needs the room
-    const uint32_t tree_l = !c->tree_l || c->tree_pad ? 0
+    const uint32_t tree_l = !c->tree_l ? 0
                             : c->tree_l == 2048 && tl_dyn + tree_l_static_bytes(TL_NT, 2048) <= c->lds_max ? 2048
                             : tl_dyn + tree_l_static_bytes(TL_NT, 1024) <= c->lds_max ? 1024 : 0;
     // k_tree_l: par 4 + kind bits in; fcS clear 4, nsc 4 out; sweep 2 reads
@@ -4964,49 +5080,15 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
       if (tree_l == 2048) tree_l_kernel(k_tree_l<TL_NT, 2048, P, M>);
       else tree_l_kernel(k_tree_l<TL_NT, 1024, P, M>);
     };
-    auto tree_l_prof = [&](auto prof) {
-      switch (c->tl_mode) {
-        case 0: tree_l_mode(prof, std::integral_constant<int, 0>()); break;
-        case 1: tree_l_mode(prof, std::integral_constant<int, 1>()); break;
-        case 2: tree_l_mode(prof, std::integral_constant<int, 2>()); break;
-        case 3: tree_l_mode(prof, std::integral_constant<int, 3>()); break;
-        default: tree_l_mode(prof, std::integral_constant<int, 4>()); break;
-      }
-    };
+    auto tree_l_prof = [&](auto prof) { tree_l_mode(prof, std::integral_constant<int, 4>()); };
     if (tree_l) {
       if (tprof) tree_l_prof(std::true_type());
       else tree_l_prof(std::false_type());
     }
-    else if (c->tree_cfg == 2)
-      hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256),
-                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
-    else if (c->tree_cfg == 3)
-      hipLaunchKernelGGL((k_tree<256, 512>), dim3((uint32_t)D), dim3(256),
-                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
-    else if (c->tree_cfg == 4)
-      hipLaunchKernelGGL((k_tree<512, 1024>), dim3((uint32_t)D), dim3(512),
-                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
-    else if (c->tree_cfg == 5)
-      hipLaunchKernelGGL((k_tree<1024, 2048>), dim3((uint32_t)D), dim3(1024),
-                         (size_t)bm_words * 8 + c->tree_pad, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
-    else if (c->tree_cfg == 1)
-      hipLaunchKernelGGL((k_tree<512, 2048>), dim3((uint32_t)D), dim3(512),
-                         (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
     else
-      hipLaunchKernelGGL((k_tree<1024, 4096>), dim3((uint32_t)D), dim3(1024),
-                         (size_t)bm_words * 8, c->stream, par, skind, doc_off, doc_log2k,
-                         kbits, bm_words, nsc, fcS, fcN, thr, (uint32_t *)link, out->status, tprof, kbm,
-                         dev_tab(c, "t_tile_first"));
+      hipLaunchKernelGGL((k_tree<256, 1024>), dim3((uint32_t)D), dim3(256), (size_t)bm_words * 8,
+                         c->stream, par, skind, doc_off, doc_log2k, kbits, bm_words, nsc, fcS, fcN, thr,
+                         (uint32_t *)link, out->status, tprof, kbm, dev_tab(c, "t_tile_first"));
   }
   if (check_launch(c, "tree")) return -1;
   if (c->tree_prof && !giant) {
@@ -5062,7 +5144,7 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
     {
       Launch L(c, "walk", (double)N * (4 + 4));
       hipLaunchKernelGGL(giant ? k_walk<true> : k_walk<false>, dim3(t.Bw), dim3(c->walk_threads),
-                         c->walk_lds, c->stream, (const void *)link, thr,
+                         0, c->stream, (const void *)link, thr,
                          dev_tab(c, "t_wblk_doc"), dev_tab(c, "t_wblk_w0"), doc_off, doc_log2k,
                          dev_tab(c, "t_doc_log2cap"), doc_W, dev_tab(c, "t_doc_Wcap"), walk_first,
                          (const uint64_t *)c->bufs["t_slot_first"].p, slots, wcnt, wnext, dyn_ctr,
@@ -5243,7 +5325,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       sval = svA;
       // the yarns inside the fused kernel (site fields of <= 4 bits): no ids
       // in rank order written, no sort by site afterwards
-      yarns_fused = want_yarns && c->yarn_fused && bt->site_bits <= 4;  // (<= 2 rounds of 8 sites)
+      yarns_fused = want_yarns && bt->site_bits <= 4;  // (<= 2 rounds of 8 sites)
       unsigned long long *tprof_f = nullptr;
       if (c->tree_prof) {
         tprof_f = scratch_t<unsigned long long>(c, "tprof3", (size_t)D * 8);
@@ -5258,9 +5340,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       // (the fused kernel is built for the tree variants 0 and 4 only: another
       // CW_TL_MODE runs the separate kernels, so the knob means the same thing
       // on both paths; CW_TREE_PROF runs variant 4)
-      fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 && !c->tree_pad &&
-                   !c->front_eff && (c->tl_mode == 0 || c->tl_mode == 4) &&
-                   (!c->tree_prof || c->tl_mode == 4) && tl_lds + 64 * 4 + 4 <= c->lds_max &&
+      fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 &&
+                   tl_lds + 64 * 4 + 4 <= c->lds_max &&
                    wd_lds + 1024 <= c->lds_max && to_lds <= TOUR_LDS_MAX;
       // (k_front writes the ids for the yarn sort; CW_TREE_PROF's kernels have no yarn code)
       yarns_fused = yarns_fused && fused_done && !c->tree_prof;
@@ -5297,19 +5378,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         if (tprof_f) {  // (the default front-end depth, so the clocks are the product's)
           if (wy) launch(k_weave_doc<1024, 2048, uint32_t, true, 4, 1>, sval);
           else launch(k_weave_doc<1024, 2048, uint16_t, true, 4, 1>, sval16);
-        } else if (c->tl_mode == 4) {
-          auto fv = [&](auto fvc) {
-            constexpr int F = decltype(fvc)::value;
-            if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, F>, sval);
-            else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 4, F, true>, sval16);
-            else launch(k_weave_doc<1024, 2048, uint16_t, false, 4, F>, sval16);
-          };
-          if (c->front_u) fv(std::integral_constant<int, 1>());
-          else fv(std::integral_constant<int, 0>());
         } else {
-          if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false>, sval);
-          else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 0, 0, true>, sval16);
-          else launch(k_weave_doc<1024, 2048, uint16_t, false>, sval16);
+          if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, 1>, sval);
+          else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 4, 1, true>, sval16);
+          else launch(k_weave_doc<1024, 2048, uint16_t, false, 4, 1>, sval16);
         }
       } else {
         Launch L(c, "front", (double)N * (8 + 8 + 1 + 2 + 4 + 1 + 2 + 4 + (skey ? 16 : 0)) + (double)N * 8);
@@ -5317,7 +5389,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            (size_t)fr_lds, c->stream, id_key,
                            cause_key, kind, doc_off, dev_tab(c, "t_tile_first"), FRONT_FUSED_SG, par,
                            skind, sval, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status, big,
-                           tprof_f, c->front_eff);
+                           tprof_f);
       }
       if (check_launch(c, fused_done ? "weave" : "front")) return -1;
       if (tprof_f && fused_done) {
@@ -5463,19 +5535,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (gdir) {
       {
         Launch L(c, "index", (double)N * 8 + (double)N / 15 * 64);
-        if (c->gd_build)
-          hipLaunchKernelGGL(k_gd_build, dim3((N + GDB_KEYS - 1) / GDB_KEYS), B256, 0, c->stream, skey, N,
-                             E, gdir, out->status);
-        else {
-          hipLaunchKernelGGL(k_gd_first, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E, gdir);
-          hipLaunchKernelGGL(k_gd_set_sorted, dim3((N + 255) / 256), B256, 0, c->stream, skey, N, E,
-                             gdir, out->status);
-        }
+        hipLaunchKernelGGL(k_gd_build, dim3((N + GDB_KEYS - 1) / GDB_KEYS), B256, 0, c->stream, skey, N,
+                           E, gdir, out->status);
       }
       if (check_launch(c, "index")) return -1;
       // cause and kind packed in one word per input node when the ids leave
       // 9 bits (the id sort's other key buffer is free by now)
-      uint64_t *ckk = c->gpack && key_bits <= 55 ? (skey == skA ? skB : skA) : nullptr;
+      uint64_t *ckk = key_bits <= 55 ? (skey == skA ? skB : skA) : nullptr;
       if (ckk) {
         Launch L(c, "gpack", (double)N * (8 + 1 + 8));
         hipLaunchKernelGGL(k_gpack, dim3((N + 255) / 256), B256, 0, c->stream, cause_key, kind, N, ckk);
@@ -6814,32 +6880,24 @@ int cw_ctx_create(int device, cw_ctx **out) {
     const char *v = getenv(name);
     return v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
   };
-  c->tb = knob("CW_TB", 1024);
-  c->walk_threads = knob("CW_WALK_THREADS", 512);
-  // one walker per thread (span == threads): a dynamic walker queue per block was slower
-  c->walk_span = std::max(c->walk_threads, knob("CW_WALK_SPAN", 512));
-  c->walk_lds = knob("CW_WALK_LDS", 0);
-  c->min_log2k = knob("CW_LOG2K", MIN_LOG2K);
-  c->min_log2cap = std::max(2u, knob("CW_LOG2CAP", 4));
-  c->tree_cfg = knob("CW_TREE", 2);
-
-  c->max_digit = std::max(1u, knob("CW_MAX_DIGIT", MAX_DIGIT));
+  // launch geometry (round 5: the A/B knobs CW_TB, CW_WALK_THREADS, CW_WALK_SPAN,
+  // CW_LOG2K, CW_LOG2CAP and CW_MAX_DIGIT are gone, their measured values stay):
+  // one walker per thread (span == threads: a dynamic walker queue per block was slower)
+  c->tb = 1024;
+  c->walk_threads = 512;
+  c->walk_span = 512;
+  c->min_log2k = MIN_LOG2K;
+  c->min_log2cap = 4;
+  c->max_digit = MAX_DIGIT;
   c->front = knob("CW_FRONT", 1);
   c->tree_prof = knob("CW_TREE_PROF", 0);
-  c->tree_pad = knob("CW_TREE_PAD", 0);
   c->tree_l = knob("CW_TREE_L", 2048);
-  c->tl_mode = knob("CW_TL_MODE", 4);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
-  c->gd_build = knob("CW_GD_BUILD", 1);
-  c->yarn_fused = knob("CW_YARN_FUSED", 1);
   c->glocal = knob("CW_GLOCAL", 1);
   c->glocal_min = knob("CW_GLOCAL_MIN", 1u << 20);
-  c->gpack = knob("CW_GPACK", 1);
-  c->front_eff = knob("CW_FRONT_EFF", 0);
   c->map_small = knob("CW_MAP_SMALL", 1);
   c->map_fused = knob("CW_MAP_FUSED", 1);
-  c->map_pack = knob("CW_MAP_PACK", 0);
   c->pack_sort = knob("CW_PACK_SORT", 1);
   c->giant_min = knob("CW_GIANT_MIN", 1u << 16);
   c->tour = knob("CW_TOUR", 1);
@@ -6850,10 +6908,6 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->giant_log2cap = std::max(2u, std::min(knob("CW_GIANT_LOG2CAP", 5), 12u));
   c->fused = knob("CW_FUSED", 1);
   c->xfold = knob("CW_XFOLD", 0);
-  c->front_u = knob("CW_FRONT_U", 1);
-  c->map_flags = (knob("CW_MAP_DIR", 1) ? 1u : 0u) | (knob("CW_MAP_LBW", 1) > 1 ? 2u : 0u) |
-                 (knob("CW_MAP_RELAXED", 1) ? 4u : 0u) | (knob("CW_MAP_DIRJOIN", 1) ? 8u : 0u) |
-                 (knob("CW_MAP_EARLY", 1) ? 16u : 0u);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

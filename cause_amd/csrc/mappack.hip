@@ -30,7 +30,7 @@
 // key weave, as k_seg_build does -- except under a self-caused id key, whose
 // key weave holds its causes (k_map_key) and is folded literally.
 
-constexpr uint32_t MPK = 2048;                 // largest pack (nodes); CW_MAP_PACK picks the geometry
+constexpr uint32_t MPK = 2048;                 // largest pack (nodes)
 constexpr uint16_t MP_ROOT = 0xFFFFu;          // cause-in-weave = the key weave's root
 constexpr uint16_t MP_CHAIN = 0xFFFEu;         // appended after the previous node
 constexpr uint16_t MP_ROOT_ID = 0xFFFDu;       // caused by the root id [0 "0" 0] (not a node)
@@ -82,14 +82,12 @@ __global__ __launch_bounds__(NT) void k_map_pack(
     uint64_t *__restrict__ seg_offsets, uint32_t *__restrict__ seg_coll,
     uint64_t *__restrict__ seg_key, int64_t *__restrict__ seg_active,
     uint32_t *__restrict__ seg_perm, uint32_t *__restrict__ status, uint32_t *ctl,
-    unsigned long long *__restrict__ tprof, uint32_t mflags, uint32_t nd_max, uint32_t epoch) {
-  // mflags (A/B knobs CW_MAP_DIR, CW_MAP_LBW, CW_MAP_RELAXED, CW_MAP_DIRJOIN):
-  // bit 0 = sort 1 through the id directory where it fits, bit 1 = four
-  // look-back windows a round trip, bit 2 = relaxed look-back atomics (the
-  // 64-bit word is the whole message: flag and count; no acquire / release
-  // fences around it), bit 3 = causes found through that directory too (no
-  // binary search), bit 4 = the element loads issued before the collection
-  // starts come in
+    unsigned long long *__restrict__ tprof, uint32_t nd_max, uint32_t epoch) {
+  // (round 3-4 A/Bs, the winners built in: sort 1 through the id directory
+  // where it fits, causes found through that directory too, the element loads
+  // issued before the collection starts come in, relaxed look-back atomics --
+  // the 64-bit word is the whole message, flag and count, so no acquire /
+  // release fences around it)
   constexpr uint32_t IT = PK / NT;
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
@@ -132,13 +130,12 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   const uint32_t d0 = pack_doc0[pk], nd = pack_doc0[pk + 1] - d0;
   const uint64_t s0 = pack_s0[pk];
   const uint32_t len = (uint32_t)(pack_s0[pk + 1] - s0);
-  const bool early = mflags & 16;
   uint64_t lc[IT], lid[IT];
   uint8_t lcis[IT], lkd[IT];
 #pragma unroll
   for (uint32_t u = 0; u < IT; u++) {
     const uint32_t j = wb_elem<IT>(u);
-    const bool ok = early && j < len;
+    const bool ok = j < len;
     lc[u] = ok ? cause[s0 + j] : 0ull;
     lid[u] = ok ? id_key[s0 + j] : 0ull;
     lcis[u] = ok ? cause_is_id[s0 + j] : 0;
@@ -171,13 +168,13 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         const uint32_t m = (lo + hi) >> 1;
         if (dstart[m] <= j) lo = m; else hi = m;
       }
-      const uint64_t c = early ? lc[u] : cause[s0 + j];
-      const uint8_t cis = early ? lcis[u] : cause_is_id[s0 + j];
+      const uint64_t c = lc[u];
+      const uint8_t cis = lcis[u];
       const bool cid = cis == 1;
       B[j] = c;
       // 0x80: the cause is an id; 0x40: the cause is nil (cause_is_id = 2)
-      K8[j] = (uint8_t)((cid ? 0x80u : cis == 2 ? 0x40u : 0u) | ((early ? lkd[u] : kind[s0 + j]) & KIND_CLASS));
-      ck[u] = early ? lid[u] : id_key[s0 + j];
+      K8[j] = (uint8_t)((cid ? 0x80u : cis == 2 ? 0x40u : 0u) | (lkd[u] & KIND_CLASS));
+      ck[u] = lid[u];
       oid |= ck[u];
       oca |= cid ? c : 0ull;
       val[u] = j;
@@ -215,7 +212,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   bool sorted = false;
   uint32_t *const dir = reinterpret_cast<uint32_t *>(P16);
   uint16_t *const wpre = VS;
-  if ((mflags & 1) && fits && ((uint64_t)nd << lw) <= DIRW) {
+  if (fits && ((uint64_t)nd << lw) <= DIRW) {
     const uint32_t nwd = nd << lw;
     for (uint32_t w = tid; w < nwd; w += NT) dir[w] = 0;
     __syncthreads();
@@ -279,7 +276,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // 2. key and cause-in-weave of every node, in id order (map.cljc:31-37).
   // With the directory of sort 1 still in P16 | Q | LQ (DIRJOIN), an id cause
   // is a bit test and a popcount; P16 is written after a barrier then.
-  const bool djoin = sorted && (mflags & 8);
+  const bool djoin = sorted;
   uint16_t pv[IT];
   unsigned long long kor = 0;
   uint32_t cor = 0;
@@ -428,8 +425,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   const unsigned long long ep = (unsigned long long)epoch << LB_EPOCH;
   if (tid == 0) {
     const unsigned long long w = (pk == 0 ? LB_INC : LB_AGG) | ep | nseg;
-    if (mflags & 4) __hip_atomic_store(lb + pk, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_store(lb + pk, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(lb + pk, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
   // 5. each key weave's list weave: member 0 the root, members 1..m in id order
@@ -683,8 +679,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
   // the nearest inclusive prefix is typically a whole residency (~500 packs)
   // back: one window per round trip cost ~8 L2 round trips (20k clocks).
   if (tid < 64) {
-    constexpr uint32_t LBW = 4;
-    const uint32_t lbw = (mflags & 2) ? LBW : 1;
+    constexpr uint32_t LBW = 1, lbw = 1;  // (four windows a round trip lost in round 3)
     const uint32_t lane = tid;
     uint32_t base = 0;
     if (pk > 0) {
@@ -694,8 +689,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
         for (uint32_t k = 0; k < LBW; k++) {
           const int64_t q = q0 - 64 * (int64_t)k - lane;  // lane 0 of window 0 = the nearest
           v[k] = !(q >= 0 && k < lbw) ? (k < lbw ? LB_INC | ep : 0ull)
-                 : (mflags & 4) ? __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : __hip_atomic_load(lb + q, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                 : __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (((v[k] >> LB_EPOCH) & 0xFFFFull) != epoch) v[k] = 0;  // an earlier call's word
         }
         bool done = false, retry = false;  // (wave-uniform: ballots)
@@ -721,10 +715,7 @@ __global__ __launch_bounds__(NT) void k_map_pack(
       }
       if (lane == 0)
       {
-        if (mflags & 4)
-          __hip_atomic_store(lb + pk, LB_INC | ep | (base + nseg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          __hip_atomic_store(lb + pk, LB_INC | ep | (base + nseg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lb + pk, LB_INC | ep | (base + nseg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
     if (lane == 0) {
@@ -779,13 +770,12 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
   const uint32_t N = (uint32_t)off[D];
   // pack table, cached while the collection layout repeats
   auto &pc = c->mpack;
-  // pack size (CW_MAP_PACK): by default the smallest of 512 / 1024 / 2048
+  // pack size: the smallest of 512 / 1024 / 2048
   // nodes that holds the largest collection -- smaller packs are more
   // workgroups a CU with cheaper barriers (config 4: 2048 nodes 3.77 ms,
   // 1024 3.26, 512 3.15; 256 nodes / one wave: 3.95)
   const uint64_t mc = pc.maxcoll;
-  const uint32_t PKN = c->map_pack == 1 ? 1024u : c->map_pack == 4 ? 512u
-                       : c->map_pack != 0 ? MPK : mc <= 512 ? 512u : mc <= 1024 ? 1024u : MPK;
+  const uint32_t PKN = mc <= 512 ? 512u : mc <= 1024 ? 1024u : MPK;
   if (!(pc.pk == PKN && pc.same)) {
     pc.off.assign(off, off + D + 1);
     pc.pk = PKN;
@@ -864,10 +854,9 @@ int weave_maps_packed(cw_ctx *c, const cw_map_batch *bt, cw_map_result *res, boo
                      (const uint64_t *)c->bufs["mp_off"].p, (const uint32_t *)c->bufs["mp_doc0"].p, \
                      (const uint64_t *)c->bufs["mp_s0"].p,                                             \
                      P, bt->token_bits, lb, cap, (uint64_t)N, so, sc, sk, sa,                          \
-                     sp, st, ctl, tprof, c->map_flags, pc.dmax, pc.epoch)
+                     sp, st, ctl, tprof, pc.dmax, pc.epoch)
     if (pc.pk == 512) CW_MAP_PACK_LAUNCH(512, 128);
     else if (pc.pk == 1024) CW_MAP_PACK_LAUNCH(1024, 256);
-    else if (c->map_pack == 2) CW_MAP_PACK_LAUNCH(2048, 1024);
     else CW_MAP_PACK_LAUNCH(2048, 512);
 #undef CW_MAP_PACK_LAUNCH
   }

@@ -1,6 +1,6 @@
 """A/B launch-geometry variants of the weave in ONE process on one workload.
 
-    python scripts/sweep.py '[{"CW_TB":"256"}, {"CW_TB":"1024"}]' [--docs 10000] [--rounds 3]
+    python scripts/sweep.py '[{}, {"CW_FUSED":"0"}]' [--docs 10000] [--rounds 3]
 
 Each variant gets its own context (knobs are read at cw_ctx_create); rounds
 interleave the variants; per-kernel ms come from the library's HIP events.

@@ -1,7 +1,7 @@
 """A/B knob variants of cw_weave_maps in ONE process on the config-4 workload
 (device memory, 10^6 collections x 100 nodes by default).
 
-    python scripts/sweep_maps.py '[{}, {"CW_MAP_PACK": "2"}]' [--colls 1000000] [--rounds 3]
+    python scripts/sweep_maps.py '[{}, {"CW_MAP_SMALL": "0"}]' [--colls 1000000] [--rounds 3]
 
 Each variant gets its own context (knobs are read at cw_ctx_create); rounds
 interleave the variants; per-kernel ms come from the library's HIP events.

@@ -295,17 +295,12 @@ def test_duplicate_ids_beside_clean_documents(weaver):
 # walk / slot geometry only matters on the HBM walk path (CW_TOUR=0); the
 # fused LDS tour takes its own splitter density (CW_TOUR_LOG2K)
 _W = {"CW_TOUR": "0"}
-KNOBS = [{}, dict(_W), dict(_W, CW_LOG2CAP="5"), dict(_W, CW_LOG2K="4", CW_LOG2CAP="5"),
-         {"CW_MAX_DIGIT": "8"}, dict(_W, CW_WALK_THREADS="256", CW_WALK_SPAN="512"),
-         dict(_W, CW_WALK_THREADS="1024", CW_WALK_SPAN="2048"),
+KNOBS = [{}, dict(_W),
          {"CW_TOUR_LOG2K": "3"}, {"CW_TOUR_LOG2K": "4"}, {"CW_TOUR_LOG2K": "7"},
          {"CW_FRONT": "0"}, {"CW_FRONT_SLOT": "4096"},
-         # the tree: k_tree (tables in HBM) and its geometries, k_tree_l's A/B modes,
-         # raw parents from the front end (the tree climbs)
-         {"CW_TREE_L": "0"}, {"CW_TREE_L": "0", "CW_TREE": "0"}, {"CW_TREE_L": "0", "CW_TREE": "1"},
-         {"CW_TREE_L": "1024"},
-         {"CW_TL_MODE": "0"}, {"CW_TL_MODE": "1"}, {"CW_TL_MODE": "2"}, {"CW_TL_MODE": "3"},
-         {"CW_TL_MODE": "0", "CW_FUSED": "0"}, {"CW_FRONT_EFF": "1"}]
+         # the tree: k_tree (tables in HBM, the fallback for documents too large
+         # for k_tree_l's LDS), k_tree_l with 1,024-rank tiles, the separate kernels
+         {"CW_TREE_L": "0"}, {"CW_TREE_L": "1024"}, {"CW_FUSED": "0"}]
 
 
 @pytest.mark.parametrize("n", [59_204, 60_000, 65_534, 65_535])
@@ -370,13 +365,9 @@ def test_full_bench_batch_vs_oracle(knobs, monkeypatch):
 # ------------------------------------------------- one giant document (config 5)
 # Giant-path front ends: the directory over the whole key range
 # (k_gd_place, small key ranges: the default here), the sorted-id directory
-# join (CW_GDIR=0: k_gd_build / k_gpack / k_gjoin, config 5's default), the
-# same with the two-pass directory build (CW_GD_BUILD=0: k_gd_first /
-# k_gd_set_sorted), without the packed cause + kind word (CW_GPACK=0), and
+# join (CW_GDIR=0: k_gd_build / k_gpack / k_gjoin, config 5's default) and
 # the bucket index + searching join (CW_GJOIN=0).
 GIANT_FRONTS = {"gdplace": {}, "gjoin": {"CW_GDIR": "0"},
-                "gjoin-2pass-dir": {"CW_GDIR": "0", "CW_GD_BUILD": "0"},
-                "gjoin-unpacked": {"CW_GDIR": "0", "CW_GPACK": "0"},
                 "bucket": {"CW_GDIR": "0", "CW_GJOIN": "0"},
                 # the tile-local sibling links (k_glocal) at every size
                 "glocal": {"CW_GDIR": "0", "CW_GLOCAL_MIN": "0"}}
@@ -485,13 +476,12 @@ def test_giant_path_splitter_blocks(log2k, monkeypatch):
 
 
 def test_giant_path_many_continuation_sublists(monkeypatch):
-    """4-entry walk slots (CW_GIANT_LOG2CAP / CW_LOG2CAP = 2): every walk goes
+    """4-entry walk slots (CW_GIANT_LOG2CAP = 2): every walk goes
     on through several continuation sublists, so the first ranking level's
     walkers pass more sublists than their 32-entry slots hold and the rest
     take the overflow path (pos + the overflow list)."""
     monkeypatch.setenv("CW_GIANT_MIN", "0")
     monkeypatch.setenv("CW_GIANT_LOG2CAP", "2")
-    monkeypatch.setenv("CW_LOG2CAP", "2")
     with abi.Weaver(0) as w:
         spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 1000)
         off, idk, ck, kd = gen.generate(spec, 0, 1)

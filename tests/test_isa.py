@@ -55,6 +55,11 @@ def test_no_kernel_uses_scratch(tmp_path):
     # (an SGPR spill goes to a VGPR lane -- v_writelane, no memory -- as long as
     # there is no private segment; k_map_pack's look-back epoch and layout
     # arguments spill 10 of them)
+    # the fused weave with in-kernel yarns (template flag YF = true, the last
+    # one) holds the staged yarns' wave-uniform bounds on top of the tree's and
+    # the tour's 30-odd pointer arguments: a few dozen SGPRs go to lanes there
+    yarn = lambda k: re.search(r"k_weave_docILi\d+ELi\d+E.Lb0ELi\d+ELi\d+ELb1E", k) is not None
+    lim = lambda k: 64 if diag(k) else 48 if yarn(k) else 16
     bad = {k: v for k, v in kernels.items() if v.get("private_segment_fixed_size", 0)
-           or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0) > (64 if diag(k) else 16)}
+           or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0) > lim(k)}
     assert not bad, f"kernels using scratch: {bad}"
