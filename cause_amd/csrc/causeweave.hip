@@ -1295,210 +1295,6 @@ __host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) 
   return sg * 16 + 4 * ((nmax + 1) / 2) + 8 * ((nmax + 31) / 32);
 }
 
-// Index of the o-th set bit (0-based) of w (o < popc(w)).
-__device__ __forceinline__ uint32_t select_bit(uint32_t w, uint32_t o) {
-  uint32_t pos = 0, c;
-  c = __popc(w & 0xFFFFu);
-  if (o >= c) { o -= c; w >>= 16; pos += 16; }
-  c = __popc(w & 0xFFu);
-  if (o >= c) { o -= c; w >>= 8; pos += 8; }
-  c = __popc(w & 0xFu);
-  if (o >= c) { o -= c; w >>= 4; pos += 4; }
-  c = __popc(w & 0x3u);
-  if (o >= c) { o -= c; w >>= 2; pos += 2; }
-  return pos + ((o >= (w & 1u)) ? 1u : 0u);
-}
-
-// Ordering LDS accesses of one wave across its lanes (a wave's LDS operations
-// run in order: only the compiler has to keep them so).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// The yarns of one document (spin 1-arity, shared.cljc:121-132: the id order
-// partitioned by site, id-ascending inside a site) written as whole runs
-// (round 5; the per-thread version scattered each node's 4 bytes over up to
-// 16 site streams: 3.9 ms of a config-2 step).  The directory (sdir: groups of
-// 96 id bits, x = the rank of the group's first id) and p16 (input index by
-// rank) are the front end's.  The site of an id repeats within a directory
-// word (site_shift + site_bits <= 5): a word's ids of site s are the bits of
-// a fixed mask.
-//   1. per wave (its threads' groups, a contiguous rank range): site counts
-//      by masked popcounts -> per-wave, per-site output cursors;
-//   2. per wave, rounds of 64 x K consecutive ranks: each lane takes K ranks
-//      (its start found by a binary search over the groups' ranks and a bit
-//      select), the wave ranks its elements by site (packed 16-bit counters,
-//      wave scans), stages them in LDS site by site, and writes each site's
-//      run of the round to its cursor: consecutive lanes, consecutive words.
-// stage: the free LDS after p16 (>= NT * K u16 entries; its first 1 KiB also
-// holds the per-wave counts of step 1).
-template <int NT>
-__device__ __forceinline__ void yarn_staged(const uint4 *sdir, uint32_t G, uint32_t n,
-                                         const uint16_t *p16, uint16_t *stage, uint32_t K,
-                                         uint32_t *__restrict__ yD, uint32_t site_shift,
-                                         uint32_t site_bits, uint32_t *wtot) {
-  constexpr uint32_t NW = NT / 64;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t S = 1u << site_bits, smask = S - 1;
-  const uint32_t per = (G + NT - 1) / NT;
-  const uint32_t gw0 = min(G, wv * 64 * per), gw1 = min(G, (wv + 1) * 64 * per);
-  // (the ids the directory holds: fewer than n when an id repeats -- a DUP
-  // document, whose outputs are unspecified but whose walk must stay inside)
-  uint32_t nid = 0;
-  if (G) {
-    const uint4 ql = sdir[G - 1];
-    nid = min(n, ql.x + __popc(ql.y) + __popc(ql.z) + __popc(ql.w));
-  }
-  const uint32_t rw0 = gw0 < G ? min(nid, sdir[gw0].x) : nid;
-  const uint32_t rw1 = gw1 < G ? min(nid, sdir[gw1].x) : nid;
-  // the mask of site s inside a 32-bit word
-  const uint32_t bw = 1u << site_shift, P = 1u << (site_shift + site_bits);
-  const uint32_t blk = bw >= 32 ? 0xFFFFFFFFu : (1u << bw) - 1u;
-  auto smask_of = [&](uint32_t s) {
-    uint32_t m = 0;
-    for (uint32_t o = 0; o < 32; o += P) m |= (blk << (s * bw)) << o;
-    return m;
-  };
-  // 1. per-wave site counts: lane s counts site s over the wave's groups
-  // (the mask lives in the lane: wave-uniform masks would spill SGPRs)
-  uint32_t *tab = reinterpret_cast<uint32_t *>(stage);  // [NW][16] counts
-  {
-    const uint32_t msk = lane < S ? smask_of(lane) : 0u;
-    uint32_t mine = 0;
-    for (uint32_t g = gw0; g < gw1; g++) {
-      const uint4 q = sdir[g];
-      mine += __popc(q.y & msk) + __popc(q.z & msk) + __popc(q.w & msk);
-    }
-    if (lane < 16) tab[wv * 16 + lane] = mine;
-  }
-  __syncthreads();
-  // lane s: this wave's cursor for site s = (sites before s, whole document)
-  // + (site s in earlier waves)
-  uint32_t cur = 0;
-  {
-    uint32_t tot = 0, before = 0;
-    if (lane < S)
-      for (uint32_t w = 0; w < NW; w++) {
-        const uint32_t v = tab[w * 16 + lane];
-        tot += v;
-        before += w < wv ? v : 0u;
-      }
-    uint32_t inc = tot;  // exclusive scan of the site totals over lanes 0..15
-    for (uint32_t o = 1; o < 16; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += y;
-    }
-    cur = inc - tot + before;
-  }
-  __syncthreads();  // (the count table is staging from here on)
-  uint16_t *const stw = stage + wv * 64 * K;
-  for (uint32_t R = rw0; R < rw1; R += 64 * K) {
-    const uint32_t t = R + K * lane;
-    const uint32_t cnt = t < rw1 ? min(K, rw1 - t) : 0u;
-    uint32_t sites[8], vals[8];
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) sites[j] = vals[j] = 0;
-    if (cnt) {
-      // the group holding rank t: the last with x <= t
-      uint32_t lo = gw0, hi = gw1;  // x(lo) <= t < x(hi)
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (sdir[mid].x <= t) lo = mid; else hi = mid;
-      }
-      uint32_t g = lo, k;
-      uint4 q = sdir[g];
-      uint32_t o = t - q.x, m;
-      const uint32_t p0 = __popc(q.y), p1 = __popc(q.z);
-      if (o < p0) { k = 0; m = q.y; }
-      else if (o < p0 + p1) { k = 1; m = q.z; o -= p0; }
-      else { k = 2; m = q.w; o -= p0 + p1; }
-      m &= 0xFFFFFFFFu << select_bit(m, o);
-#pragma unroll
-      for (uint32_t j = 0; j < 8; j++) {
-        if (j >= cnt) break;
-        while (m == 0 && g < G) {
-          if (++k == 3) {
-            if (++g == G) break;
-            q = sdir[g];
-            k = 0;
-          }
-          m = k == 0 ? q.y : k == 1 ? q.z : q.w;
-        }
-        const uint32_t b = (uint32_t)__ffs(m) - 1;
-        m &= m - 1;
-        sites[j] = (b >> site_shift) & smask;
-        vals[j] = p16[t + j];
-      }
-    }
-    // the wave's elements of this round ranked by site
-    uint32_t own[8], ex[8];
-#pragma unroll
-    for (uint32_t w = 0; w < 8; w++) own[w] = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) {
-      if (j >= cnt) break;
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++)
-        if (w == (sites[j] >> 1)) own[w] += 1u << ((sites[j] & 1) * 16);
-    }
-    // lane s (< 16): the round's count of site s and its exclusive prefix over
-    // the sites (kept lane by lane: wave-uniform tables would spill SGPRs)
-    uint32_t tl = 0;
-#pragma unroll
-    for (uint32_t w = 0; w < 8; w++) {
-      uint32_t inc = own[w];
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
-      }
-      ex[w] = inc - own[w];
-      const uint32_t tot = (uint32_t)__shfl((int)inc, 63, 64);  // (a VGPR broadcast, no SGPR)
-      if (w == (lane >> 1)) tl = (tot >> ((lane & 1) * 16)) & 0xFFFFu;
-    }
-    if (lane >= 16) tl = 0;
-    uint32_t offl = tl;  // exclusive scan over lanes 0..15
-    for (uint32_t o = 1; o < 16; o <<= 1) {
-      const uint32_t y = __shfl_up(offl, o, 64);
-      if (lane >= o) offl += y;
-    }
-    const uint32_t total = (uint32_t)__shfl((int)offl, 15, 64);
-    offl -= tl;
-    // stage site by site
-#pragma unroll
-    for (uint32_t j = 0; j < 8; j++) {
-      const bool on = j < cnt;
-      const uint32_t s = sites[j], sh = (s & 1) * 16;
-      uint32_t e = 0;
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++)
-        if (on && w == (s >> 1)) {
-          e = (ex[w] >> sh) & 0xFFFFu;
-          ex[w] += 1u << sh;
-        }
-      const uint32_t base_s = (uint32_t)__shfl((int)offl, (int)s, 64);  // (every lane takes part)
-      if (on) stw[base_s + e] = (uint16_t)vals[j];
-    }
-    wave_lds_sync();
-    // each site's run of this round to its cursor
-    for (uint32_t i0 = 0; i0 < total; i0 += 64) {  // (wave-uniform: the shuffles see every lane)
-      const uint32_t i = i0 + lane;
-      uint32_t s = 0;  // the last site whose run starts at or before i
-#pragma unroll
-      for (uint32_t step = 8; step > 0; step >>= 1) {
-        const uint32_t o = (uint32_t)__shfl((int)offl, (int)(s + step), 64);
-        if (s + step < 16 && o <= i) s += step;
-      }
-      const uint32_t o0 = (uint32_t)__shfl((int)offl, (int)s, 64);
-      const uint32_t c = (uint32_t)__shfl((int)cur, (int)s, 64) + i - o0;
-      if (i < total && c < n) yD[c] = stw[i];
-    }
-    cur += tl;  // lane s's cursor moves past site s's run
-    wave_lds_sync();
-  }
-}
-
 // one document d (the whole workgroup); lds: the dynamic LDS.  Returns false
 // when the document's ids leave the directory (big[0] counts it).  PT / VT:
 // the width of par / sval (u16 inside k_weave_doc: n < 2^16); skind may be
@@ -1514,9 +1310,7 @@ __device__ __forceinline__ bool front_doc(
     uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t d, uint4 *sdir,
-    uint32_t *__restrict__ yarn = nullptr, uint32_t site_shift = 0, uint32_t site_bits = 0,
-    uint32_t lds_total = 0) {
+    unsigned long long *__restrict__ tprof, uint32_t d, uint4 *sdir) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (tprof) {
@@ -1708,83 +1502,6 @@ __device__ __forceinline__ bool front_doc(
       for (uint32_t k = 0; k < 3; k++)
         for (uint32_t m = wv[k]; m != 0 && r < n; m &= m - 1)
           skey[base + r++] = (uint64_t)g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
-    }
-  }
-  // the yarns through per-wave LDS staging (round 5): the site pattern of an id
-  // repeats within a 32-bit directory word (site_shift + site_bits <= 5), and
-  // the free LDS after p16 (at least the class bitmaps, dead by now) holds a
-  // staging run of >= 2 ranks per lane
-  const uint32_t y_used = sg * 16 + 4 * ((n + 1) / 2);
-  const uint32_t y_lanes_k = lds_total > y_used ? (lds_total - y_used) / (NT * 2) : 0u;
-  if (yarn && site_shift + site_bits <= 5 && y_lanes_k >= 2) {
-    yarn_staged<NT>(sdir, G, n, p16, reinterpret_cast<uint16_t *>(reinterpret_cast<uint8_t *>(sdir) + y_used),
-                    min(y_lanes_k, 8u), yarn + base, site_shift, site_bits, wtot);
-  } else if (yarn) {
-    // the yarns (spin: the id order partitioned by site, id-ascending inside a
-    // site) from the same directory walk: a thread's groups are a contiguous
-    // range of ranks, so per-site counts, block prefix sums over the threads
-    // and the site totals place every rank's input index (p16, by rank) -- no
-    // id sort by site afterwards.  Eight sites a round (8 x 16-bit counters
-    // in 4 words: more spill the fused kernel's registers), site_bits <= 4.
-    constexpr uint32_t YB = 8, YW = YB / 2;
-    const uint32_t per = (G + NT - 1) / NT, g0 = min(G, tid * per), g1 = min(G, g0 + per);
-    const uint32_t smask = (1u << site_bits) - 1;
-    auto site_of = [&](uint32_t g, uint32_t k, uint32_t m) {
-      const uint32_t id = g * FR_GROUP_BITS + 32 * k + (uint32_t)(__ffs(m) - 1);
-      return (id >> site_shift) & smask;
-    };
-    uint32_t *const yD = yarn + base;
-    uint32_t off = 0;  // the sites of earlier rounds
-    bool hi = false, more = false;  // a site past the first round's (config 2: 8 of 16 used)
-#pragma unroll 1
-    for (uint32_t s0 = 0; s0 <= smask; s0 += YB) {
-      if (s0 > 0 && !more) break;
-      uint32_t cw[YW];
-#pragma unroll
-      for (uint32_t w = 0; w < YW; w++) cw[w] = 0;
-      for (uint32_t g = g0; g < g1; g++) {
-        const uint4 q = sdir[g];
-#pragma unroll 1
-        for (uint32_t k = 0; k < 3; k++)
-          for (uint32_t m = k == 0 ? q.y : k == 1 ? q.z : q.w; m != 0; m &= m - 1) {
-            const uint32_t st = site_of(g, k, m) - s0;  // (wraps when below this round)
-            hi |= st >= YB && st < 0x80000000u;
-#pragma unroll
-            for (uint32_t w = 0; w < YW; w++)  // (no run-time index: the counters stay in VGPRs)
-              if (w == (st >> 1)) cw[w] += 1u << ((st & 1) * 16);
-          }
-      }
-      if (s0 == 0) more = __syncthreads_or(hi);
-      // site s0 + 2 w + h: its prefix over the threads and its total are half
-      // h of word w's scan; the sites in order give the bases, packed in cw
-#pragma unroll
-      for (uint32_t w = 0; w < YW; w++) {
-        uint32_t tot;
-        const uint32_t pre = block_exscan<NT>(cw[w], wtot, &tot);
-        const uint32_t b0 = off + (pre & 0xFFFFu);
-        off += tot & 0xFFFFu;
-        const uint32_t b1 = off + (pre >> 16);
-        off += tot >> 16;
-        cw[w] = (b0 & 0xFFFFu) | (b1 << 16);
-      }
-      for (uint32_t g = g0; g < g1; g++) {
-        const uint4 q = sdir[g];
-        uint32_t r = q.x;
-#pragma unroll 1
-        for (uint32_t k = 0; k < 3; k++)
-          for (uint32_t m = k == 0 ? q.y : k == 1 ? q.z : q.w; m != 0 && r < n; m &= m - 1, r++) {
-            const uint32_t st = site_of(g, k, m) - s0, sh = (st & 1) * 16;
-            if (st >= YB) continue;
-            uint32_t p = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < YW; w++)
-              if (w == (st >> 1)) {
-                p = (cw[w] >> sh) & 0xFFFFu;
-                cw[w] += 1u << sh;
-              }
-            if (p < n) yD[p] = p16[r];
-          }
-      }
     }
   }
   stamp(4);
@@ -3663,7 +3380,7 @@ __global__ __launch_bounds__(NT) void k_tour(const uint32_t *__restrict__ link,
 // there is one tail instead of three.  A document whose ids leave the front
 // end's directory counts itself in big[0] and stops: the host then weaves the
 // batch with the separate kernels.
-template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0, int FV = 0, bool YF = false>
+template <int NT, int TILE_T, typename VT, bool PROF, int TLM = 0, int FV = 0>
 __global__ __launch_bounds__(NT) void k_weave_doc(
     const uint64_t *__restrict__ id_key, const uint64_t *__restrict__ cause_key,
     const uint8_t *__restrict__ kind, const uint32_t *__restrict__ doc_off,
@@ -3674,10 +3391,8 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
     uint32_t kbits, uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp, uint32_t *__restrict__ perm,
     uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc,
-    unsigned long long *__restrict__ tprof, uint32_t *__restrict__ yarn, uint32_t site_sb) {
+    unsigned long long *__restrict__ tprof) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
-  // (site_sb: the yarns' site field, shift | bits << 8 -- one argument: the
-  // kernel is at its SGPR limit)
   const uint32_t d = blockIdx.x;
   // (tprof, CW_TREE_PROF: the three phases' clocks per document)
   const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -3686,10 +3401,7 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
   if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, d,
-                     reinterpret_cast<uint4 *>(lds_w), YF ? yarn : nullptr, site_sb & 0xFFu,
-                     site_sb >> 8,  // (YF = false: the yarn code compiles away)
-                     // (a lower bound of the dynamic LDS: the largest document's front end)
-                     front_lds_bytes(32 * (bm_words - 1) + 1, sg)))
+                     reinterpret_cast<uint4 *>(lds_w)))
     return;
   __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
   const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -3705,6 +3417,142 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
     tprof[(size_t)d * 4 + 1] = t2 - t1;
     tprof[(size_t)d * 4 + 2] = t3 - t2;
   }
+}
+
+// The yarns of the documents k_weave_doc took (spin 1-arity, shared.cljc:121-132:
+// the id order partitioned by site, id-ascending inside a site), one workgroup
+// per document after it, from what it leaves in HBM: every input's rank
+// (rank16) and every rank's input index (sval16).  In LDS: the site of every
+// rank (a byte), then the yarn as u16 input indices, written out as whole lines.
+// 16 B a node: id 8 + rank 2 + sval 2 in, yarn_perm 4 out.  (Round 4 placed the
+// yarns inside the fused kernel's front end, from its directory: +3.9 ms on a
+// config-2 step; an LDS-staged version there, +3.8 ms; this kernel: 2.55 ms,
+// of which ~1.8 ms is its LDS work -- site scatter 0.3, counts 0.6, placement
+// 0.8 -- and ~0.8 ms its HBM reads, profiles/r05_yarn_ab.txt.)
+__host__ __device__ inline uint32_t yarn_lds_bytes(uint32_t nmax) {
+  return ((nmax + 3) & ~3u) + 2 * ((nmax + 1) & ~1u);  // sites (a byte a rank), the yarn (u16)
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_yarn_doc(const uint64_t *__restrict__ id_key,
+                                                 const uint16_t *__restrict__ rank16,
+                                                 const uint16_t *__restrict__ sval16,
+                                                 const uint32_t *__restrict__ doc_off,
+                                                 uint32_t site_shift, uint32_t site_bits,
+                                                 uint32_t *__restrict__ yarn) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_y[];
+  __shared__ uint32_t wrow[NT / 64][8];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t d = blockIdx.x;
+  const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
+  uint8_t *const sr = reinterpret_cast<uint8_t *>(lds_y);
+  uint16_t *const out = reinterpret_cast<uint16_t *>(sr + ((n + 3) & ~3u));
+  const uint32_t smask = (1u << site_bits) - 1;
+  // each thread's ranks for steps 2-3 (a multiple of 8: the sites are read
+  // four to a word)
+  const uint32_t per = ((n + NT - 1) / NT + 7) & ~7u, r0 = min(n, tid * per), r1 = min(n, r0 + per);
+  for (uint32_t w = tid; w < (n + 3) / 4; w += NT) lds_y[w] = 0xFFFFFFFFu;  // (no site: a DUP doc)
+  __syncthreads();
+  // 1. the site of every rank
+  constexpr uint32_t U = 8;
+  for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
+    uint64_t x[U];
+    uint32_t r[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++) {
+      const uint32_t i = i0 + u * NT;
+      x[u] = i < n ? lane_at(id_key + base, i) : 0ull;
+      r[u] = i < n ? lane_at(rank16 + base, i) : 0xFFFFu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < U; u++)
+      if (r[u] < n) sr[r[u]] = (uint8_t)((x[u] >> site_shift) & smask);
+  }
+  __syncthreads();
+  // 2. per-site counts over each thread's contiguous ranks (two 16-bit
+  // counters a register, no run-time index; a range starts at a multiple of 8
+  // ranks: the sites are read four to a word), block scans -> each thread's
+  // output position per site
+  const uint32_t *const sr32 = lds_y;
+  uint32_t cw[8];
+#pragma unroll
+  for (uint32_t w = 0; w < 8; w++) cw[w] = 0;
+  for (uint32_t r = r0; r < r1; r += 4) {
+    const uint32_t w4 = sr32[r >> 2];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+      const uint32_t st = r + k < r1 ? (w4 >> (8 * k)) & 0xFFu : 0xFFu;
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++)
+        if (w == (st >> 1)) cw[w] += 1u << ((st & 1) * 16);
+    }
+  }
+  // the eight registers scanned together: wave scans, the waves' totals
+  // through LDS (one row of eight words a wave)
+  {
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    uint32_t inc[8];
+#pragma unroll
+    for (uint32_t w = 0; w < 8; w++) {
+      inc[w] = cw[w];
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc[w], o, 64);
+        if (lane >= o) inc[w] += y;
+      }
+    }
+    if (lane == 63)
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++) wrow[wv][w] = inc[w];
+    __syncthreads();
+    uint32_t before[8], tot[8];
+#pragma unroll
+    for (uint32_t w = 0; w < 8; w++) before[w] = tot[w] = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < NT / 64; i++) {
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++) {
+        const uint32_t t = wrow[i][w];
+        before[w] += i < wv ? t : 0u;
+        tot[w] += t;
+      }
+    }
+    uint32_t off = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 8; w++) {
+      const uint32_t pre = before[w] + inc[w] - cw[w];
+      const uint32_t b0 = off + (pre & 0xFFFFu);
+      off += tot[w] & 0xFFFFu;
+      const uint32_t b1 = off + (pre >> 16);
+      off += tot[w] >> 16;
+      cw[w] = (b0 & 0xFFFFu) | (b1 << 16);
+    }
+  }
+  // 3. each rank's input index at its place in the yarns (eight ranks' input
+  // indices loaded together: one HBM latency per eight ranks)
+  for (uint32_t r = r0; r < r1; r += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) v[k] = r + k < r1 ? sval16[base + r + k] : 0u;
+    const uint32_t wa = sr32[r >> 2], wb = r + 4 < r1 ? sr32[(r >> 2) + 1] : 0xFFFFFFFFu;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) {
+      const uint32_t st = r + k < r1 ? ((k < 4 ? wa : wb) >> (8 * (k & 3))) & 0xFFu : 0xFFu;
+      const uint32_t sh = (st & 1) * 16;
+      uint32_t p = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t w = 0; w < 8; w++)
+        if (w == (st >> 1)) {
+          p = (cw[w] >> sh) & 0xFFFFu;
+          cw[w] += 1u << sh;
+        }
+      if (p < n) out[p] = (uint16_t)v[k];
+    }
+  }
+  __syncthreads();
+  // 4. the yarns out, coalesced (written straight from step 3 as scattered
+  // 4-byte pieces they took 6.5 ms a config-2 step instead of 2.5)
+  for (uint32_t p = tid; p < n; p += NT) lane_at(yarn + base, p) = out[p];
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
@@ -5323,9 +5171,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       if (!big || !rank16 || !kbm) return fail(c, "out of device memory (front)");
       HIPCHK(c, hipMemsetAsync(big, 0, 16, c->stream));
       sval = svA;
-      // the yarns inside the fused kernel (site fields of <= 4 bits): no ids
-      // in rank order written, no sort by site afterwards
-      yarns_fused = want_yarns && bt->site_bits <= 4;  // (<= 2 rounds of 8 sites)
+      // the yarns by k_yarn_doc after the fused kernel (site fields of <= 4
+      // bits, the document's sites and yarn in LDS): no ids in rank order
+      // written, no sort by site afterwards
+      yarns_fused = want_yarns && bt->site_bits <= 4 && yarn_lds_bytes(t.nmax) + 64 <= c->lds_max;
       unsigned long long *tprof_f = nullptr;
       if (c->tree_prof) {
         tprof_f = scratch_t<unsigned long long>(c, "tprof3", (size_t)D * 8);
@@ -5343,8 +5192,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 &&
                    tl_lds + 64 * 4 + 4 <= c->lds_max &&
                    wd_lds + 1024 <= c->lds_max && to_lds <= TOUR_LDS_MAX;
-      // (k_front writes the ids for the yarn sort; CW_TREE_PROF's kernels have no yarn code)
-      yarns_fused = yarns_fused && fused_done && !c->tree_prof;
+      // (k_front writes the ids for the yarn sort)
+      yarns_fused = yarns_fused && fused_done;
       skey = want_yarns && !yarns_fused ? skA : nullptr;
       if (fused_done) {
         uint32_t *fcS = scratch_t<uint32_t>(c, "fcS", N), *thr = scratch_t<uint32_t>(c, "thr", N);
@@ -5371,8 +5220,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              nullptr, sv_ptr, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status,
                              big, dev_tab(c, "t_doc_log2k"), kbits_t, (t.nmax + 31) / 32, nsc, fcS,
                              (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
-                             out->visible_count, loc, tprof_f, yarns_fused ? out->yarn_perm : nullptr,
-                             bt->site_shift | bt->site_bits << 8);
+                             out->visible_count, loc, tprof_f);
         };
         const bool wy = want_yarns && !yarns_fused;  // (u32 sval: the yarn sort's values)
         if (tprof_f) {  // (the default front-end depth, so the clocks are the product's)
@@ -5380,7 +5228,6 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
           else launch(k_weave_doc<1024, 2048, uint16_t, true, 4, 1>, sval16);
         } else {
           if (wy) launch(k_weave_doc<1024, 2048, uint32_t, false, 4, 1>, sval);
-          else if (yarns_fused) launch(k_weave_doc<1024, 2048, uint16_t, false, 4, 1, true>, sval16);
           else launch(k_weave_doc<1024, 2048, uint16_t, false, 4, 1>, sval16);
         }
       } else {
@@ -5416,6 +5263,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       if (c->pin_small[0] == 0) {
         front_done = true;
         c->x_hint = c->pin_small[1] != 0;  // flagged documents, for the exact path
+        if (fused_done && yarns_fused) {
+          Launch L(c, "yarns", (double)N * (8 + 2 + 2 + 4));
+          hipLaunchKernelGGL(k_yarn_doc<1024>, dim3((uint32_t)D), dim3(1024), (size_t)yarn_lds_bytes(t.nmax),
+                             c->stream, id_key, rank16, (const uint16_t *)c->bufs["sval16"].p,
+                             doc_off, bt->site_shift, bt->site_bits, out->yarn_perm);
+        }
+        if (check_launch(c, "yarns")) return -1;
       } else {  // a document's ids leave the small directory: the three-kernel front end
         HIPCHK(c, hipMemsetAsync(out->status, 0, D * 4, c->stream));
         if (fused_done) {  // (and the separate tree and tour: the fused kernel stopped early)

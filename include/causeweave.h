@@ -248,7 +248,12 @@ typedef struct {
 } cw_map_result;
 
 /* memspace: where id_key / cause / cause_is_id / kind and every result array
- * live (coll_offsets is always host memory; n_segs is returned in the struct). */
+ * live (coll_offsets is always host memory; n_segs is returned in the struct).
+ * On a nonzero return every result array holds unspecified values: a
+ * device-memory call that repeats the previous call's collection count takes
+ * that call's pack table on trust and checks the whole layout while the kernel
+ * runs, so it may have written the outputs before it finds coll_offsets
+ * invalid. */
 int cw_weave_maps(cw_ctx *ctx, const cw_map_batch *batch, cw_map_result *result, int memspace);
 
 /* ---------------------------------------------------------------- merge ---- */

@@ -20,3 +20,6 @@ for rep in 1 2; do
     echo "$lib $(cut -c1-220 $out/ab_$rep.txt)"
   done
 done
+# the counters this box lists (address translation, for the giant path's walk)
+(cd /tmp && timeout -k 5 60 rocprofv3 -L > "$OLDPWD/$out/counters.txt" 2>&1) || true
+grep -io "[A-Za-z_0-9]*\(UTCL\|TLB\|TRANSLAT\)[A-Za-z_0-9]*" $out/counters.txt | sort -u | head -40
