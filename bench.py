@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--dist", action="store_true",
                     help="--config 5 on one GPU through the distributed path (sample sort, "
                          "exchange, gather; always taken when N > 1)")
+    ap.add_argument("--cache", default=None,
+                    help="configs 1/2/5: save the generated input under this directory, or load "
+                         "it from there when present (several profiler passes, one generation)")
     ap.add_argument("--check", action="store_true",
                     help="after timing, every rank compares its outputs with the CPU oracle "
                          "(configs 2, 3 and 4; the JSON line gets a 'check' object)")
@@ -741,8 +744,19 @@ def main():
     layout = spec.layout()
     t0 = time.time()
     k32 = a.keys == 32
-    with heartbeat("generating the input"):
-        off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16, k32=k32)
+    tag = f"c{a.config}_n{spec.doc_size}_d{d0}-{d1}_k{a.keys}"
+    cached = a.cache and all(os.path.exists(os.path.join(a.cache, f"{tag}_{x}.npy"))
+                             for x in ("off", "id", "cause", "kind"))
+    if cached:  # (PMC passes re-run the bench: generate a large input once a call)
+        off, idk, ck, kd = (np.load(os.path.join(a.cache, f"{tag}_{x}.npy"))
+                            for x in ("off", "id", "cause", "kind"))
+    else:
+        with heartbeat("generating the input"):
+            off, idk, ck, kd = gen.generate(spec, d0, d1, nthreads=16, k32=k32)
+        if a.cache:
+            os.makedirs(a.cache, exist_ok=True)
+            for x, arr in zip(("off", "id", "cause", "kind"), (off, idk, ck, kd)):
+                np.save(os.path.join(a.cache, f"{tag}_{x}.npy"), arr)
     N = len(idk)
     t_gen = time.time() - t0
     kv = np.int32 if k32 else np.int64
@@ -910,10 +924,13 @@ def main():
     kernel_ms_total = sum(v[1] for v in stats.values())
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
-    traffic, tnote = pmc_traffic(name, f"config{a.config}",
+    # (config 5 has passes at its scaled default, 2^26 nodes, and at BASELINE's
+    # full 2,000,000,001 nodes: workload "config5full")
+    full5 = a.config == 5 and a.giant == 2_000_000_001
+    traffic, tnote = pmc_traffic(name, "config5full" if full5 else f"config{a.config}",
                                  a.keys == 64 and (a.config == 1 or (a.config == 2 and a.docs == 10_000
                                                    and a.nodes == 50_000) or
-                                                   (a.config == 5 and a.giant == 1 << 26)))
+                                                   (a.config == 5 and a.giant == 1 << 26) or full5))
 
     if rank == 0:
         cpu = None
@@ -956,6 +973,9 @@ def main():
             "ms_per_step_events_on_every_launch_rank0": dt_allprof / a.steps * 1e3,
             "end_to_end_pcie": e2e,
             "gen_s": t_gen,
+            # device memory in use after the timed steps (inputs, outputs and the
+            # library's scratch): the config-5 sizing
+            "hbm_used_gib": round((lambda f, t: (t - f) / 2**30)(*torch.cuda.mem_get_info(dev)), 2),
         }
         if cpu:
             line["speedup_vs_cpu_baseline"] = value / cpu["value"]

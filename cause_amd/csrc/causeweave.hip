@@ -4256,6 +4256,7 @@ struct PendingEvt {
 struct cw_ctx {
   int device = 0;
   uint32_t lds_max = 160 * 1024;  // LDS a workgroup may use on this device (queried at create)
+  size_t hbm_total = 0;             // device memory (queried at create)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   bool async = false;
@@ -4358,7 +4359,9 @@ void *scratch(cw_ctx *c, const char *name, size_t bytes) {
     if (b.p) (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
-    size_t want = bytes + bytes / 8;  // headroom for slightly larger batches
+    // headroom for slightly larger batches, at most 256 MiB (a 2e9-node list
+    // would otherwise hold 12% of its scratch idle)
+    size_t want = bytes + std::min(bytes / 8, (size_t)256 << 20);
     if (hipMalloc(&b.p, want) != hipSuccess) {
       (void)hipGetLastError();
       return nullptr;
@@ -4499,10 +4502,14 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     uint32_t log2k = t.tour ? t.tour_log2k : c->min_log2k, log2cap = c->min_log2cap;
     // one giant document: every slot overflow takes a sublist id from one
     // counter; 32-entry slots overflow ~8x less often (walk 2.8 -> 1.5 ms at
-    // 6.7e7 nodes) for 8 more bytes a node, so below 2^30 nodes
-    // (CW_GIANT_LOG2CAP: the tests shrink it to send walks through many
-    // continuation sublists)
-    if (giant && n < (1u << 30)) log2cap = std::max(log2cap, c->giant_log2cap);
+    // 6.7e7 nodes) for 4 more bytes a node (16-node blocks), so whenever the
+    // list fits the device with them (round 5: the rule was n < 2^30, and the
+    // 2e9-node walk ran 1.8x slower a node than at 5.4e8 -- the same loads,
+    // L2 misses and HBM bytes a node, twice the continuation sublists;
+    // DESIGN 5e).  (CW_GIANT_LOG2CAP: the tests shrink it to send walks
+    // through many continuation sublists)
+    if (giant && (n < (1u << 30) || (uint64_t)n * GIANT_CAP32_BYTES <= c->hbm_total))
+      log2cap = std::max(log2cap, c->giant_log2cap);
     // and 16-node splitter blocks: half the sublists to rank for a slightly
     // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8),
     // once there are walkers enough to fill the chip (config 1's 10^5 nodes:
@@ -6729,6 +6736,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
     if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) == hipSuccess &&
         lds > 0)
       c->lds_max = (uint32_t)lds;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess) c->hbm_total = tot;
   }
   auto knob = [](const char *name, uint32_t dflt) {
     const char *v = getenv(name);

@@ -55,7 +55,7 @@ def main():
             # the library reports sort passes by what they sort: on the giant
             # path (configs 1, 5) the 64-bit keys are the id sort, the 32-bit
             # ones the group-key sort; elsewhere they are not separable
-            if a.workload not in ("config1", "config5") or not name.startswith("radix_") or \
+            if not a.workload.startswith(("config1", "config5")) or not name.startswith("radix_") or \
                     "<" not in sym:
                 continue  # (the scans serve both sorts)
             width = "idsort" if "unsigned long" in sym else "gsort"
