@@ -3227,10 +3227,14 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
   }
   __syncthreads();
   stamp(0);
-  auto split_at = [&](uint32_t u) { return (sbm[u >> 5] >> (u & 31)) & 1u; };
   bool bad = false;
   // pass 1: per-lane walker state machines over the sublists; every node's
-  // (sublist, index inside it) goes to HBM scratch (fire-and-forget stores)
+  // (sublist, index inside it) goes to HBM scratch (fire-and-forget stores).
+  // A step reads the node's successor and its splitter bit together (one LDS
+  // round trip a node; round 5: 12.28 -> 12.22 ms a config-2 step.  Two
+  // walkers a lane stepped together lost, 12.54 ms, and so did the tree's two
+  // chains a lane in its list walk and pointer jumping, 13.04 ms:
+  // profiles/r05_tour_chains_ab.txt)
   {
     uint32_t j = tid, u = 0, cnt = 0;
     bool live = j < S;
@@ -3241,7 +3245,9 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
       cnt = 1;
     }
     while (live) {
-      const bool end = u == TOUR_END || u >= n || split_at(u) || cnt > n;
+      const uint32_t us = u < n ? u : 0u;
+      const uint32_t nx = succ[us], sw = sbm[us >> 5];  // both reads in flight
+      const bool end = u >= n || ((sw >> (us & 31)) & 1u) || cnt > n;
       if (end) {
         bad |= (u != TOUR_END && u >= n) || cnt > n;
         sub[j] = min(cnt, 0xFFFFu) | (u < n ? (u >> log2k) : TOUR_END) << 16;
@@ -3256,7 +3262,7 @@ __device__ __forceinline__ void tour_doc(const uint32_t *__restrict__ link,
       } else {
         lane_at(locD, u) = (j << 16) | cnt;
         cnt++;
-        u = succ[u];
+        u = nx;
       }
     }
   }
