@@ -633,7 +633,13 @@ def main_stream(a, world, rank, local, dist, torch, dev):
     wall_max = shard.reduce_max_time(st.wall_s, dist, dev) if world > 1 else st.wall_s
     total = T * n
     name, (launches, ms, by) = max(stats.items(), key=lambda kv: kv[1][1])
-    achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    achieved_kernel = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    # SURVEY 8(d)'s bytes for the fused weave (as config 2): B_io per node of a
+    # batch -- ids, causes, kinds in, weave_perm and the visible bit out
+    kw_io, pw_io = (4 if k32 else 8), (2 if perm16 else 4)
+    b_io = kw_io + kw_io + 1 + pw_io + 1 / 8
+    whole = name == "weave"
+    achieved = (B * n * b_io * launches if whole else by) / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     # a config-3 batch has the config-2 batch's shape: the same kernels' counters
     traffic, tnote = pmc_traffic(name, "config2", B == 10_000 and a.nodes == 50_000)
     if rank == 0:
@@ -658,6 +664,9 @@ def main_stream(a, world, rank, local, dist, torch, dev):
                        "parallelism": f"docs sharded x{world}"},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "frac_io": achieved / HBM_PEAK_GBS if whole else None,
+                         "bytes_alg_per_node": b_io if whole else by / launches / (B * n),
+                         "achieved_kernel_scratch": achieved_kernel,
                          "traffic": traffic, "traffic_note": tnote,
                          "launches_per_step": launches / nb,
                          "kernel_ms_per_step": ms / nb},
@@ -919,7 +928,7 @@ def main():
     # handoffs (achieved_kernel_scratch) are not algorithmic bytes.
     b_io = (4 + 4 + 1 + 4 + 1 / 8) if k32 else (8 + 8 + 1 + 4 + 1 / 8)
     whole = name == "weave"
-    by_io = N * b_io * launches / a.steps if whole else by
+    by_io = N * b_io * launches if whole else by  # (launches and ms: over all timed steps)
     achieved = by_io / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     kernel_ms_total = sum(v[1] for v in stats.values())
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
