@@ -3429,14 +3429,15 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
 // the id order partitioned by site, id-ascending inside a site), one workgroup
 // per document after it, from what it leaves in HBM: every input's rank
 // (rank16) and every rank's input index (sval16).  In LDS: the site of every
-// rank (a byte), then the yarn as u16 input indices, written out as whole lines.
-// 16 B a node: id 8 + rank 2 + sval 2 in, yarn_perm 4 out.  (Round 4 placed the
-// yarns inside the fused kernel's front end, from its directory: +3.9 ms on a
-// config-2 step; an LDS-staged version there, +3.8 ms; this kernel: 2.55 ms,
-// of which ~1.8 ms is its LDS work -- site scatter 0.3, counts 0.6, placement
-// 0.8 -- and ~0.8 ms its HBM reads, profiles/r05_yarn_ab.txt.)
+// rank (a byte, 50 KB at 50,001 nodes: two workgroups a CU); the yarn is
+// written straight from a wave-level multisplit, each wave's ranks going to
+// 16 runs that grow a chunk at a time.  16 B a node: id 8 + rank 2 + sval 2
+// in, yarn_perm 4 out.  (Round 4 placed the yarns inside the fused kernel's
+// front end: +3.9 ms on a config-2 step; round 5: an LDS-staged version there,
+// +3.8 ms; this kernel with per-thread rank ranges and the yarn staged in LDS,
+// 2.60 ms; with the multisplit and no staging, 2.37 ms; profiles/r05_yarn_ab.txt.)
 __host__ __device__ inline uint32_t yarn_lds_bytes(uint32_t nmax) {
-  return ((nmax + 3) & ~3u) + 2 * ((nmax + 1) & ~1u);  // sites (a byte a rank), the yarn (u16)
+  return (nmax + 3) & ~3u;  // the site of every rank (a byte)
 }
 
 template <int NT>
@@ -3447,16 +3448,12 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint64_t *__restrict__ id
                                                  uint32_t site_shift, uint32_t site_bits,
                                                  uint32_t *__restrict__ yarn) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_y[];
-  __shared__ uint32_t wrow[NT / 64][8];
+  __shared__ uint32_t wrow[NT / 64][16];
   const uint32_t tid = threadIdx.x;
   const uint32_t d = blockIdx.x;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   uint8_t *const sr = reinterpret_cast<uint8_t *>(lds_y);
-  uint16_t *const out = reinterpret_cast<uint16_t *>(sr + ((n + 3) & ~3u));
   const uint32_t smask = (1u << site_bits) - 1;
-  // each thread's ranks for steps 2-3 (a multiple of 8: the sites are read
-  // four to a word)
-  const uint32_t per = ((n + NT - 1) / NT + 7) & ~7u, r0 = min(n, tid * per), r1 = min(n, r0 + per);
   for (uint32_t w = tid; w < (n + 3) / 4; w += NT) lds_y[w] = 0xFFFFFFFFu;  // (no site: a DUP doc)
   __syncthreads();
   // 1. the site of every rank
@@ -3475,90 +3472,70 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint64_t *__restrict__ id
       if (r[u] < n) sr[r[u]] = (uint8_t)((x[u] >> site_shift) & smask);
   }
   __syncthreads();
-  // 2. per-site counts over each thread's contiguous ranks (two 16-bit
-  // counters a register, no run-time index; a range starts at a multiple of 8
-  // ranks: the sites are read four to a word), block scans -> each thread's
-  // output position per site
-  const uint32_t *const sr32 = lds_y;
-  uint32_t cw[8];
-#pragma unroll
-  for (uint32_t w = 0; w < 8; w++) cw[w] = 0;
-  for (uint32_t r = r0; r < r1; r += 4) {
-    const uint32_t w4 = sr32[r >> 2];
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-      const uint32_t st = r + k < r1 ? (w4 >> (8 * k)) & 0xFFu : 0xFFu;
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++)
-        if (w == (st >> 1)) cw[w] += 1u << ((st & 1) * 16);
-    }
-  }
-  // the eight registers scanned together: wave scans, the waves' totals
-  // through LDS (one row of eight words a wave)
+  // 2-3. a wave-level multisplit: wave wv owns a contiguous range of ranks and
+  // takes them 64 at a time, lane = rank; four ballots of the site bits give
+  // every lane the mask of its site's lanes, so a site's count is a popcount
+  // and a rank's place among its site's ranks of the chunk is the popcount of
+  // that mask below the lane.  Pass A counts per site and wave (wave-uniform
+  // registers), the 16 x 16 totals go through LDS, pass B places every rank's
+  // input index at its site's running offset (lane s of the wave holds site
+  // s's).  (Round 5 v3 gave each thread a contiguous range and sixteen 16-bit
+  // counters: 2.55 ms a config-2 step, its counting and placement ALU-bound.)
   {
+    constexpr uint32_t NW = NT / 64;
     const uint32_t lane = tid & 63, wv = tid >> 6;
-    uint32_t inc[8];
-#pragma unroll
-    for (uint32_t w = 0; w < 8; w++) {
-      inc[w] = cw[w];
-#pragma unroll
-      for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc[w], o, 64);
-        if (lane >= o) inc[w] += y;
-      }
+    const uint32_t perw = ((n + NW - 1) / NW + 63) & ~63u;
+    const uint32_t w0 = min(n, wv * perw), w1 = min(n, w0 + perw);
+    // the lanes of site `st` among this chunk's ballots (st = 0xFF: none)
+    auto site_mask = [&](uint32_t st, uint64_t valid, uint64_t b0, uint64_t b1, uint64_t b2,
+                         uint64_t b3) -> uint64_t {
+      return valid & ((st & 1u) ? b0 : ~b0) & ((st & 2u) ? b1 : ~b1) & ((st & 4u) ? b2 : ~b2) &
+             ((st & 8u) ? b3 : ~b3);
+    };
+    // pass A: lane s (< 16) counts site s over the wave's range
+    uint32_t cnt = 0;
+    for (uint32_t c = w0; c < w1; c += 64) {
+      const uint32_t r = c + lane;
+      const uint32_t st = r < w1 ? sr[r] : 0xFFu;
+      const uint64_t valid = __ballot(st < 16u), b0 = __ballot(st & 1u), b1 = __ballot(st & 2u),
+                     b2 = __ballot(st & 4u), b3 = __ballot(st & 8u);
+      cnt += (uint32_t)__popcll(site_mask(lane, valid, b0, b1, b2, b3));
     }
-    if (lane == 63)
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++) wrow[wv][w] = inc[w];
+    if (lane < 16) wrow[wv][lane] = cnt;
     __syncthreads();
-    uint32_t before[8], tot[8];
-#pragma unroll
-    for (uint32_t w = 0; w < 8; w++) before[w] = tot[w] = 0;
+    // lane s: the ranks of sites < s (all waves) + of site s in earlier waves
+    uint32_t before = 0, tot = 0;
+    if (lane < 16) {
 #pragma unroll 1
-    for (uint32_t i = 0; i < NT / 64; i++) {
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++) {
-        const uint32_t t = wrow[i][w];
-        before[w] += i < wv ? t : 0u;
-        tot[w] += t;
+      for (uint32_t i = 0; i < NW; i++) {
+        const uint32_t t = wrow[i][lane];
+        before += i < wv ? t : 0u;
+        tot += t;
       }
     }
-    uint32_t off = 0;
+    uint32_t ex = tot;  // exclusive scan of the site totals over lanes 0..15
 #pragma unroll
-    for (uint32_t w = 0; w < 8; w++) {
-      const uint32_t pre = before[w] + inc[w] - cw[w];
-      const uint32_t b0 = off + (pre & 0xFFFFu);
-      off += tot[w] & 0xFFFFu;
-      const uint32_t b1 = off + (pre >> 16);
-      off += tot[w] >> 16;
-      cw[w] = (b0 & 0xFFFFu) | (b1 << 16);
+    for (uint32_t o = 1; o < 16; o <<= 1) {
+      const uint32_t y = __shfl_up(ex, o, 64);
+      if (lane >= o) ex += y;
+    }
+    uint32_t off = ex - tot + before;  // lane s: where this wave's next site-s rank goes
+    // pass B: input indices two chunks ahead (one HBM latency per chunk pair)
+    const uint16_t *const svD = sval16 + base;
+    uint32_t *const yD = yarn + base;
+    uint32_t va = w0 + lane < w1 ? svD[w0 + lane] : 0u;
+    for (uint32_t c = w0; c < w1; c += 64) {
+      const uint32_t r = c + lane;
+      const uint32_t vn = r + 64 < w1 ? svD[r + 64] : 0u;
+      const uint32_t st = r < w1 ? sr[r] : 0xFFu;
+      const uint64_t valid = __ballot(st < 16u), b0 = __ballot(st & 1u), b1 = __ballot(st & 2u),
+                     b2 = __ballot(st & 4u), b3 = __ballot(st & 8u);
+      const uint32_t base_s = __shfl(off, st & 15u, 64);
+      if (st < 16u) yD[base_s + lanes_below(site_mask(st, valid, b0, b1, b2, b3))] = va;
+      off += (uint32_t)__popcll(site_mask(lane, valid, b0, b1, b2, b3));
+      va = vn;
     }
   }
-  // 3. each rank's input index at its place in the yarns (eight ranks' input
-  // indices loaded together: one HBM latency per eight ranks)
-  for (uint32_t r = r0; r < r1; r += 8) {
-    uint32_t v[8];
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) v[k] = r + k < r1 ? sval16[base + r + k] : 0u;
-    const uint32_t wa = sr32[r >> 2], wb = r + 4 < r1 ? sr32[(r >> 2) + 1] : 0xFFFFFFFFu;
-#pragma unroll
-    for (uint32_t k = 0; k < 8; k++) {
-      const uint32_t st = r + k < r1 ? ((k < 4 ? wa : wb) >> (8 * (k & 3))) & 0xFFu : 0xFFu;
-      const uint32_t sh = (st & 1) * 16;
-      uint32_t p = 0xFFFFFFFFu;
-#pragma unroll
-      for (uint32_t w = 0; w < 8; w++)
-        if (w == (st >> 1)) {
-          p = (cw[w] >> sh) & 0xFFFFu;
-          cw[w] += 1u << sh;
-        }
-      if (p < n) out[p] = (uint16_t)v[k];
-    }
-  }
-  __syncthreads();
-  // 4. the yarns out, coalesced (written straight from step 3 as scattered
-  // 4-byte pieces they took 6.5 ms a config-2 step instead of 2.5)
-  for (uint32_t p = tid; p < n; p += NT) lane_at(yarn + base, p) = out[p];
 }
 
 __global__ __launch_bounds__(256) void k_pack_bits(const uint8_t *__restrict__ vis8, uint32_t N,
