@@ -1310,7 +1310,8 @@ __device__ __forceinline__ bool front_doc(
     uint8_t *__restrict__ skind, VT *__restrict__ sval, uint32_t *__restrict__ kbm,
     uint64_t *__restrict__ skey, uint16_t *rank16, uint64_t *__restrict__ max_ts, uint32_t ts_shift,
     uint32_t *__restrict__ status, uint32_t *__restrict__ big,
-    unsigned long long *__restrict__ tprof, uint32_t d, uint4 *sdir) {
+    unsigned long long *__restrict__ tprof, uint32_t d, uint4 *sdir,
+    uint8_t *__restrict__ site8 = nullptr, uint32_t site_shift = 0, uint32_t site_mask = 0) {
   unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tlast = 0;
   auto stamp = [&](int ph) {  // diagnostic phase times (CW_TREE_PROF)
     if (tprof) {
@@ -1447,6 +1448,8 @@ __device__ __forceinline__ bool front_doc(
         if (cls & 2) atomicOr(&clsB[r >> 5], 1u << (r & 31));
       }
       lane_at(rankD, i) = (uint16_t)min(r, 0xFFFFu);
+      // the site of every input for the yarns (k_yarn_doc): one coalesced byte
+      if (site8) lane_at(site8 + base, i) = (uint8_t)((k[u] >> site_shift) & site_mask);
     }
   }
   if (st) atomicOr(&bst, st);
@@ -3397,7 +3400,8 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
     uint32_t kbits, uint32_t bm_words, uint32_t *__restrict__ nsc, uint32_t *__restrict__ fcS,
     uint32_t *__restrict__ link, uint32_t *__restrict__ osp, uint32_t *__restrict__ perm,
     uint32_t *__restrict__ vbits, uint32_t *__restrict__ vcount, uint32_t *loc,
-    unsigned long long *__restrict__ tprof) {
+    unsigned long long *__restrict__ tprof, uint8_t *__restrict__ site8, uint32_t site_shift,
+    uint32_t site_mask) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
   const uint32_t d = blockIdx.x;
   // (tprof, CW_TREE_PROF: the three phases' clocks per document)
@@ -3407,7 +3411,7 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
   if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, d,
-                     reinterpret_cast<uint4 *>(lds_w)))
+                     reinterpret_cast<uint4 *>(lds_w), site8, site_shift, site_mask))
     return;
   __syncthreads();  // (workgroup-scope release/acquire: this CU's writes are visible to it)
   const unsigned long long t1 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -3431,8 +3435,8 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
 // (rank16) and every rank's input index (sval16).  In LDS: the site of every
 // rank (a byte, 50 KB at 50,001 nodes: two workgroups a CU); the yarn is
 // written straight from a wave-level multisplit, each wave's ranks going to
-// 16 runs that grow a chunk at a time.  16 B a node: id 8 + rank 2 + sval 2
-// in, yarn_perm 4 out.  (Round 4 placed the yarns inside the fused kernel's
+// 16 runs that grow a chunk at a time.  9 B a node: site 1 + rank 2 + sval 2
+// in, yarn_perm 4 out (the fused kernel writes the site byte: +1 B there).  (Round 4 placed the yarns inside the fused kernel's
 // front end: +3.9 ms on a config-2 step; round 5: an LDS-staged version there,
 // +3.8 ms; this kernel with per-thread rank ranges and the yarn staged in LDS,
 // 2.60 ms; with the multisplit and no staging, 2.37 ms; profiles/r05_yarn_ab.txt.)
@@ -3441,11 +3445,10 @@ __host__ __device__ inline uint32_t yarn_lds_bytes(uint32_t nmax) {
 }
 
 template <int NT>
-__global__ __launch_bounds__(NT) void k_yarn_doc(const uint64_t *__restrict__ id_key,
+__global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ site8,
                                                  const uint16_t *__restrict__ rank16,
                                                  const uint16_t *__restrict__ sval16,
                                                  const uint32_t *__restrict__ doc_off,
-                                                 uint32_t site_shift, uint32_t site_bits,
                                                  uint32_t *__restrict__ yarn) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_y[];
   __shared__ uint32_t wrow[NT / 64][16];
@@ -3453,23 +3456,22 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint64_t *__restrict__ id
   const uint32_t d = blockIdx.x;
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   uint8_t *const sr = reinterpret_cast<uint8_t *>(lds_y);
-  const uint32_t smask = (1u << site_bits) - 1;
   for (uint32_t w = tid; w < (n + 3) / 4; w += NT) lds_y[w] = 0xFFFFFFFFu;  // (no site: a DUP doc)
   __syncthreads();
-  // 1. the site of every rank
+  // 1. the site of every rank (the fused kernel's front end wrote each input's
+  // site byte beside its rank)
   constexpr uint32_t U = 8;
   for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
-    uint64_t x[U];
-    uint32_t r[U];
+    uint32_t x[U], r[U];
 #pragma unroll
     for (uint32_t u = 0; u < U; u++) {
       const uint32_t i = i0 + u * NT;
-      x[u] = i < n ? lane_at(id_key + base, i) : 0ull;
+      x[u] = i < n ? lane_at(site8 + base, i) : 0u;
       r[u] = i < n ? lane_at(rank16 + base, i) : 0xFFFFu;
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
-      if (r[u] < n) sr[r[u]] = (uint8_t)((x[u] >> site_shift) & smask);
+      if (r[u] < n) sr[r[u]] = (uint8_t)x[u];
   }
   __syncthreads();
   // 2-3. a wave-level multisplit: wave wv owns a contiguous range of ranks and
@@ -5193,6 +5195,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         const uint32_t kbits_t = ceil_log2((uint64_t)t.nmax + 1) + 1;
         // par and (without yarns, which sort by it) sval as u16, no skind
         uint16_t *par16 = scratch_t<uint16_t>(c, "par16", N);
+        // the site of every input, for k_yarn_doc (one byte a node)
+        uint8_t *site8 = yarns_fused ? scratch_t<uint8_t>(c, "site8", N) : nullptr;
+        if (yarns_fused && !site8) return fail(c, "out of device memory (fused weave)");
         uint16_t *sval16 = want_yarns && !yarns_fused ? nullptr : scratch_t<uint16_t>(c, "sval16", N);
         if (!par16 || (!(want_yarns && !yarns_fused) && !sval16))
           return fail(c, "out of device memory (fused weave)");
@@ -5201,7 +5206,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         // fcS clear 4, nsc 4; fcS + nsc back 8, link 4), tour (link 4, sval, the
         // (sublist, index) records out and back 8, weave_perm 4, bits)
         const double sv = want_yarns ? 4 : 2;
-        Launch L(c, "weave", (double)N * (8 + 8 + 8 + 1 + 2 + 2 + 2 + sv + (skey ? 16 : 0) + 0.25) +
+        Launch L(c, "weave", (double)N * (8 + 8 + 8 + 1 + 2 + 2 + 2 + sv + (skey ? 16 : 0) + (site8 ? 1 : 0) + 0.25) +
                                  (double)N * (2 + 0.25 + 4 + 4 + 8 + 4) +
                                  (double)N * (4 + sv + 8 + 4 + 0.125));
         auto launch = [&](auto kern, auto *sv_ptr) {
@@ -5210,7 +5215,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                              nullptr, sv_ptr, kbm, skey, rank16, out->max_ts, bt->ts_shift, out->status,
                              big, dev_tab(c, "t_doc_log2k"), kbits_t, (t.nmax + 31) / 32, nsc, fcS,
                              (uint32_t *)link, thr, out->weave_perm, out->visible_bits,
-                             out->visible_count, loc, tprof_f);
+                             out->visible_count, loc, tprof_f, site8, bt->site_shift,
+                             (1u << bt->site_bits) - 1u);
         };
         const bool wy = want_yarns && !yarns_fused;  // (u32 sval: the yarn sort's values)
         if (tprof_f) {  // (the default front-end depth, so the clocks are the product's)
@@ -5254,10 +5260,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         front_done = true;
         c->x_hint = c->pin_small[1] != 0;  // flagged documents, for the exact path
         if (fused_done && yarns_fused) {
-          Launch L(c, "yarns", (double)N * (8 + 2 + 2 + 4));
+          Launch L(c, "yarns", (double)N * (1 + 2 + 2 + 4));
           hipLaunchKernelGGL(k_yarn_doc<1024>, dim3((uint32_t)D), dim3(1024), (size_t)yarn_lds_bytes(t.nmax),
-                             c->stream, id_key, rank16, (const uint16_t *)c->bufs["sval16"].p,
-                             doc_off, bt->site_shift, bt->site_bits, out->yarn_perm);
+                             c->stream, (const uint8_t *)c->bufs["site8"].p, rank16,
+                             (const uint16_t *)c->bufs["sval16"].p, doc_off, out->yarn_perm);
         }
         if (check_launch(c, "yarns")) return -1;
       } else {  // a document's ids leave the small directory: the three-kernel front end
