@@ -3460,7 +3460,7 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
   __syncthreads();
   // 1. the site of every rank (the fused kernel's front end wrote each input's
   // site byte beside its rank)
-  constexpr uint32_t U = 8;
+  constexpr uint32_t U = 16;
   for (uint32_t i0 = tid; i0 < n; i0 += U * NT) {
     uint32_t x[U], r[U];
 #pragma unroll
@@ -3522,20 +3522,30 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
       if (lane >= o) ex += y;
     }
     uint32_t off = ex - tot + before;  // lane s: where this wave's next site-s rank goes
-    // pass B: input indices two chunks ahead (one HBM latency per chunk pair)
+    // pass B: the input indices of PB chunks loaded together (one HBM latency
+    // per PB chunks, not per chunk)
     const uint16_t *const svD = sval16 + base;
     uint32_t *const yD = yarn + base;
-    uint32_t va = w0 + lane < w1 ? svD[w0 + lane] : 0u;
-    for (uint32_t c = w0; c < w1; c += 64) {
-      const uint32_t r = c + lane;
-      const uint32_t vn = r + 64 < w1 ? svD[r + 64] : 0u;
-      const uint32_t st = r < w1 ? sr[r] : 0xFFu;
-      const uint64_t valid = __ballot(st < 16u), b0 = __ballot(st & 1u), b1 = __ballot(st & 2u),
-                     b2 = __ballot(st & 4u), b3 = __ballot(st & 8u);
-      const uint32_t base_s = __shfl(off, st & 15u, 64);
-      if (st < 16u) yD[base_s + lanes_below(site_mask(st, valid, b0, b1, b2, b3))] = va;
-      off += (uint32_t)__popcll(site_mask(lane, valid, b0, b1, b2, b3));
-      va = vn;
+    constexpr uint32_t PB = 8;
+    for (uint32_t c0 = w0; c0 < w1; c0 += PB * 64) {
+      uint32_t v[PB];
+#pragma unroll
+      for (uint32_t k = 0; k < PB; k++) {
+        const uint32_t r = c0 + k * 64 + lane;
+        v[k] = r < w1 ? svD[r] : 0u;
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < PB; k++) {
+        const uint32_t c = c0 + k * 64;
+        if (c >= w1) break;  // (wave-uniform)
+        const uint32_t r = c + lane;
+        const uint32_t st = r < w1 ? sr[r] : 0xFFu;
+        const uint64_t valid = __ballot(st < 16u), b0 = __ballot(st & 1u), b1 = __ballot(st & 2u),
+                       b2 = __ballot(st & 4u), b3 = __ballot(st & 8u);
+        const uint32_t base_s = __shfl(off, st & 15u, 64);
+        if (st < 16u) yD[base_s + lanes_below(site_mask(st, valid, b0, b1, b2, b3))] = v[k];
+        off += (uint32_t)__popcll(site_mask(lane, valid, b0, b1, b2, b3));
+      }
     }
   }
 }
