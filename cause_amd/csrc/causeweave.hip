@@ -3432,14 +3432,17 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
 // The yarns of the documents k_weave_doc took (spin 1-arity, shared.cljc:121-132:
 // the id order partitioned by site, id-ascending inside a site), one workgroup
 // per document after it, from what it leaves in HBM: every input's rank
-// (rank16) and every rank's input index (sval16).  In LDS: the site of every
-// rank (a byte, 50 KB at 50,001 nodes: two workgroups a CU); the yarn is
-// written straight from a wave-level multisplit, each wave's ranks going to
-// 16 runs that grow a chunk at a time.  9 B a node: site 1 + rank 2 + sval 2
-// in, yarn_perm 4 out (the fused kernel writes the site byte: +1 B there).  (Round 4 placed the yarns inside the fused kernel's
-// front end: +3.9 ms on a config-2 step; round 5: an LDS-staged version there,
-// +3.8 ms; this kernel with per-thread rank ranges and the yarn staged in LDS,
-// 2.60 ms; with the multisplit and no staging, 2.37 ms; profiles/r05_yarn_ab.txt.)
+// (rank16) and site byte (site8, written by the fused kernel's front end) and
+// every rank's input index (sval16).  In LDS: the site of every rank (a byte,
+// 50 KB at 50,001 nodes: two workgroups a CU); the yarn is written straight
+// from a wave-level multisplit, each wave's ranks going to 16 runs that grow a
+// chunk at a time.  9 B a node: site 1 + rank 2 + sval 2 in, yarn_perm 4 out
+// (+1 B in the fused kernel for the site byte).  Round 4 placed the yarns
+// inside the fused kernel's front end: +3.9 ms on a config-2 step; round 5:
+// an LDS-staged version there, +3.8 ms; this kernel with per-thread rank
+// ranges and the yarn staged in LDS, 2.60 ms; the multisplit with no staging,
+// 2.37 ms; site bytes instead of ids, 1.76 ms; the input indices loaded eight
+// chunks at a time, 1.47 ms (profiles/r05_yarn_ab.txt).
 __host__ __device__ inline uint32_t yarn_lds_bytes(uint32_t nmax) {
   return (nmax + 3) & ~3u;  // the site of every rank (a byte)
 }
