@@ -12,6 +12,7 @@ mkdir -p $O
 cp profiles/pmc_traffic.json gpurun_out/pmc_traffic.json
 pmc() {  # $1 = dir, $2 = seconds, rest = bench args
   local dir=$1 lim=$2; shift 2
+  mkdir -p "$R/$dir"
   for pass in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 $lim rocprofv3 --kernel-trace --pmc $pass \
       --output-format csv -d "$R/$dir/pmc_$pass" -o run -- \
