@@ -1412,17 +1412,21 @@ __device__ __forceinline__ bool front_doc(
       qd[u] = i < n ? lane_at(kindD, i) : 0;
     }
   };
-  load_group(tid);
+  // (U2 <= 4: the next group's loads go out before this group is ranked;
+  // wider groups load and rank in turn -- double-buffered they spill)
+  constexpr bool PF = U2 <= 4;
+  if (PF) load_group(tid);
   for (uint32_t i0 = tid; i0 < n; i0 += U2 * NT) {
     uint64_t k[U2], c[U2];
     uint8_t kd[U2];
+    if (!PF) load_group(i0);
 #pragma unroll
     for (uint32_t u = 0; u < U2; u++) {
       k[u] = qk[u];
       c[u] = qc[u];
       kd[u] = qd[u];
     }
-    if (i0 + U2 * NT < n) load_group(i0 + U2 * NT);
+    if (PF && i0 + U2 * NT < n) load_group(i0 + U2 * NT);
 #pragma unroll
     for (uint32_t u = 0; u < U2; u++) {
       const uint32_t i = i0 + u * NT;
@@ -3407,8 +3411,10 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
   // (tprof, CW_TREE_PROF: the three phases' clocks per document)
   const unsigned long long t0 = PROF ? __builtin_amdgcn_s_memtime() : 0ull;
   // FV (CW_FRONT_U): items in flight per thread in the front end's directory
-  // and input-index passes (1: 16, 0: 4 as in k_front)
-  constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 4, U3 = U1;
+  // and input-index passes (1: 16, 0: 4 as in k_front); the rank pass loads
+  // and ranks 6 items a thread in turn (round 5: 4 double-buffered, 12.17 ->
+  // 12.11 ms a config-2 step; 8 spill)
+  constexpr uint32_t U1 = FV == 0 ? 4 : 16, U2 = 6, U3 = U1;
   if (!front_doc<NT, uint16_t, VT, U1, U2, U3>(id_key, cause_key, kind, doc_off, tile_first, sg, par, skind, sval, kbm, skey,
                      rank16, max_ts, ts_shift, status, big, nullptr, d,
                      reinterpret_cast<uint4 *>(lds_w), site8, site_shift, site_mask))
