@@ -965,6 +965,7 @@ __global__ __launch_bounds__(256) void k_x2_chain(
   }
 }
 
+constexpr uint32_t X2_JUMPS = 3;
 __global__ __launch_bounds__(256) void k_x2_jump(
     const uint32_t *__restrict__ tile_start, const uint32_t *__restrict__ tile_doc,
     const uint32_t *__restrict__ doc_off, const uint32_t *__restrict__ sbase2,
@@ -972,10 +973,17 @@ __global__ __launch_bounds__(256) void k_x2_jump(
   const uint32_t t = blockIdx.x, f = tile_doc[t];
   if (sbase2[f] == X_NONE || !only[f]) return;
   const uint32_t base = doc_off[f];
+  // X2_JUMPS jumps a launch: each one at least adds the reach every node had
+  // when the launch began, so a launch multiplies it by X2_JUMPS + 1 (the
+  // host launches ceil(log_{X2_JUMPS+1} n) + 1 of them)
   for (uint32_t i = tile_start[t] + threadIdx.x; i < tile_start[t + 1]; i += blockDim.x) {
-    const uint32_t j = __hip_atomic_load(&jmp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t k = __hip_atomic_load(&jmp[base + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k != j) __hip_atomic_store(&jmp[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t j = __hip_atomic_load(&jmp[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t q = 0; q < X2_JUMPS; q++) {
+      const uint32_t k = __hip_atomic_load(&jmp[base + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == j) break;
+      __hip_atomic_store(&jmp[i], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      j = k;
+    }
   }
 }
 
@@ -1472,7 +1480,9 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
         return check_launch(c, "xsyn_pos");
       };
       if (positions2(1, p2A, nullptr)) return -1;
-      const uint32_t jumps = ceil_log2(nmax) + 1;
+      // launches of k_x2_jump: reach (X2_JUMPS + 1)^launches >= nmax
+      uint32_t jumps = 1;
+      for (uint64_t reach = 1; reach < nmax; reach *= X2_JUMPS + 1) jumps++;
       std::vector<uint8_t> only(x2), h_moved(F);
       for (uint32_t round = 0;; round++) {
         XMinTree mt, mtn;
