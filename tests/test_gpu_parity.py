@@ -159,6 +159,16 @@ def test_generated_config2_shape(weaver):
     check_batch(weaver, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF)
 
 
+def test_yarns_every_site_value(weaver):
+    """k_yarn_doc's multisplit over the widest site field it takes (4 bits:
+    the root's site 0 and sites 1..15, every one of the 16 classes in use),
+    documents of the fused weave's sizes, yarn_perm against the oracle."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=20_000, n_sites=15, seed=77)
+    assert spec.layout().site_bits == 4
+    off, idk, ck, kd = gen.generate(spec, 0, 24)
+    check_batch(weaver, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF)
+
+
 def test_generated_mixed_sizes(weaver):
     """Documents spanning many sort tiles and many splitter blocks, plus
     tiny ones, in one batch."""
