@@ -5197,9 +5197,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       const uint32_t tl_lds = tree_l_lds_bytes(t.nmax) + tree_l_tile_bytes(1024, 2048);
       const uint32_t to_lds = tour_lds_bytes(t.nmax, t.tour_log2k);
       const uint32_t wd_lds = std::max(fr_lds, std::max(tl_lds, to_lds));
-      // (the fused kernel is built for the tree variants 0 and 4 only: another
-      // CW_TL_MODE runs the separate kernels, so the knob means the same thing
-      // on both paths; CW_TREE_PROF runs variant 4)
+      // (the fused kernel needs k_tree_l's 2,048-rank tiles: CW_TREE_L = 0 or
+      // 1024 run the separate kernels)
       fused_done = c->fused && t.tour && !giant1 && c->tree_l == 2048 &&
                    tl_lds + 64 * 4 + 4 <= c->lds_max &&
                    wd_lds + 1024 <= c->lds_max && to_lds <= TOUR_LDS_MAX;

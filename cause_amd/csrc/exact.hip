@@ -55,16 +55,19 @@
 //
 // Phase 2 -- documents with an early node.  The fold is the preorder of its
 // insertion tree: each node's parent is the node right before its insertion
-// point at its time, children by descending id.  From any weave W, k_xpred
-// finds every node's insertion point in W restricted to the older nodes (the
-// scan above, with searches in min-trees), the insertion tree is woven (all
-// classes normal: a plain preorder), and the rounds repeat until the weave no
-// longer changes.  A weave that reproduces itself is the fold's (by induction
-// over the nodes in id order), and each round fixes at least the oldest
-// misplaced node; from phase 1's weave a few rounds suffice (the appended
-// nodes after round 1 use the region rule above on the insertion tree, where
-// a subtree ends at the first older node).  Render bits then come from the
-// weave itself (hide? against the next node).
+// point at its time, children by descending id.  From any weave W each node's
+// insertion split in W restricted to the older nodes is found with min-tree
+// searches (k_x2_xf, k_x2_anchor), named AFTER a node or BEFORE the older
+// child woven first (which does not move from round to round); BEFORE anchors
+// form chains that pointer jumping takes down to their AFTER-anchored bottom
+// (k_x2_chain, k_x2_jump), and the insertion tree is woven on layout 2 (2n + 1
+// slots: rank r at 2r + 2, its placeholder at 2r + 1, which holds a bottom's
+// BEFORE chain; k_x2_build).  The rounds repeat until the weave reproduces
+// itself -- that weave is the fold's (by induction over the nodes in id
+// order) -- and chains of early nodes settle in O(log n) rounds.  A document
+// of <= 4,096 nodes still moving after X_ROUND_CAP rounds takes the serial
+// fold.  Render bits then come from the weave itself (hide? against the next
+// node).  DESIGN.md 5f.
 //
 // The literal fold on one lane per document (k_xfold, ~1 us a node) is kept
 // as a cross-check behind CW_XFOLD=1.
