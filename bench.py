@@ -184,6 +184,19 @@ class heartbeat:
         self.t.join()
 
 
+def b_io_bytes(key_bytes, perm_bytes):
+    """SURVEY 8(d)'s algorithmic bytes per node of the weave: id + cause keys
+    and the kind byte in, weave_perm and one visible bit out."""
+    return key_bytes + key_bytes + 1 + perm_bytes + 1 / 8
+
+
+def achieved_gbs(bytes_per_launch, launches, ms_total):
+    """GB/s of a kernel over the timed steps: its bytes per launch times the
+    launches, over the summed launch time (launches and ms both over ALL the
+    timed steps, as cw_get_kernel_stats reports them)."""
+    return bytes_per_launch * launches / (ms_total / 1e3) / 1e9 if ms_total > 0 else 0.0
+
+
 def pmc_traffic(kernel, workload, default_size):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, scripts/pmc_traffic.py: FETCH_SIZE doubled per
@@ -636,10 +649,9 @@ def main_stream(a, world, rank, local, dist, torch, dev):
     achieved_kernel = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     # SURVEY 8(d)'s bytes for the fused weave (as config 2): B_io per node of a
     # batch -- ids, causes, kinds in, weave_perm and the visible bit out
-    kw_io, pw_io = (4 if k32 else 8), (2 if perm16 else 4)
-    b_io = kw_io + kw_io + 1 + pw_io + 1 / 8
+    b_io = b_io_bytes(4 if k32 else 8, 2 if perm16 else 4)
     whole = name == "weave"
-    achieved = (B * n * b_io * launches if whole else by) / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    achieved = achieved_gbs(B * n * b_io if whole else by / max(launches, 1), launches, ms)
     # a config-3 batch has the config-2 batch's shape: the same kernels' counters
     traffic, tnote = pmc_traffic(name, "config2", B == 10_000 and a.nodes == 50_000)
     if rank == 0:
@@ -926,10 +938,9 @@ def main():
     # with u32).  The fused per-document kernel does the whole weave, so its
     # algorithmic bytes are B_io x the nodes of a launch; its own scratch
     # handoffs (achieved_kernel_scratch) are not algorithmic bytes.
-    b_io = (4 + 4 + 1 + 4 + 1 / 8) if k32 else (8 + 8 + 1 + 4 + 1 / 8)
+    b_io = b_io_bytes(4 if k32 else 8, 4)
     whole = name == "weave"
-    by_io = N * b_io * launches if whole else by  # (launches and ms: over all timed steps)
-    achieved = by_io / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    achieved = achieved_gbs(N * b_io, launches, ms) if whole else achieved_gbs(by / launches, launches, ms)
     kernel_ms_total = sum(v[1] for v in stats.values())
     # HBM bytes per launch of that kernel from the committed rocprofv3 PMC
     # passes (scripts/pmc_traffic.py; FETCH_SIZE doubled per MI355X_MICROARCH.md)
