@@ -79,6 +79,10 @@ def parse():
     ap.add_argument("--check", action="store_true",
                     help="after timing, every rank compares its outputs with the CPU oracle "
                          "(configs 2, 3 and 4; the JSON line gets a 'check' object)")
+    ap.add_argument("--check-docs", type=int, default=256,
+                    help="without --check: the last timed step's outputs of this many documents "
+                         "(configs 1/2/5; collections for config 4) spread over the batch are "
+                         "compared with the oracle after timing (0: off)")
     return ap.parse_args()
 
 
@@ -132,21 +136,71 @@ def check_lists(off, idk, ck, kd, perm, bits, vcount, status):
     return bad
 
 
-def check_maps(off, idk, ck, ci, kd, o, S):
-    """--check: this rank's config-4 key weaves and active nodes vs the literal
-    c.map/weave fold (oracle/weave_oracle.c): mismatching collections."""
+def sample_docs(D, k):
+    """k document indices spread evenly over [0, D) (all of them if D <= k)."""
+    if D <= k:
+        return np.arange(D, dtype=np.int64)
+    return np.unique(np.linspace(0, D - 1, k).round().astype(np.int64))
+
+
+def snapshot_lists(off, docs, perm, bits, vcount, status):
+    """Device outputs of the sampled documents, copied to the host right after
+    the timed steps (so later untimed calls cannot be what gets checked)."""
+    snap = []
+    for d in docs:
+        lo, hi = int(off[d]), int(off[d + 1])
+        w0, w1 = lo >> 5, (hi + 31) >> 5
+        snap.append((int(d), perm[lo:hi].cpu().numpy().view(np.uint32).copy(),
+                     bits[w0:w1].cpu().numpy().view(np.uint32).copy(),
+                     int(vcount[d].item()), int(status[d].item())))
+    return snap
+
+
+def check_snapshot_lists(off, idk, ck, kd, snap):
+    """The timed step's outputs of the sampled documents vs the oracle
+    (effective-tree preorder + visibility in C, pinned to the literal fold by
+    tests/test_fullsize_literal.py) -> (documents checked, mismatches)."""
+    import oracle
+
+    sizes = [int(off[d + 1] - off[d]) for d, *_ in snap]
+    sub_off = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    sel = np.concatenate([np.arange(int(off[d]), int(off[d + 1])) for d, *_ in snap])
+    want, vis, st = oracle.batch_lists(sub_off, idk[sel], ck[sel], kd[sel],
+                                       method=oracle.METHOD_EFF, nthreads=16)
+    bad = 0
+    for j, (d, gp, gb, gvc, gst) in enumerate(snap):
+        lo, hi = int(off[d]), int(off[d + 1])
+        a, b = int(sub_off[j]), int(sub_off[j + 1])
+        allbits = np.unpackbits(gb.view(np.uint8), bitorder="little")
+        gvis = allbits[lo - ((lo >> 5) << 5):][:hi - lo]
+        ok = (gst == st[j] and np.array_equal(gp, want[a:b]) and
+              np.array_equal(gvis, vis[a:b]) and gvc == int(vis[a:b].sum()))
+        bad += 0 if ok else 1
+    return len(snap), bad
+
+
+def check_maps(off, idk, ck, ci, kd, o, S, colls=None):
+    """This rank's config-4 key weaves and active nodes vs the literal
+    c.map/weave fold (oracle/weave_oracle.c), for every collection or only
+    `colls` -> (mismatching collections, collections checked)."""
     import oracle
 
     h = {k: v.cpu().numpy() for k, v in o.items()}
     so, sc, sk = h["seg_offsets"].view(np.uint64), h["seg_coll"].view(np.uint32), h["seg_key"].view(np.uint64)
     sa, sp, gst = h["seg_active"], h["seg_perm"].view(np.uint32), h["status"].view(np.uint32)
-    got = [dict() for _ in range(len(off) - 1)]
+    D = len(off) - 1
+    todo = range(D) if colls is None else [int(c) for c in colls]
+    want_set = set(todo)
+    got = [dict() for _ in range(D)]
     for s in range(S):
+        c = int(sc[s])
+        if c not in want_set:
+            continue
         kw = sp[int(so[s]):int(so[s + 1])]
-        got[int(sc[s])][int(sk[s])] = (int(sa[s]), kw[1:].tolist() if kw[0] == 0xFFFFFFFF else None)
+        got[c][int(sk[s])] = (int(sa[s]), kw[1:].tolist() if kw[0] == 0xFFFFFFFF else None)
     tok, idk_bit, nil = np.uint64(1 << 63), 1 << 63, (1 << 64) - 1
     bad = 0
-    for d in range(len(off) - 1):
+    for d in todo:
         a, b = int(off[d]), int(off[d + 1])
         c = oracle.map_causes(ck[a:b], ci[a:b])
         nk, npos, skk, saa = oracle.map_weave(idk[a:b], c, ci[a:b], kd[a:b], 0)
@@ -157,7 +211,7 @@ def check_maps(off, idk, ck, ci, kd, o, S):
         api = lambda k: nil if k == nil else (k & ~idk_bit if k & idk_bit else idk_bit | k)
         want = {api(int(k)): (int(act), groups.get(int(k), [])) for k, act in zip(skk, saa)}
         bad += 0 if (gst[d] == 0 and got[d] == want) else 1
-    return bad
+    return bad, len(todo)
 
 
 class heartbeat:
@@ -500,12 +554,18 @@ def main_maps(a, world, rank, local, dist, torch, dev):
     achieved = by / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     traffic, tnote = pmc_traffic(name, "config4", a.colls == 1_000_000)
     check = None
-    if a.check:
+    if a.check or a.check_docs > 0:
+        # --check: every collection; otherwise --check-docs collections spread
+        # over the batch (the last timed step's outputs: nothing ran since)
+        colls = None if a.check else sample_docs(D, a.check_docs)
         with heartbeat("--check against the oracle"):
-            bad = check_maps(off, idk, ck, ci, kd, o, S)
-        tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
+            bad, nchk = check_maps(off, idk, ck, ci, kd, o, S, colls)
+        tot = shard.reduce_sum([bad, nchk], dist, dev) if world > 1 else [bad, nchk]
         check = {"collections_checked": tot[1], "mismatches": tot[0],
-                 "against": "literal c.map/weave fold + active-node (oracle, C)"}
+                 "against": "literal c.map/weave fold + active-node (oracle, C)",
+                 "what": "every collection" if a.check else
+                         f"{a.check_docs} collections spread evenly over each rank's batch, "
+                         f"outputs of the last timed step"}
     if rank == 0:
         # timed after the GPU region, on rank 0 at every N (the other ranks are done)
         cpu = cpu_baseline_maps(spec, a.cpu_seconds) if not a.no_cpu else None
@@ -835,6 +895,17 @@ def main():
     w.set_profiling(False)
     w.set_profile_only(None)
     stats_dom = w.kernel_stats()
+    # parity on the timed path: the last timed step's outputs of --check-docs
+    # documents spread over the batch, copied out now and compared with the
+    # oracle after every GPU measurement (outside the timed region)
+    snap, snap_note = None, None
+    if a.check_docs > 0 and not a.check:
+        if a.config == 5 and N > (1 << 27):
+            snap_note = (f"not checked in the bench: one {N:,}-node list is too large for the "
+                         f"oracle in the bench's budget (tests/test_gpu_giant_full.py checks "
+                         f"2,000,040,001 nodes position by position)")
+        else:
+            snap = snapshot_lists(off, sample_docs(D, a.check_docs), perm, bits, vcount, status)
     # the per-kernel breakdown (information): the same steps with events on
     # every launch
     w.reset_kernel_stats()
@@ -898,7 +969,19 @@ def main():
             bad = check_lists(off, *_k64(idk, ck), kd, perm, bits, vcount, status)
         tot = shard.reduce_sum([bad, D], dist, dev) if world > 1 else [bad, D]
         check = {"documents_checked": tot[1], "mismatches": tot[0],
-                 "against": "effective-tree preorder + visibility (oracle, C)"}
+                 "against": "effective-tree preorder + visibility (oracle, C)",
+                 "what": "every document of the batch, outputs of the last untimed step"}
+    elif snap is not None:
+        with heartbeat("sample check against the oracle"):
+            nchk, bad = check_snapshot_lists(off, *_k64(idk, ck), kd, snap)
+        tot = shard.reduce_sum([bad, nchk], dist, dev) if world > 1 else [bad, nchk]
+        check = {"documents_checked": tot[1], "mismatches": tot[0],
+                 "against": "effective-tree preorder + visibility (oracle, C)",
+                 "what": (f"the last timed step's weave_perm, visible bits, visible_count and "
+                          f"status of {a.check_docs} documents spread evenly over each rank's "
+                          f"batch (fewer if the batch is smaller), copied out after timing")}
+    elif snap_note:
+        check = {"documents_checked": 0, "mismatches": None, "note": snap_note}
 
     # PCIe-inclusive rate (not the headline value): inputs from pinned host
     # buffers, the weave, weave_perm + visible bits back, serialised
@@ -973,7 +1056,7 @@ def main():
                                        else f"docs sharded x{world}")},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "frac_io": achieved / HBM_PEAK_GBS,
+                         "frac_io": achieved / HBM_PEAK_GBS if whole else None,
                          "bytes_alg_per_node": b_io if whole else by / launches / N,
                          "bytes_alg_note": ("B_io (SURVEY 8d): id + cause + kind in, weave_perm + "
                                             "visible bit out, per node of the launch" if whole else

@@ -22,3 +22,35 @@ def test_achieved_counts_every_launch():
     assert gbs == pytest.approx(n * b / 12e-3 / 1e9)
     assert gbs / bench.HBM_PEAK_GBS == pytest.approx(0.11, abs=0.005)
     assert bench.achieved_gbs(1.0, 3, 0.0) == 0.0
+
+
+def test_sample_check_catches_a_wrong_document():
+    """The bench line's parity check on the timed path (check_snapshot_lists):
+    zero mismatches on the oracle's own outputs laid out as the device writes
+    them (doc-local weave_perm, one batch-wide render bitmap), one mismatch
+    when a sampled document's order is disturbed."""
+    import dataclasses
+
+    import numpy as np
+    import torch
+
+    import oracle
+    from cause_amd import gen
+
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=700)
+    off, idk, ck, kd = gen.generate(spec, 0, 9, nthreads=2)
+    perm, vis, st = oracle.batch_lists(off, idk, ck, kd, method=oracle.METHOD_EFF)
+    N, D = len(idk), len(off) - 1
+    bits = np.packbits(np.concatenate([vis, np.zeros((-N) % 32, np.uint8)]), bitorder="little")
+    t_perm = torch.from_numpy(perm.view(np.int32).copy())
+    t_bits = torch.from_numpy(bits.view(np.int32).copy())
+    vc = np.array([vis[int(off[d]):int(off[d + 1])].sum() for d in range(D)], np.int32)
+    t_vc, t_st = torch.from_numpy(vc), torch.from_numpy(st.view(np.int32).copy())
+    docs = bench.sample_docs(D, 4)
+    assert list(docs) == [0, 3, 5, 8]
+    snap = bench.snapshot_lists(off, docs, t_perm, t_bits, t_vc, t_st)
+    assert bench.check_snapshot_lists(off, idk, ck, kd, snap) == (4, 0)
+    lo = int(off[5])
+    t_perm[lo + 1], t_perm[lo + 2] = t_perm[lo + 2].clone(), t_perm[lo + 1].clone()
+    snap = bench.snapshot_lists(off, docs, t_perm, t_bits, t_vc, t_st)
+    assert bench.check_snapshot_lists(off, idk, ck, kd, snap) == (4, 1)
