@@ -96,8 +96,23 @@ const char *cw_last_error(const cw_ctx *ctx);
 /* Launch on an existing HIP stream (hipStream_t passed as void*); NULL restores
  * the context's own stream. */
 int cw_ctx_set_stream(cw_ctx *ctx, void *hip_stream);
-/* 0: synchronous calls (default).  1: device-memory calls return right after
- * enqueueing (the caller synchronises the stream). */
+/* 0: synchronous calls (default).  1: device-memory calls return without a
+ * final stream synchronisation (the caller synchronises the stream before it
+ * reads the results).  They are NOT fully asynchronous: a call may wait on the
+ * stream for a few bytes the host needs to pick the next kernels.
+ *  - cw_weave_lists / _k32 (batches of documents < 2^16 nodes, the fused
+ *    per-document kernel): one blocking 8-byte readback right after that
+ *    kernel -- whether a document's ids left its rank directory (the batch is
+ *    then rewoven by the separate kernels) and whether the exact path has
+ *    documents to fix.  The call returns while the yarn kernel (yarn_perm) and
+ *    any later kernel still run; work queued on the stream BEFORE the call
+ *    is waited for too.
+ *  - the other front ends wait likewise once for their 8-byte directory
+ *    flag; one giant document (>= 2^22 nodes) waits for its 4-byte status.
+ *  - cw_weave_maps, cw_partition_keys and the out-of-domain (exact) path read
+ *    back counts they size later launches with.
+ * A caller that wants to overlap host work with the weave should run it on
+ * its own thread or queue the weave behind no other work. */
 int cw_ctx_set_async(cw_ctx *ctx, int async);
 /* Per-kernel timing with HIP events on the launch stream (event pairs are read
  * back when the stats are asked for; asynchronous calls stay asynchronous). */
