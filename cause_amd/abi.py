@@ -185,6 +185,8 @@ def lib():
         L.cw_ctx_set_profile_only.argtypes = [C.c_void_p, C.c_char_p]
         L.cw_get_kernel_stats.argtypes = [C.c_void_p, C.POINTER(CwKernelStat), C.c_int]
         L.cw_reset_kernel_stats.argtypes = [C.c_void_p]
+        L.cw_get_counter.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint64)]
+        L.cw_get_counter.restype = C.c_int
         L.cw_weave_lists.argtypes = [C.c_void_p, C.POINTER(CwListBatch), C.POINTER(CwListResult),
                                      C.c_int]
         L.cw_weave_lists.restype = C.c_int
@@ -331,6 +333,13 @@ class Weaver:
 
     def reset_kernel_stats(self):
         self._L.cw_reset_kernel_stats(self._h)
+
+    def counter(self, name: str) -> int:
+        """A diagnostic counter of the last call (cw_get_counter; waits for the
+        stream): "continued_sublists" = walk-slot overflows of the last HBM walk."""
+        v = C.c_uint64(0)
+        self._check(self._L.cw_get_counter(self._h, name.encode(), C.byref(v)), "get_counter")
+        return int(v.value)
 
     @staticmethod
     def _batch(offsets, id_ptr, cause_ptr, kind_ptr, layout, key_bits=None):

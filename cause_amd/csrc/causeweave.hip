@@ -4309,8 +4309,12 @@ struct cw_ctx {
   uint32_t giant_log2k = 4;        // CW_GIANT_LOG2K: least splitter block of a giant document
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
+  const uint32_t *last_dyn = nullptr;  // the last HBM walk's continued-sublist counters
+  uint32_t last_dyn_n = 0;             // ... (one per document of that walk)
   uint32_t x_iters = 0;            // synthetic-list weaves of the last exact path (exact.hip)
   uint32_t xfold = 0;              // CW_XFOLD: documents with an early node take the serial fold
+  uint32_t x_round_cap = 48;       // CW_X_ROUND_CAP: anchor rounds before a small still-moving
+                                   // document takes the serial fold (exact.hip X_ROUND_CAP)
   uint32_t *pin_status = nullptr;  // pinned: a giant document's status, copied after the front end
   hipEvent_t ev_status = nullptr;  // ... and recorded there (exact.hip waits on it, not the stream)
   bool x_pending = false;          // pin_status / ev_status hold this call's giant document
@@ -4512,8 +4516,18 @@ void build_tables(cw_ctx *c, uint64_t D, const uint64_t *off, bool giant) {
     // L2 misses and HBM bytes a node, twice the continuation sublists;
     // DESIGN 5e).  (CW_GIANT_LOG2CAP: the tests shrink it to send walks
     // through many continuation sublists)
-    if (giant && (n < (1u << 30) || (uint64_t)n * GIANT_CAP32_BYTES <= c->hbm_total))
-      log2cap = std::max(log2cap, c->giant_log2cap);
+    // (the knob sets the giant slot size itself, also below min_log2cap)
+    // The test is against the device memory free at this call plus the
+    // scratch this context already holds (it is reused), not the device's
+    // total: a shared device or large caller buffers keep 16-entry slots.
+    bool cap32 = giant && n < (1u << 30);
+    if (giant && !cap32) {
+      size_t fr = 0, tot = 0;
+      uint64_t held = 0;
+      for (auto &kv : c->bufs) held += kv.second.bytes;
+      if (hipMemGetInfo(&fr, &tot) == hipSuccess) cap32 = (uint64_t)n * GIANT_CAP32_BYTES <= fr + held;
+    }
+    if (cap32) log2cap = c->giant_log2cap;
     // and 16-node splitter blocks: half the sublists to rank for a slightly
     // longer walk (15.68 -> 15.17 ms a step at 6.7e7 nodes; 32 nodes: 16.8),
     // once there are walkers enough to fill the chip (config 1's 10^5 nodes:
@@ -4995,6 +5009,8 @@ int weave_tail(cw_ctx *c, uint64_t D, uint32_t N, bool giant, const uint32_t *pa
   } else {
     // 6. walk: sublists of the preorder successor list
     if (!(giant && !linked)) HIPCHK(c, hipMemsetAsync(dyn_ctr, 0, D * 4, c->stream));  // (k_geff did)
+    c->last_dyn = dyn_ctr;  // (cw_get_counter "continued_sublists")
+    c->last_dyn_n = (uint32_t)D;
     unsigned long long *wprof = nullptr;
     if (c->tree_prof && giant) {
       wprof = scratch_t<unsigned long long>(c, "wprof", 4);
@@ -6778,6 +6794,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->giant_log2cap = std::max(2u, std::min(knob("CW_GIANT_LOG2CAP", 5), 12u));
   c->fused = knob("CW_FUSED", 1);
   c->xfold = knob("CW_XFOLD", 0);
+  c->x_round_cap = std::max(1u, knob("CW_X_ROUND_CAP", 48));
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;
@@ -7031,6 +7048,19 @@ int cw_weave_linked(cw_ctx *c, const cw_linked_list *l, cw_list_result *r) {
   if (!c) return -1;
   c->err.clear();
   return weave_linked_impl(c, l, r);
+}
+
+int cw_get_counter(cw_ctx *c, const char *name, uint64_t *value) {
+  if (!c || !name || !value) return -1;
+  if (strcmp(name, "continued_sublists") != 0) return fail(c, "unknown counter %s", name);
+  *value = 0;
+  if (!c->last_dyn || !c->last_dyn_n) return 0;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::vector<uint32_t> h(c->last_dyn_n);
+  HIPCHK(c, hipMemcpy(h.data(), c->last_dyn, h.size() * 4, hipMemcpyDeviceToHost));
+  for (uint32_t v : h) *value += v;
+  return 0;
 }
 
 int cw_reset_kernel_stats(cw_ctx *c) {

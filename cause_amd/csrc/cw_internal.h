@@ -26,9 +26,11 @@ constexpr int JOIN_ITEMS = 4;
 constexpr uint32_t MAX_SUBLISTS = 16384;          // rank: 128 KiB of LDS
 constexpr uint32_t CHAIN = 64;                     // rank: sublists per LDS chain head
 constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter block
-// One giant document takes 32-entry walk slots when n * this many bytes fits the
-// device (its whole footprint is ~100 B a node with them).
-constexpr uint64_t GIANT_CAP32_BYTES = 128;
+// One giant document takes 32-entry walk slots when n * this many bytes of
+// device memory are free (plus the context's own reusable scratch) at the
+// call: the library's scratch with them is ~92 B a node (2e9 nodes: 218 GiB
+// in use with the caller's 21 B a node of inputs and outputs).
+constexpr uint64_t GIANT_CAP32_BYTES = 100;
 
 // link word (u32): low 29 bits = the node's preorder successor (SUCC_END for the
 // last node), bit 31 = the node renders, bit 30 = the node is a splitter, bit

@@ -803,6 +803,7 @@ __global__ __launch_bounds__(256) void k_xsyn_final(
 
 constexpr uint32_t XB_BIT = 0x80000000u;  // anchor word: BEFORE rank (low bits), else AFTER slot
 constexpr uint32_t X_ROUND_CAP = 48;     // rounds before a small still-moving document is folded
+                                         // (the default of cw_ctx::x_round_cap, CW_X_ROUND_CAP)
 constexpr uint32_t X_CAP_FOLD_MAX = 4096;  // ... serially (k_xfold: ~n^2 steps at worst)
 
 // Positions of a layout-2 weave.  from1: round 0's W is phase 1's weave
@@ -1541,7 +1542,7 @@ int exact_weave_flagged(cw_ctx *c, uint32_t F, const std::vector<uint64_t> &xoff
         bool more = false;
         for (uint32_t f = 0; f < F; f++) {
           only[f] = only[f] && h_moved[f];  // a document that reproduced its weave is done
-          if (only[f] && round + 1 >= X_ROUND_CAP && xoff[f + 1] - xoff[f] <= X_CAP_FOLD_MAX) {
+          if (only[f] && round + 1 >= c->x_round_cap && xoff[f + 1] - xoff[f] <= X_CAP_FOLD_MAX) {
             only[f] = 0;  // small and still moving: the serial fold (emitted after the synthetic lists)
             run[f] = 1;
             any_serial = true;

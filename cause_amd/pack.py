@@ -217,7 +217,8 @@ def pack_maps(docs) -> PackedMaps:
     so does a cause naming it; every other id packs by its site's rank in
     String.compareTo order, which may put site-ids such as " a " before "0"
     (list_test.cljc:85-96): an id with ts >= 1 still packs above 0, and only an
-    id that itself sorts before the root id (ts 0) is refused."""
+    id -- a node's or an id cause -- that itself sorts before the root id (ts 0)
+    is refused (it would pack onto the root id)."""
     docs = [list(d) for d in docs]
     lay = layout_for([[(n[0], n[1] if valid_id(n[1]) else None, n[2]) for n in d]
                       + [((0, "0", 0), None, None)] for d in docs])
@@ -238,6 +239,10 @@ def pack_maps(docs) -> PackedMaps:
                 raise KeyRangeError(f"map node id {nid} sorts before the root id")
             idk[j] = pk(nid)
             if valid_id(cause):
+                # a cause id [0 s tx] with s before "0" would pack onto the root
+                # id (or out of order): refused like such a node id
+                if cause[0] == 0 and java_str_key(cause[1]) < java_str_key("0"):
+                    raise KeyRangeError(f"map cause id {cause} sorts before the root id")
                 ck[j] = pk(cause)
                 ci[j] = 1
             elif cause is None:  # the nil key (cause_is_id = 2, include/causeweave.h)

@@ -132,6 +132,11 @@ typedef struct {
 /* Copies up to `cap` stats; returns how many kernels have stats. */
 int cw_get_kernel_stats(const cw_ctx *ctx, cw_kernel_stat *out, int cap);
 int cw_reset_kernel_stats(cw_ctx *ctx);
+/* Diagnostic counter of the last call on this context (waits for the stream):
+ * "continued_sublists" = sublists the last HBM walk (one-list / giant path)
+ * opened because a walker's slot filled up.  0 on success, < 0 for an
+ * unknown name. */
+int cw_get_counter(cw_ctx *ctx, const char *name, uint64_t *value);
 
 /* ---------------------------------------------------------------- lists ---- */
 typedef struct {

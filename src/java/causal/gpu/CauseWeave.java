@@ -301,12 +301,18 @@ public final class CauseWeave implements AutoCloseable {
       String[] r = internSites(withRoot);
       // site-ids may sort before "0" (String.compareTo, e.g. " a ", list_test.cljc:85-96):
       // the virtual root [0 "0" 0] still packs to 0 and so does a cause naming it; an
-      // id with ts >= 1 packs above 0 whatever its site's rank.  Only a node id that
-      // itself sorts before the root id (ts 0) is refused -- as cause_amd/pack.py does.
-      for (Node n : d)
+      // id with ts >= 1 packs above 0 whatever its site's rank.  Only an id (a node's or
+      // an id cause) that itself sorts before the root id (ts 0) is refused -- as
+      // cause_amd/pack.py does.
+      for (Node n : d) {
         if (n.ts == 0 && n.site.compareTo("0") < 0)
           throw new IllegalArgumentException("map node id [0 \"" + n.site + "\" " + n.tx
               + "] sorts before the root id");
+        // an id cause [0 s tx] with s before "0" would pack onto the root id
+        if (n.causeKind == 0 && n.cts == 0 && n.csite.compareTo("0") < 0)
+          throw new IllegalArgumentException("map cause id [0 \"" + n.csite + "\" " + n.ctx
+              + "] sorts before the root id");
+      }
       ranks.add(r);
       msite = Math.max(msite, r.length - 1);
       for (Node n : d) {

@@ -348,6 +348,29 @@ def test_chain_families_few_rounds():
     assert res.status[3] == 0 and (res.status[[0, 1, 2, 4, 5, 6, 7]] & abi.STATUS_NON_LAMPORT).all()
 
 
+def test_round_cap_hands_still_moving_documents_to_the_serial_fold(monkeypatch):
+    """a small document still moving after the anchor-round cap
+    leaves layout 2 for the serial literal fold (only -> run, any_serial; it
+    is emitted with the synthetic lists, then overwritten by k_xfold).  With
+    the cap at one round (CW_X_ROUND_CAP) every chain family takes that
+    handoff: k_xfold runs and the batch is bit-exact against the literal fold,
+    the clean neighbour included."""
+    from tests import exact_model as M
+
+    monkeypatch.setenv("CW_X_ROUND_CAP", "1")
+    n = 1500
+    docs = [M.chain_doc(f, n, random.Random(k)) for k, f in enumerate(M.CHAIN_FAMILIES)]
+    docs.insert(2, M.random_doc(random.Random(9), n))
+    off, idk, ck, kd, lay = _rank_docs(docs)
+    with abi.Weaver(0) as w:
+        w.reset_kernel_stats()
+        w.set_profiling(True)
+        res = check_batch(w, off, idk, ck, kd, lay, method=oracle.METHOD_LITERAL)
+        w.set_profiling(False)
+        assert "xfold" in w.kernel_stats()
+    assert res.status[2] == 0
+
+
 def _with_reverse_chain(off, idk, ck, a, L):
     """Ranks [a, a + L) of the one document: rank r caused by rank r + 1 (the
     last keeps its cause) -- a reverse chain of L early nodes."""

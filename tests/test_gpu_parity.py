@@ -486,18 +486,30 @@ def test_giant_path_splitter_blocks(log2k, monkeypatch):
 
 
 def test_giant_path_many_continuation_sublists(monkeypatch):
-    """4-entry walk slots (CW_GIANT_LOG2CAP = 2): every walk goes
-    on through several continuation sublists, so the first ranking level's
+    """4-entry walk slots (CW_GIANT_LOG2CAP = 2, which sets the giant slot
+    size itself, below the library's 16-entry minimum): every walk goes on
+    through several continuation sublists, so the first ranking level's
     walkers pass more sublists than their 32-entry slots hold and the rest
-    take the overflow path (pos + the overflow list)."""
+    take the overflow path (pos + the overflow list).  The walk's
+    continued-sublist counter proves the overflows happened."""
     monkeypatch.setenv("CW_GIANT_MIN", "0")
     monkeypatch.setenv("CW_GIANT_LOG2CAP", "2")
     with abi.Weaver(0) as w:
         spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 1000)
         off, idk, ck, kd = gen.generate(spec, 0, 1)
         check_batch(w, off, idk, ck, kd, spec.layout(), method=oracle.METHOD_EFF, yarns=False)
+        cont = w.counter("continued_sublists")
+        # 16-node splitter blocks in 4-entry slots: most sublists continue
+        assert cont > len(idk) // 16, cont
         off, idk, ck, kd = gen.generate(gen.CONFIG1, 0, 1)
         check_batch(w, off, idk, ck, kd, gen.CONFIG1.layout(), method=oracle.METHOD_LINKED)
+        assert w.counter("continued_sublists") > 0
+    monkeypatch.setenv("CW_GIANT_LOG2CAP", "5")
+    with abi.Weaver(0) as w:  # the default 32-entry slots overflow far less often
+        spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=(1 << 22) + 1000)
+        off, idk, ck, kd = gen.generate(spec, 0, 1)
+        w.weave_lists(off, idk, ck, kd, spec.layout())
+        assert w.counter("continued_sublists") < cont // 4
 
 
 def test_few_large_documents_per_document_giant_path():

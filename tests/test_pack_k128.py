@@ -65,3 +65,15 @@ def test_map_packing_takes_sites_before_zero():
     assert [nodes[j][0] for j in order] == sorted((n[0] for n in nodes), key=R.id_key)
     with pytest.raises(pack.KeyRangeError):
         pack.pack_maps([[((0, " a ", 0), "k", "x")]])
+
+
+def test_map_cause_id_before_the_root_is_refused():
+    """An id cause [0 s tx] whose site sorts before "0" would pack onto the
+    root id 0 (and a cause naming it would weave under the root): refused like
+    a node id that sorts before the root."""
+    site = "-" * 13  # a valid ::s/id site (13 chars) that sorts before "0"
+    with pytest.raises(pack.KeyRangeError):
+        pack.pack_maps([[((1, "0", 0), (0, site, 0), "x")]])
+    # the same site with ts >= 1 packs above the root
+    pm = pack.pack_maps([[((1, site, 0), "k", "x"), ((2, "0", 0), (1, site, 0), R.HIDE)]])
+    assert pm.cause[1] > 0 and pm.cause_is_id[1] == 1
