@@ -13,7 +13,7 @@ GENLIB  := cause_amd/libcauseweave_gen.so
 ORACLE  := oracle/liboracle.so
 
 HIP_SRC := cause_amd/csrc/causeweave.hip
-HIP_HDR := include/causeweave.h cause_amd/csrc/cw_internal.h cause_amd/csrc/exact.hip cause_amd/csrc/k128.hip cause_amd/csrc/mappack.hip cause_amd/csrc/dist.hip
+HIP_HDR := include/causeweave.h cause_amd/csrc/cw_internal.h cause_amd/csrc/exact.hip cause_amd/csrc/k128.hip cause_amd/csrc/mappack.hip cause_amd/csrc/dist.hip cause_amd/csrc/onesweep.hip
 
 all: $(LIB) $(GENLIB) $(ORACLE)
 

@@ -4309,6 +4309,13 @@ struct cw_ctx {
   uint32_t giant_log2k = 4;        // CW_GIANT_LOG2K: least splitter block of a giant document
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
+  uint32_t onesweep = 1;           // CW_ONESWEEP: one-array sorts by the one-sweep passes
+                                   // (1: 4,096-key tiles of 512 threads, 2: 8,192 of 1,024,
+                                   // 3: 8,192 of 512; 0: histogram-scan-scatter)
+  uint32_t onesweep_min = 1u << 16;  // CW_ONESWEEP_MIN: ... for arrays of at least this many keys
+  const void *os_lb = nullptr;     // onesweep.hip's look-back words: buffer, size, last epoch
+  size_t os_lb_words = 0;
+  uint32_t os_epoch = 0;
   const uint32_t *last_dyn = nullptr;  // the last HBM walk's continued-sublist counters
   uint32_t last_dyn_n = 0;             // ... (one per document of that walk)
   uint32_t x_iters = 0;            // synthetic-list weaves of the last exact path (exact.hip)
@@ -4640,6 +4647,89 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 // <= MAX_DIGIT bits (at least one pass).  Pass 0 reads (kin, vin) -- vin ==
 // nullptr means identity values -- and the passes ping-pong between (kA,vA)
 // and (kB,vB).
+#include "onesweep.hip"
+
+// One array (one document, or rt's one list): the one-sweep passes
+// (onesweep.hip) -- one histogram launch for every pass, one scan launch, one
+// launch a pass.  Same contract as radix_sort.
+template <typename K>
+int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA, uint32_t *vA,
+                  K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N, K **kout,
+                  uint32_t **vout, uint32_t *inv, uint32_t *vfinal) {
+  const uint32_t geom = c->onesweep;  // 1: 512 x 8, 2: 1024 x 8, 3: 512 x 16 keys a tile
+  const uint32_t TS = geom == 1 ? 4096 : 8192;
+  OsDigits dg{};
+  dg.passes = (bits + OS_MAX_BITS - 1) / OS_MAX_BITS;
+  if (dg.passes > OS_MAX_PASSES) return fail(c, "onesweep: %u key bits", bits);
+  for (uint32_t p = 0, sh = shift0; p < dg.passes; p++) {
+    // the wider digits last, as radix_sort
+    dg.bits[p] = bits / dg.passes + (p >= dg.passes - bits % dg.passes ? 1u : 0u);
+    dg.shift[p] = sh;
+    sh += dg.bits[p];
+  }
+  const uint32_t T = (N + TS - 1) / TS;
+  const size_t hist_words = (size_t)OS_MAX_PASSES * OS_MAX_BINS;
+  uint32_t *hist = scratch_t<uint32_t>(c, "os_hist", 2 * hist_words);
+  const size_t lb_words = (size_t)T * OS_MAX_BINS;
+  unsigned long long *lb = scratch_t<unsigned long long>(c, "os_lb", lb_words);
+  if (!hist || !lb) return fail(c, "out of device memory (onesweep)");
+  uint32_t *base = hist + hist_words;
+  // look-back words: cleared when the buffer is new or the 16-bit epoch wraps
+  if (lb != c->os_lb || lb_words > c->os_lb_words || c->os_epoch + dg.passes > 0xFFFFu) {
+    HIPCHK(c, hipMemsetAsync(lb, 0, c->bufs["os_lb"].bytes, c->stream));
+    c->os_lb = lb;
+    c->os_lb_words = c->bufs["os_lb"].bytes / 8;
+    c->os_epoch = 0;
+  }
+  HIPCHK(c, hipMemsetAsync(hist, 0, hist_words * 4, c->stream));
+  char nm[48];
+  snprintf(nm, sizeof nm, "%s_hist", tag);
+  {
+    Launch L(c, nm, (double)N * sizeof(K));
+    const uint32_t span = 256 * OS_HIST_ITEMS;
+    hipLaunchKernelGGL(k_os_hist<K>, dim3((N + span - 1) / span), dim3(256),
+                       (size_t)4 * dg.passes * OS_MAX_BINS * 4, c->stream, kin, N, dg, hist);
+  }
+  if (check_launch(c, nm)) return -1;
+  snprintf(nm, sizeof nm, "%s_scan", tag);
+  {
+    Launch L(c, nm, (double)dg.passes * OS_MAX_BINS * 8);
+    hipLaunchKernelGGL(k_os_scan, dim3(dg.passes), dim3(OS_MAX_BINS), 0, c->stream, hist, dg, base);
+  }
+  if (check_launch(c, nm)) return -1;
+  const K *ki = kin;
+  const uint32_t *vi = vin;
+  K *ko = kA;
+  uint32_t *vo = vA;
+  snprintf(nm, sizeof nm, "%s_scatter", tag);
+  for (uint32_t p = 0; p < dg.passes; p++) {
+    const bool last = p + 1 == dg.passes;
+    if (last && vfinal) {
+      ko = nullptr;
+      vo = vfinal;
+    }
+    const uint32_t ep = ++c->os_epoch;
+    {
+      Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)));
+      auto launch = [&](auto kern, uint32_t nt) {
+        hipLaunchKernelGGL(kern, dim3(T), dim3(nt), 0, c->stream, ki, vi, ko, vo, last ? inv : nullptr,
+                           N, dg.shift[p], dg.bits[p], base + (size_t)p * OS_MAX_BINS, lb, ep);
+      };
+      if (geom == 1) launch(k_os_pass<K, 512, 8>, 512);
+      else if (geom == 2) launch(k_os_pass<K, 1024, 8>, 1024);
+      else launch(k_os_pass<K, 512, 16>, 512);
+    }
+    if (check_launch(c, nm)) return -1;
+    ki = ko;
+    vi = vo;
+    ko = (ko == kA) ? kB : kA;
+    vo = (vo == vA) ? vB : vA;
+  }
+  *kout = const_cast<K *>(ki);
+  *vout = const_cast<uint32_t *>(vi);
+  return 0;
+}
+
 // rt: the tiles of another array than the batch's (one device-sized list, the
 // giant tree's cross-tile children), instead of c->tab's
 struct RSTab {
@@ -4675,6 +4765,10 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
     *vout = vA;
     return 0;
   }
+  // one array (config 5's ids, the giant tree's cross-tile children): the
+  // one-sweep passes (CW_ONESWEEP; 0 = the histogram-scan-scatter passes below)
+  if (c->onesweep && tt.D == 1 && N >= c->onesweep_min)
+    return onesweep_sort<K>(c, tag, kin, vin, kA, vA, kB, vB, bits, shift0, N, kout, vout, inv, vfinal);
   const uint32_t maxd = std::min<uint32_t>(c->max_digit, MAX_DIGIT);
   const int passes = (int)((bits + maxd - 1) / maxd);
   uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)tt.T * (1u << ((bits + passes - 1) / passes)));
@@ -5341,7 +5435,9 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         skey = want_yarns ? skA : nullptr;
         sval = svA;
         {
-          Launch L(c, "gplace", (double)N * (8 + 8 + 1 + 4 + 1 + 4 + (skey ? 8 : 0)) + (double)N * 2 * 64);
+          // (SURVEY 8d's bytes: ids, causes and kinds in, par, kind, sval (and keys)
+          // out -- not the directory lines each lookup touches: those are traffic)
+          Launch L(c, "gplace", (double)N * (8 + 8 + 1 + 4 + 1 + 4 + (skey ? 8 : 0)));
           hipLaunchKernelGGL(k_gd_place, GN, dim3(256), 0, c->stream, id_key, cause_key, kind, N,
                              reinterpret_cast<const uint4 *>(dir), maxid, bt->ts_shift, out->max_ts,
                              par, skind, sval, skey, out->status);
@@ -5431,7 +5527,10 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
         hipLaunchKernelGGL(k_gpack, dim3((N + 255) / 256), B256, 0, c->stream, cause_key, kind, N, ckk);
       }
       {
-        Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1) + (double)N * 64);
+        // SURVEY 8d's join bytes (the cause read, the parent rank written) plus
+        // the sorted position's input index and kind: not the directory line a
+        // lookup touches (round 5 counted N x 64 of those as algorithmic)
+        Launch L(c, "join", (double)N * (4 + 8 + 8 + 1 + 4 + 1));
         hipLaunchKernelGGL(k_gjoin, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
                            c->stream, skey, sval, cause_key, kind, N, ckk,
                            reinterpret_cast<const uint4 *>(gdir), E, par, skind, out->status);
@@ -6795,6 +6894,8 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->fused = knob("CW_FUSED", 1);
   c->xfold = knob("CW_XFOLD", 0);
   c->x_round_cap = std::max(1u, knob("CW_X_ROUND_CAP", 48));
+  c->onesweep = std::min(knob("CW_ONESWEEP", 1), 3u);
+  c->onesweep_min = knob("CW_ONESWEEP_MIN", 1u << 16);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;
