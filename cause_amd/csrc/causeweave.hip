@@ -1893,6 +1893,13 @@ __host__ __device__ inline uint32_t tree_l_lds_bytes(uint32_t nmax) {
   return ((nmax + 31) / 32) * 8 + ((nmax + 1) / 2) * 4;  // two bitmaps + u16 table
 }
 
+// Sweep 2 of the tree without the barrier between pointer jumping and the
+// write-out (round 6; CW_S2_JUMP_BARRIER=1 at build time restores it for A/Bs).
+#ifndef CW_S2_JUMP_BARRIER
+#define CW_S2_JUMP_BARRIER 0
+#endif
+constexpr bool S2_JUMP_NOBAR = CW_S2_JUMP_BARRIER == 0;
+
 // MODE 4 (the one built; round 3's A/B variants 0-3 lost and are gone): a
 // group whose parent lies in the tile (69% of config-2 nodes) keeps its list
 // head in a direct table indexed by (class, parent - tile start): one exchange
@@ -2264,7 +2271,10 @@ __device__ __forceinline__ void tree_l_doc(
         }
       }
     }
-    __syncthreads();
+    // (no barrier here: a lane writes out only the entries it resolved itself,
+    // into tab and the links, which no jumping lane reads; the barrier after
+    // the writes keeps the next tile's T and its reads of tab apart -- round 6)
+    if (!S2_JUMP_NOBAR) __syncthreads();
     stamp(6);
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++) {
@@ -4309,9 +4319,12 @@ struct cw_ctx {
   uint32_t giant_log2k = 4;        // CW_GIANT_LOG2K: least splitter block of a giant document
   uint32_t fused = 1;              // CW_FUSED: front end + tree + tour in one kernel (k_weave_doc)
   bool x_hint = true;              // the last list weave may have flagged documents (exact.hip)
-  uint32_t onesweep = 1;           // CW_ONESWEEP: one-array sorts by the one-sweep passes
-                                   // (1: 4,096-key tiles of 512 threads, 2: 8,192 of 1,024,
-                                   // 3: 8,192 of 512; 0: histogram-scan-scatter)
+  uint32_t onesweep = 4;           // CW_ONESWEEP: one-array sorts by the one-sweep passes
+                                   // (tiles of 4,096 keys x 512 threads, 8,192 x 1,024,
+                                   // 8,192 x 512: 1-3 in one look-back chain, 4-6 in
+                                   // OS_RANGES chains; 0: histogram-scan-scatter)
+  uint32_t n_cu = 256;             // compute units of the device (histogram grid)
+  uint32_t os_exp = 0;             // CW_OS_EXP: onesweep timing experiments (wrong results)
   uint32_t onesweep_min = 1u << 16;  // CW_ONESWEEP_MIN: ... for arrays of at least this many keys
   const void *os_lb = nullptr;     // onesweep.hip's look-back words: buffer, size, last epoch
   size_t os_lb_words = 0;
@@ -4656,8 +4669,12 @@ template <typename K>
 int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA, uint32_t *vA,
                   K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N, K **kout,
                   uint32_t **vout, uint32_t *inv, uint32_t *vfinal) {
-  const uint32_t geom = c->onesweep;  // 1: 512 x 8, 2: 1024 x 8, 3: 512 x 16 keys a tile
-  const uint32_t TS = geom == 1 ? 4096 : 8192;
+  const uint32_t geom = c->onesweep;
+  // 1-3 one chain: 512 x 8, 1024 x 8, 512 x 16 keys a tile; 4-6 the same in
+  // OS_RANGES chains (4 = 1024 x 8, 5 = 512 x 8, 6 = 512 x 16)
+  const uint32_t shape = geom == 4 ? 2 : geom == 5 ? 1 : geom == 6 ? 3 : geom;
+  const uint32_t TS = shape == 1 ? 4096 : 8192;
+  const bool ranged = geom > 3;
   OsDigits dg{};
   dg.passes = (bits + OS_MAX_BITS - 1) / OS_MAX_BITS;
   if (dg.passes > OS_MAX_PASSES) return fail(c, "onesweep: %u key bits", bits);
@@ -4668,12 +4685,15 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
     sh += dg.bits[p];
   }
   const uint32_t T = (N + TS - 1) / TS;
-  const size_t hist_words = (size_t)OS_MAX_PASSES * OS_MAX_BINS;
-  uint32_t *hist = scratch_t<uint32_t>(c, "os_hist", 2 * hist_words);
-  const size_t lb_words = (size_t)T * OS_MAX_BINS;
+  const uint32_t nr = ranged ? OS_RANGES : 1u;
+  const uint32_t Tr = (T + nr - 1) / nr;  // tiles a range
+  const uint32_t rlen = ranged ? Tr * TS : 0xFFFFFFFFu;
+  const size_t hist_words = (size_t)OS_MAX_PASSES * OS_RANGES * OS_MAX_BINS;
+  uint32_t *hist = scratch_t<uint32_t>(c, "os_hist", 2 * hist_words + OS_MAX_PASSES * OS_RANGES);
+  const size_t lb_words = (size_t)Tr * nr * OS_MAX_BINS;
   unsigned long long *lb = scratch_t<unsigned long long>(c, "os_lb", lb_words);
   if (!hist || !lb) return fail(c, "out of device memory (onesweep)");
-  uint32_t *base = hist + hist_words;
+  uint32_t *base = hist + hist_words, *ticket = base + hist_words;
   // look-back words: cleared when the buffer is new or the 16-bit epoch wraps
   if (lb != c->os_lb || lb_words > c->os_lb_words || c->os_epoch + dg.passes > 0xFFFFu) {
     HIPCHK(c, hipMemsetAsync(lb, 0, c->bufs["os_lb"].bytes, c->stream));
@@ -4682,42 +4702,62 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
     c->os_epoch = 0;
   }
   HIPCHK(c, hipMemsetAsync(hist, 0, hist_words * 4, c->stream));
-  char nm[48];
-  snprintf(nm, sizeof nm, "%s_hist", tag);
-  {
-    Launch L(c, nm, (double)N * sizeof(K));
-    const uint32_t span = 256 * OS_HIST_ITEMS;
-    hipLaunchKernelGGL(k_os_hist<K>, dim3((N + span - 1) / span), dim3(256),
-                       (size_t)4 * dg.passes * OS_MAX_BINS * 4, c->stream, kin, N, dg, hist);
-  }
-  if (check_launch(c, nm)) return -1;
-  snprintf(nm, sizeof nm, "%s_scan", tag);
-  {
-    Launch L(c, nm, (double)dg.passes * OS_MAX_BINS * 8);
-    hipLaunchKernelGGL(k_os_scan, dim3(dg.passes), dim3(OS_MAX_BINS), 0, c->stream, hist, dg, base);
-  }
-  if (check_launch(c, nm)) return -1;
+  if (ranged) HIPCHK(c, hipMemsetAsync(ticket, 0, OS_MAX_PASSES * OS_RANGES * 4, c->stream));
+  char nm[48], nm_scan[48], nm_hist[48];
+  snprintf(nm, sizeof nm, "%s_scatter", tag);
+  snprintf(nm_scan, sizeof nm_scan, "%s_scan", tag);
+  snprintf(nm_hist, sizeof nm_hist, "%s_hist", tag);
+  // the digit counts of a pass's input (every pass at once when there is one
+  // range: the counts do not depend on the order), then the bucket bases
+  auto count = [&](const K *keys, uint32_t p0, uint32_t np) -> int {
+    OsDigits d = dg;
+    d.passes = np;
+    for (uint32_t q = 0; q < np; q++) {
+      d.shift[q] = dg.shift[p0 + q];
+      d.bits[q] = dg.bits[p0 + q];
+    }
+    uint32_t *hp = hist + (size_t)p0 * OS_RANGES * OS_MAX_BINS;
+    {
+      Launch L(c, nm_hist, (double)N * sizeof(K));
+      const uint32_t span = 256 * OS_HIST_ITEMS;
+      const uint32_t G = std::max(nr, std::min(c->n_cu * 4, (N + span - 1) / span) / nr * nr);
+      hipLaunchKernelGGL(k_os_hist<K>, dim3(G), dim3(256), (size_t)4 * np * OS_MAX_BINS * 4, c->stream,
+                         keys, N, d, rlen, nr, hp);
+    }
+    if (check_launch(c, nm_hist)) return -1;
+    {
+      Launch L(c, nm_scan, (double)np * OS_RANGES * OS_MAX_BINS * 8);
+      hipLaunchKernelGGL(k_os_scan, dim3(np), dim3(OS_MAX_BINS), 0, c->stream, hp, d,
+                         base + (size_t)p0 * OS_RANGES * OS_MAX_BINS);
+    }
+    return check_launch(c, nm_scan);
+  };
+  if (!ranged && count(kin, 0, dg.passes)) return -1;
   const K *ki = kin;
   const uint32_t *vi = vin;
   K *ko = kA;
   uint32_t *vo = vA;
-  snprintf(nm, sizeof nm, "%s_scatter", tag);
   for (uint32_t p = 0; p < dg.passes; p++) {
     const bool last = p + 1 == dg.passes;
     if (last && vfinal) {
       ko = nullptr;
       vo = vfinal;
     }
+    // ranged: each pass counts its own input by range (a range's counts depend
+    // on which keys the previous pass put there)
+    if (ranged && count(ki, p, 1)) return -1;
     const uint32_t ep = ++c->os_epoch;
+    const size_t pw = (size_t)p * OS_RANGES * OS_MAX_BINS;
     {
       Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)));
       auto launch = [&](auto kern, uint32_t nt) {
-        hipLaunchKernelGGL(kern, dim3(T), dim3(nt), 0, c->stream, ki, vi, ko, vo, last ? inv : nullptr,
-                           N, dg.shift[p], dg.bits[p], base + (size_t)p * OS_MAX_BINS, lb, ep);
+        hipLaunchKernelGGL(kern, dim3(Tr * nr), dim3(nt), 0, c->stream, ki, vi, ko, vo,
+                           last ? inv : nullptr, N, dg.shift[p], dg.bits[p], base + pw, lb, ep, c->os_exp,
+                           Tr, ranged ? ticket + p * OS_RANGES : nullptr);
       };
-      if (geom == 1) launch(k_os_pass<K, 512, 8>, 512);
-      else if (geom == 2) launch(k_os_pass<K, 1024, 8>, 1024);
-      else launch(k_os_pass<K, 512, 16>, 512);
+      if (shape == 1) launch(k_os_pass<K, 512, 8>, 512);
+      else if (shape == 3) launch(k_os_pass<K, 512, 16>, 512);
+      else launch(k_os_pass<K, 1024, 8>, 1024);
     }
     if (check_launch(c, nm)) return -1;
     ki = ko;
@@ -6860,6 +6900,9 @@ int cw_ctx_create(int device, cw_ctx **out) {
       c->lds_max = (uint32_t)lds;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) == hipSuccess) c->hbm_total = tot;
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+      c->n_cu = (uint32_t)ncu;
   }
   auto knob = [](const char *name, uint32_t dflt) {
     const char *v = getenv(name);
@@ -6894,8 +6937,9 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->fused = knob("CW_FUSED", 1);
   c->xfold = knob("CW_XFOLD", 0);
   c->x_round_cap = std::max(1u, knob("CW_X_ROUND_CAP", 48));
-  c->onesweep = std::min(knob("CW_ONESWEEP", 1), 3u);
+  c->onesweep = std::min(knob("CW_ONESWEEP", 4), 6u);
   c->onesweep_min = knob("CW_ONESWEEP_MIN", 1u << 16);
+  c->os_exp = knob("CW_OS_EXP", 0);
   c->front_slot_groups = std::max(1u, std::min(knob("CW_FRONT_SLOT", 65536), 131072u) / 16);
   c->front_min_avg = knob("CW_FRONT_MIN_AVG", 1024);
   *out = c;

@@ -38,7 +38,7 @@ def _check(w, k, bits):
     assert np.array_equal(io, order.astype(np.uint32))
 
 
-@pytest.mark.parametrize("geom", ["1", "2", "3"])
+@pytest.mark.parametrize("geom", ["1", "2", "3", "4", "5", "6"])
 def test_onesweep_geometries(monkeypatch, geom):
     monkeypatch.setenv("CW_ONESWEEP", geom)
     with abi.Weaver(0) as w:
@@ -54,7 +54,7 @@ def test_onesweep_equals_the_hist_scan_scatter_passes(monkeypatch):
     monkeypatch.setenv("CW_ONESWEEP", "0")
     with abi.Weaver(0) as w:
         ref = w.sort_keys(k, 35)
-    monkeypatch.setenv("CW_ONESWEEP", "1")
+    monkeypatch.delenv("CW_ONESWEEP")  # the default geometry
     with abi.Weaver(0) as w:
         w.reset_kernel_stats()
         w.set_profiling(True)
@@ -65,13 +65,16 @@ def test_onesweep_equals_the_hist_scan_scatter_passes(monkeypatch):
             again = w.sort_keys(k, 35)
             assert np.array_equal(again[1], ref[1])
     assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
-    assert st["ksort_scatter"][0] == 4 and st["ksort_hist"][0] == 1  # 4 passes, one histogram
+    # 4 passes; the ranged default counts each pass's input (one histogram
+    # launch a pass), the single-chain geometries all passes at once
+    assert st["ksort_scatter"][0] == 4 and st["ksort_hist"][0] == 4
 
 
-def test_onesweep_keys32(monkeypatch):
+@pytest.mark.parametrize("geom", ["1", "4", "5"])
+def test_onesweep_keys32(monkeypatch, geom):
     import torch
 
-    monkeypatch.setenv("CW_ONESWEEP", "1")
+    monkeypatch.setenv("CW_ONESWEEP", geom)
     rng = np.random.default_rng(3)
     with abi.Weaver(0) as w:
         for n, bits in ((70_000, 32), (1_000_001, 21)):
