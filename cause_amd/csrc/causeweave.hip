@@ -1301,6 +1301,12 @@ __host__ __device__ inline uint32_t front_lds_bytes(uint32_t nmax, uint32_t sg) 
 // null (the tree reads the class bitmaps).
 // U1 / U2 / U3: items a thread keeps in flight in the directory, rank and
 // input-index passes (the fused kernel's front end is latency-bound: CW_FRONT_U)
+// Where the fused front end writes the yarns' site bytes (round 6 A/B).
+#ifndef CW_SITE8_RANKPASS
+#define CW_SITE8_RANKPASS 0
+#endif
+constexpr bool SITE8_PASS1 = CW_SITE8_RANKPASS == 0;
+
 template <int NT, typename PT = uint32_t, typename VT = uint32_t, uint32_t U1 = 4, uint32_t U2 = 4,
           uint32_t U3 = 4>
 __device__ __forceinline__ bool front_doc(
@@ -1355,6 +1361,10 @@ __device__ __forceinline__ bool front_doc(
     for (uint32_t u = 0; u < U1; u++) {
       if (i0 + u * NT >= n) continue;
       mx = max(mx, x[u]);
+      // the site of every input for the yarns (k_yarn_doc): one coalesced byte,
+      // written in this pass, whose loads are few and early (CW_SITE8_RANKPASS = 1
+      // at build time: in the rank pass, as round 5 had it)
+      if (SITE8_PASS1 && site8) lane_at(site8 + base, i0 + u * NT) = (uint8_t)((x[u] >> site_shift) & site_mask);
       if (x[u] >= lim) {
         far = true;
         continue;
@@ -1453,7 +1463,7 @@ __device__ __forceinline__ bool front_doc(
       }
       lane_at(rankD, i) = (uint16_t)min(r, 0xFFFFu);
       // the site of every input for the yarns (k_yarn_doc): one coalesced byte
-      if (site8) lane_at(site8 + base, i) = (uint8_t)((k[u] >> site_shift) & site_mask);
+      if (!SITE8_PASS1 && site8) lane_at(site8 + base, i) = (uint8_t)((k[u] >> site_shift) & site_mask);
     }
   }
   if (st) atomicOr(&bst, st);
