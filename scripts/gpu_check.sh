@@ -30,7 +30,7 @@ for s in $steps; do
         tag=$(echo $pass | tr ' ' '_')
         (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace \
           --pmc $pass --output-format csv -d "$R/$P/pmc_$tag" -o run -- \
-          python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu ${PMC_BENCH_ARGS:-} > "$R/$P/pmc_$tag.log" 2>&1)
+          python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu --no-refresh --no-h2d --check-docs 0 ${PMC_BENCH_ARGS:-} > "$R/$P/pmc_$tag.log" 2>&1)
       done ;;
     list)
       (cd /tmp && rocprofv3 -L > "$R/gpurun_out/counters.txt" 2>&1) ;;

@@ -16,7 +16,7 @@ pmc() {  # $1 = dir, $2 = seconds, rest = bench args
   for pass in FETCH_SIZE WRITE_SIZE; do
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 $lim rocprofv3 --kernel-trace --pmc $pass \
       --output-format csv -d "$R/$dir/pmc_$pass" -o run -- \
-      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu --no-refresh "$@" > "$R/$dir/pmc_$pass.log" 2>&1)
+      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu --no-refresh --check-docs 0 "$@" > "$R/$dir/pmc_$pass.log" 2>&1)
     echo "pmc $dir $pass ok"
   done
 }

@@ -51,7 +51,16 @@ def main():
         if not sym.startswith("k_"):  # torch's own kernels (status readbacks)
             continue
         name = stat_name(sym)
-        if name.startswith("radix_") or name.startswith("gscan_"):
+        if name.startswith("os_"):
+            # the one-sweep sort (onesweep.hip): by key width on the giant path,
+            # as the histogram-scan-scatter kernels below; its scan is one block
+            if not a.workload.startswith(("config1", "config5")) or name.startswith("os_scan") or \
+                    "<" not in sym:
+                continue
+            width = "idsort" if "unsigned long" in sym else "gsort"
+            part = "scatter" if name.startswith("os_pass") else "hist"
+            name = f"{width}_{part}"
+        elif name.startswith("radix_") or name.startswith("gscan_"):
             # the library reports sort passes by what they sort: on the giant
             # path (configs 1, 5) the 64-bit keys are the id sort, the 32-bit
             # ones the group-key sort; elsewhere they are not separable
