@@ -881,6 +881,13 @@ __global__ __launch_bounds__(256) void k_gpack(const uint64_t *__restrict__ caus
   }
 }
 
+// the rank of every cause through the directory, par and kind by rank, the
+// domain checks (k_gjoin, k_gjoin_r)
+__device__ __forceinline__ void gjoin_items(const uint64_t (&ck)[GJOIN_ITEMS], const uint8_t (&kd)[GJOIN_ITEMS],
+                                            uint32_t i0, uint32_t n, uint64_t kmax,
+                                            const uint4 *__restrict__ dir, uint32_t *__restrict__ par,
+                                            uint8_t *__restrict__ skind, uint32_t *__restrict__ status);
+
 __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey,
                                                const uint32_t *__restrict__ sval,
                                                const uint64_t *__restrict__ cause_key,
@@ -914,6 +921,36 @@ __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey
       kd[k] = i < n ? kind[gi[k]] : 0;
     }
   }
+  gjoin_items(ck, kd, i0, n, kmax, dir, par, skind, status);
+}
+
+// k_gjoin after an id sort that carried cause | kind (OsPayload): both read in
+// rank order, as two u32 halves, instead of gathered by input index -- a
+// random line a node (round 5: 58 ms of config 5's 2e9 nodes)
+__global__ __launch_bounds__(256) void k_gjoin_r(const uint64_t *__restrict__ skey,
+                                                 const uint32_t *__restrict__ plo,
+                                                 const uint32_t *__restrict__ phi, uint32_t n,
+                                                 const uint4 *__restrict__ dir, uint64_t E,
+                                                 uint32_t *__restrict__ par, uint8_t *__restrict__ skind,
+                                                 uint32_t *__restrict__ status) {
+  const uint32_t i0 = blockIdx.x * (256 * GJOIN_ITEMS) + threadIdx.x;
+  const uint64_t kmax = min(skey[n - 1], E * GD_KEYS - 1);
+  uint64_t ck[GJOIN_ITEMS];
+  uint8_t kd[GJOIN_ITEMS];
+#pragma unroll
+  for (int k = 0; k < GJOIN_ITEMS; k++) {
+    const uint32_t i = i0 + k * 256;
+    const uint32_t lo = i < n ? plo[i] : 0u, hi = i < n ? phi[i] : 0u;
+    ck[k] = (uint64_t)(hi & 0xFFFFFFu) << 32 | lo;
+    kd[k] = (uint8_t)(hi >> 24);
+  }
+  gjoin_items(ck, kd, i0, n, kmax, dir, par, skind, status);
+}
+
+__device__ __forceinline__ void gjoin_items(const uint64_t (&ck)[GJOIN_ITEMS], const uint8_t (&kd)[GJOIN_ITEMS],
+                                            uint32_t i0, uint32_t n, uint64_t kmax,
+                                            const uint4 *__restrict__ dir, uint32_t *__restrict__ par,
+                                            uint8_t *__restrict__ skind, uint32_t *__restrict__ status) {
   uint32_t st = 0;
 #pragma unroll
   for (int k = 0; k < GJOIN_ITEMS; k++) {
@@ -4318,6 +4355,7 @@ struct cw_ctx {
   uint32_t tree_l = 2048;          // CW_TREE_L: k_tree_l (tables in LDS) when the largest document fits: its tile (2048 or 1024; 0 = k_tree)
   uint32_t gdir = 32;              // CW_GDIR: MiB of global rank directory a giant document may use
   uint32_t gjoin = 1;              // CW_GJOIN: the giant path joins through a directory of its sorted ids
+  uint32_t id_payload = 1;         // CW_ID_PAYLOAD: the id sort carries cause | kind to rank order (round 6)
   uint32_t map_small = 1;          // CW_MAP_SMALL: one wave per key weave of <= 64 nodes
   uint32_t pack_sort = 1;          // CW_PACK_SORT: in-LDS sort of packs of small documents
   uint32_t giant_min = 1u << 16;   // CW_GIANT_MIN: a one-document batch this large uses the giant tree
@@ -4672,13 +4710,23 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 // and (kB,vB).
 #include "onesweep.hip"
 
+// The cause | kind payload of an id sort (OsPayload): its source, two pairs of
+// u32 half buffers for the passes, and where the last pass left it (lo_out ==
+// nullptr: the sort did not carry it -- not the one-sweep path).
+struct OsPayloadBufs {
+  const uint64_t *cause;
+  const uint8_t *kind;
+  uint32_t *lo[2], *hi[2];
+  uint32_t *lo_out, *hi_out;
+};
+
 // One array (one document, or rt's one list): the one-sweep passes
 // (onesweep.hip) -- one histogram launch for every pass, one scan launch, one
 // launch a pass.  Same contract as radix_sort.
 template <typename K>
 int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA, uint32_t *vA,
                   K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N, K **kout,
-                  uint32_t **vout, uint32_t *inv, uint32_t *vfinal) {
+                  uint32_t **vout, uint32_t *inv, uint32_t *vfinal, OsPayloadBufs *plb = nullptr) {
   const uint32_t geom = c->onesweep;
   // 1-3 one chain: 512 x 8, 1024 x 8, 512 x 16 keys a tile; 4-6 the same in
   // OS_RANGES chains (4 = 1024 x 8, 5 = 512 x 8, 6 = 512 x 16)
@@ -4758,15 +4806,28 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
     if (ranged && count(ki, p, 1)) return -1;
     const uint32_t ep = ++c->os_epoch;
     const size_t pw = (size_t)p * OS_RANGES * OS_MAX_BINS;
+    // the payload: packed from its source in pass 0, then the half buffers in turn
+    OsPayload pl{};
+    const bool carry = plb && sizeof(K) == 8 && shape == 2;
+    if (carry) {
+      pl.cause = p == 0 ? plb->cause : nullptr;
+      pl.kind = p == 0 ? plb->kind : nullptr;
+      pl.lo_in = p == 0 ? nullptr : plb->lo[(p + 1) & 1];
+      pl.hi_in = p == 0 ? nullptr : plb->hi[(p + 1) & 1];
+      pl.lo_out = plb->lo[p & 1];
+      pl.hi_out = plb->hi[p & 1];
+    }
     {
-      Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0)));
+      Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0) +
+                                   (carry ? (p == 0 ? 9 : 8) + 8 : 0)));
       auto launch = [&](auto kern, uint32_t nt) {
         hipLaunchKernelGGL(kern, dim3(Tr * nr), dim3(nt), 0, c->stream, ki, vi, ko, vo,
                            last ? inv : nullptr, N, dg.shift[p], dg.bits[p], base + pw, lb, ep, c->os_exp,
-                           Tr, ranged ? ticket + p * OS_RANGES : nullptr);
+                           Tr, ranged ? ticket + p * OS_RANGES : nullptr, pl);
       };
       if (shape == 1) launch(k_os_pass<K, 512, 8>, 512);
       else if (shape == 3) launch(k_os_pass<K, 512, 16>, 512);
+      else if (carry) launch(k_os_pass<K, 1024, 8, sizeof(K) == 8>, 1024);
       else launch(k_os_pass<K, 1024, 8>, 1024);
     }
     if (check_launch(c, nm)) return -1;
@@ -4777,6 +4838,11 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
   }
   *kout = const_cast<K *>(ki);
   *vout = const_cast<uint32_t *>(vi);
+  if (plb) {
+    const bool carried = sizeof(K) == 8 && shape == 2;
+    plb->lo_out = carried ? plb->lo[(dg.passes + 1) & 1] : nullptr;
+    plb->hi_out = carried ? plb->hi[(dg.passes + 1) & 1] : nullptr;
+  }
   return 0;
 }
 
@@ -4791,7 +4857,8 @@ template <typename K>
 int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K *kA,
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
                K **kout, uint32_t **vout, uint32_t *inv = nullptr, uint32_t *vfinal = nullptr,
-               const RSTab *rt = nullptr) {
+               const RSTab *rt = nullptr, OsPayloadBufs *plb = nullptr) {
+  if (plb) plb->lo_out = plb->hi_out = nullptr;  // (carried only by the one-sweep passes)
   auto &t = c->tab;
   const RSTab tt = rt ? *rt
                       : RSTab{t.T, (uint32_t)(t.doc_off.size() - 1), dev_tab(c, "t_tile_start"),
@@ -4818,7 +4885,7 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
   // one array (config 5's ids, the giant tree's cross-tile children): the
   // one-sweep passes (CW_ONESWEEP; 0 = the histogram-scan-scatter passes below)
   if (c->onesweep && tt.D == 1 && N >= c->onesweep_min)
-    return onesweep_sort<K>(c, tag, kin, vin, kA, vA, kB, vB, bits, shift0, N, kout, vout, inv, vfinal);
+    return onesweep_sort<K>(c, tag, kin, vin, kA, vA, kB, vB, bits, shift0, N, kout, vout, inv, vfinal, plb);
   const uint32_t maxd = std::min<uint32_t>(c->max_digit, MAX_DIGIT);
   const int passes = (int)((bits + maxd - 1) / maxd);
   uint32_t *hist = scratch_t<uint32_t>(c, "hist", (size_t)tt.T * (1u << ((bits + passes - 1) / passes)));
@@ -5549,9 +5616,23 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       }
     }
     if (!front_done) {
-    // 1. id sort
+    // 1. id sort (one giant document: carrying every node's cause and kind to
+    // rank order, in the giant tree's four u32 buffers, free until the tree)
+    const bool gd_join = is_giant(c, D, bt->doc_offsets) && c->gjoin && key_bits <= GD_MAX_BITS;
+    OsPayloadBufs plb{};
+    OsPayloadBufs *plp = nullptr;
+    if (gd_join && key_bits <= 55 && c->id_payload) {
+      plb.cause = cause_key;
+      plb.kind = kind;
+      plb.lo[0] = scratch_t<uint32_t>(c, "g_keyA", N);
+      plb.hi[0] = scratch_t<uint32_t>(c, "g_keyB", N);
+      plb.lo[1] = scratch_t<uint32_t>(c, "g_valA", N);
+      plb.hi[1] = scratch_t<uint32_t>(c, "g_valB", N);
+      if (!plb.lo[0] || !plb.hi[0] || !plb.lo[1] || !plb.hi[1]) return fail(c, "out of device memory (id sort)");
+      plp = &plb;
+    }
     if (radix_sort<uint64_t>(c, "idsort", id_key, nullptr, skA, svA, skB, svB, key_bits, 0, N,
-                             &skey, &sval))
+                             &skey, &sval, nullptr, nullptr, nullptr, plp))
       return -1;
 
     // 2. join
@@ -5559,9 +5640,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     // each cause with one line (no bucket index, no search)
     const uint64_t E = ((1ull << std::min(key_bits, 63u)) + GD_KEYS - 1) / GD_KEYS;
     uint32_t *gdir = nullptr;
-    if (is_giant(c, D, bt->doc_offsets) && c->gjoin && key_bits <= GD_MAX_BITS) {
-      gdir = scratch_t<uint32_t>(c, "gd_dir", E * GD_WORDS);
-    }
+    if (gd_join) gdir = scratch_t<uint32_t>(c, "gd_dir", E * GD_WORDS);
     if (gdir) {
       {
         Launch L(c, "index", (double)N * 8 + (double)N / 15 * 64);
@@ -5569,6 +5648,20 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
                            E, gdir, out->status);
       }
       if (check_launch(c, "index")) return -1;
+      if (plp && plb.lo_out) {
+        {
+          // SURVEY 8d's join bytes: the cause (with the kind) read, the parent
+          // rank and kind written -- all in rank order now
+          Launch L(c, "join", (double)N * (8 + 4 + 1));
+          hipLaunchKernelGGL(k_gjoin_r, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
+                             c->stream, skey, plb.lo_out, plb.hi_out, N, reinterpret_cast<const uint4 *>(gdir),
+                             E, par, skind, out->status);
+        }
+        if (check_launch(c, "join")) return -1;
+        // (the exact path gathers causes by input index: the carried ones go
+        // with the giant tree's buffers)
+        c->xfront = {skey, sval, reinterpret_cast<const uint4 *>(gdir), E, nullptr, N, false};
+      } else {
       // cause and kind packed in one word per input node when the ids leave
       // 9 bits (the id sort's other key buffer is free by now)
       uint64_t *ckk = key_bits <= 55 ? (skey == skA ? skB : skA) : nullptr;
@@ -5587,6 +5680,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
       }
       if (check_launch(c, "join")) return -1;
       c->xfront = {skey, sval, reinterpret_cast<const uint4 *>(gdir), E, ckk, N, false};
+      }
     } else {
     uint32_t *bkt = scratch_t<uint32_t>(c, "bkt", t.Btot);
     if (!bkt) return fail(c, "out of device memory (bucket index)");
@@ -6932,6 +7026,7 @@ int cw_ctx_create(int device, cw_ctx **out) {
   c->tree_l = knob("CW_TREE_L", 2048);
   c->gdir = knob("CW_GDIR", 32);
   c->gjoin = knob("CW_GJOIN", 1);
+  c->id_payload = knob("CW_ID_PAYLOAD", 1);
   c->glocal = knob("CW_GLOCAL", 1);
   c->glocal_min = knob("CW_GLOCAL_MIN", 1u << 20);
   c->map_small = knob("CW_MAP_SMALL", 1);

@@ -114,19 +114,38 @@ __global__ __launch_bounds__(OS_MAX_BINS) void k_os_scan(const uint32_t *__restr
   }
 }
 
+// A second value carried through the passes (PL): config 5's cause and kind,
+// packed cause | kind << 56 (causes of 2^56 and more as 2^56 - 1, above every
+// id of a sort this is used for) and kept as two u32 halves.  The first pass
+// packs it from the inputs (cause, kind by element index); the id sort then
+// leaves every rank's cause and kind in rank order, and the join reads them
+// sequentially instead of gathering them by input index (round 6).
+struct OsPayload {
+  const uint64_t *cause;  // pass 0's source (by element index)
+  const uint8_t *kind;
+  const uint32_t *lo_in, *hi_in;  // later passes' source
+  uint32_t *lo_out, *hi_out;
+};
+__device__ __forceinline__ uint64_t os_pack_ck(uint64_t c, uint8_t kd) {
+  constexpr uint64_t M56 = (1ull << 56) - 1;
+  return (c < M56 ? c : M56) | ((uint64_t)kd << 56);
+}
+
 // One LSD pass.  NT threads, IT keys a thread (wave-blocked: wave w holds the
 // tile's elements [w * IT * 64, (w + 1) * IT * 64)), digit = (key >> shift) &
 // (2^dbits - 1), dbits <= OS_MAX_BITS, NT >= 2^dbits.  vals_in == nullptr: the
 // value is the element's index.  keys_out == nullptr: values only.  inv: also
 // inv[value] = the element's sorted position (the last pass of a sort whose
-// values are input indices).
-template <typename K, int NT, int IT>
+// values are input indices).  PL: the payload above, staged through the key
+// buffer after the keys are out.
+template <typename K, int NT, int IT, bool PL = false>
 __global__ __launch_bounds__(NT) void k_os_pass(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
     uint32_t *__restrict__ vals_out, uint32_t *__restrict__ inv, uint32_t n, uint32_t shift,
     uint32_t dbits, const uint32_t *__restrict__ base, unsigned long long *lb, uint32_t epoch,
-    uint32_t exp, uint32_t tiles_per_range, uint32_t *__restrict__ ticket) {
+    uint32_t exp, uint32_t tiles_per_range, uint32_t *__restrict__ ticket, OsPayload pl) {
   constexpr uint32_t TS = NT * IT, NW = NT / 64;
+  static_assert(!PL || sizeof(K) == 8, "the payload is staged in a u64 key buffer");
   static_assert(NT >= OS_MAX_BINS, "one thread per bucket");
   const uint32_t EXPS = exp;
   __shared__ K skey[TS];
@@ -151,12 +170,17 @@ __global__ __launch_bounds__(NT) void k_os_pass(
   const uint32_t *const bx = base + (size_t)x * OS_MAX_BINS;
   K key[IT];
   uint32_t val[IT], dig[IT], pin[IT];
+  uint64_t pv[PL ? IT : 1];
 #pragma unroll
   for (uint32_t k = 0; k < IT; k++) {
     const uint32_t j = (w * IT + k) * 64 + lane;
     const bool v = j < len;
     key[k] = v ? keys_in[s + j] : (K)0;
     val[k] = v ? (vals_in ? vals_in[s + j] : s + j) : 0u;
+    if (PL) {
+      if (pl.cause) pv[k] = v ? os_pack_ck(pl.cause[s + j], pl.kind[s + j]) : 0ull;
+      else pv[k] = v ? ((uint64_t)pl.hi_in[s + j] << 32 | pl.lo_in[s + j]) : 0ull;
+    }
   }
   // rank of every key among the keys of its digit in its wave (stable: item
   // order, then lane order); the wave's LDS operations run in order, so the
@@ -206,6 +230,7 @@ __global__ __launch_bounds__(NT) void k_os_pass(
     const uint32_t j = (w * IT + k) * 64 + lane;
     if (j < len) {
       const uint32_t pos = bstart[dig[k]] + cw[w][dig[k]] + pin[k];
+      pin[k] = pos;  // (kept for the payload)
       skey[pos] = key[k];
       sval[pos] = val[k];
     }
@@ -256,13 +281,35 @@ __global__ __launch_bounds__(NT) void k_os_pass(
   }
   __syncthreads();
   // digit runs out, coalesced
-  for (uint32_t j = tid; j < (EXPS & 4u ? 0u : len); j += NT) {
+  uint32_t dk[PL ? IT : 1];
+#pragma unroll
+  for (uint32_t k = 0; k < IT; k++) {
+    const uint32_t j = tid + k * NT;
+    if (PL) dk[k] = 0xFFFFFFFFu;
+    if (j >= (EXPS & 4u ? 0u : len)) continue;
     const K kk = skey[j];
     uint32_t dst = goff[(uint32_t)(kk >> shift) & dmask] + j;
     if (EXPS) dst %= n;  // (an experiment's positions are garbage: keep them in the buffer)
+    if (PL) dk[k] = dst;
     if (keys_out) keys_out[dst] = kk;
     const uint32_t vv = sval[j];
     vals_out[dst] = vv;
     if (inv) inv[vv] = dst;
+  }
+  if (PL) {
+    // the payload through the key buffer: the same positions, the same runs
+    uint64_t *const sp = reinterpret_cast<uint64_t *>(skey);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++)
+      if ((w * IT + k) * 64 + lane < len) sp[pin[k]] = pv[k];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < IT; k++) {
+      if (dk[k] == 0xFFFFFFFFu) continue;
+      const uint64_t x = sp[tid + k * NT];
+      pl.lo_out[dk[k]] = (uint32_t)x;
+      pl.hi_out[dk[k]] = (uint32_t)(x >> 32);
+    }
   }
 }
