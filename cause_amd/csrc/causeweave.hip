@@ -776,19 +776,21 @@ __global__ __launch_bounds__(1024) void k_gd_add(uint32_t *__restrict__ dir, uin
 // has one writer, the block holding its first id ("lead"): ids at the start
 // of a block that continue the previous block's entry are left to that block,
 // which reads ahead for them (<= GD_KEYS ids).  Entries between two ids get
-// word 0 = the next id's index from that id's thread.
-constexpr uint32_t GDB_KEYS = 512;
+// word 0 = the next id's index from that id's thread.  The slots go through LDS
+// GDB_SLOTS at a time (round 6: 512 ids and a slot for each, 36 KB a block,
+// cleared whole -- four blocks a CU, 16 KB of ids in flight, 15.4 ms at config
+// 5's 2e9 ids; config 5's ids fill ~18 entries a 512-id block).
+constexpr uint32_t GDB_KEYS = 1024, GDB_SLOTS = 128;
 __global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ skey, uint32_t n,
                                                   uint64_t E, uint32_t *__restrict__ dir,
                                                   uint32_t *__restrict__ status) {
   constexpr uint32_t KT = GDB_KEYS / 256;  // consecutive ids a thread
-  __shared__ uint32_t sbits[GDB_KEYS][GD_WORDS];
-  __shared__ uint64_t sent[GDB_KEYS];
+  __shared__ uint32_t sbits[GDB_SLOTS][GD_WORDS];
+  __shared__ uint64_t sent[GDB_SLOTS];
   __shared__ uint32_t wtot[4];
   const uint32_t tid = threadIdx.x, i0 = blockIdx.x * GDB_KEYS;
   const uint32_t i1 = min(i0 + GDB_KEYS, n);
   auto ent = [&](uint64_t x) { return min(x / GD_KEYS, E - 1); };  // (ids past E: flagged)
-  for (uint32_t w = tid; w < GDB_KEYS * GD_WORDS; w += 256) (&sbits[0][0])[w] = 0;
   uint64_t key[KT];
   bool lead[KT];
   uint32_t nl = 0, st = 0;
@@ -800,10 +802,13 @@ __global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ s
 #pragma unroll
   for (uint32_t k = 0; k < KT; k++) {
     const uint32_t i = i0 + tid * KT + k;
+    key[k] = i < i1 ? skey[i] : 0ull;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < KT; k++) {
+    const uint32_t i = i0 + tid * KT + k;
     lead[k] = false;
-    key[k] = 0;
     if (i >= i1) continue;
-    key[k] = skey[i];
     const uint64_t xp = k > 0 ? key[k - 1] : prev;
     if (i > 0 && xp == key[k]) st |= CW_STATUS_DUP;
     if (key[k] / GD_KEYS >= E) st |= CW_STATUS_INTERNAL;  // an id beyond key_bits
@@ -819,41 +824,53 @@ __global__ __launch_bounds__(256) void k_gd_build(const uint64_t *__restrict__ s
     }
   }
   uint32_t nslot;
-  const uint32_t s0 = block_exscan<256>(nl, wtot, &nslot);  // (its barriers order the clear)
+  const uint32_t s0 = block_exscan<256>(nl, wtot, &nslot);
   // an id's slot: the leads at or before it, less one; none: the previous
   // block's entry (skipped)
   uint32_t slot[KT], seen = s0;
 #pragma unroll
   for (uint32_t k = 0; k < KT; k++) {
     const uint32_t i = i0 + tid * KT + k;
-    if (lead[k]) {
-      sent[seen] = ent(key[k]);
-      sbits[seen][0] = i;
-      seen++;
-    }
-    slot[k] = seen > 0 && i < i1 ? seen - 1 : GDB_KEYS;
+    if (lead[k]) seen++;
+    slot[k] = seen > 0 && i < i1 ? seen - 1 : 0xFFFFFFFFu;
   }
-  __syncthreads();
+  for (uint32_t r0 = 0; r0 < nslot; r0 += GDB_SLOTS) {
+    const uint32_t ns = min(GDB_SLOTS, nslot - r0);
+    for (uint32_t w = tid; w < ns * GD_WORDS; w += 256) (&sbits[0][0])[w] = 0;
+    __syncthreads();
 #pragma unroll
-  for (uint32_t k = 0; k < KT; k++)
-    if (slot[k] < GDB_KEYS && key[k] / GD_KEYS < E) {
-      const uint32_t b = (uint32_t)(key[k] % GD_KEYS);
-      atomicOr(&sbits[slot[k]][1 + (b >> 5)], 1u << (b & 31));
-    }
-  if (nslot > 0) {  // the next block's ids in this block's last entry
-    const uint64_t elast = sent[nslot - 1];
-    for (uint32_t j = i1 + tid; j < n && j < i1 + GD_KEYS; j += 256) {
-      const uint64_t x = skey[j];
-      if (ent(x) == elast && x / GD_KEYS < E) {
-        const uint32_t b = (uint32_t)(x % GD_KEYS);
-        atomicOr(&sbits[nslot - 1][1 + (b >> 5)], 1u << (b & 31));
+    for (uint32_t k = 0; k < KT; k++) {
+      const uint32_t q = slot[k] - r0;
+      if (lead[k] && q < ns) {
+        sent[q] = ent(key[k]);
+        sbits[q][0] = i0 + tid * KT + k;
       }
     }
-  }
-  __syncthreads();
-  for (uint32_t w = tid; w < nslot * GD_WORDS; w += 256) {
-    const uint32_t s = w / GD_WORDS, wd = w % GD_WORDS;
-    dir[sent[s] * GD_WORDS + wd] = sbits[s][wd];
+    __syncthreads();  // (word 0 before the bits' atomics of the same line)
+#pragma unroll
+    for (uint32_t k = 0; k < KT; k++) {
+      const uint32_t q = slot[k] - r0;
+      if (q < ns && key[k] / GD_KEYS < E) {
+        const uint32_t b = (uint32_t)(key[k] % GD_KEYS);
+        atomicOr(&sbits[q][1 + (b >> 5)], 1u << (b & 31));
+      }
+    }
+    if (r0 + ns == nslot) {  // the next block's ids in this block's last entry
+      const uint64_t elast = sent[ns - 1];
+      for (uint32_t j = i1 + tid; j < n && j < i1 + GD_KEYS; j += 256) {
+        const uint64_t x = skey[j];
+        if (ent(x) == elast && x / GD_KEYS < E) {
+          const uint32_t b = (uint32_t)(x % GD_KEYS);
+          atomicOr(&sbits[ns - 1][1 + (b >> 5)], 1u << (b & 31));
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < ns * GD_WORDS; w += 256) {
+      const uint32_t q = w / GD_WORDS, wd = w % GD_WORDS;
+      dir[sent[q] * GD_WORDS + wd] = sbits[q][wd];
+    }
+    __syncthreads();
   }
   const uint64_t any = __ballot(st != 0);
   if (any) {
