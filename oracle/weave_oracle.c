@@ -29,18 +29,65 @@ static int cmp_lnode(const void *a, const void *b) {
   return x->idx < y->idx ? -1 : (x->idx > y->idx);
 }
 
+/* Lists of at least this many nodes sort by LSD radix passes and find their
+ * causes by one merge against the sorted ids (the same answers as qsort and
+ * a binary search a node, O(n) passes instead: one list of 5e8 nodes is
+ * checked in minutes, not hours). */
+#define OR_RADIX_MIN 16384
+#define OR_RADIX_BITS 11
+
+static unsigned sig_bits(uint64_t x) {
+  unsigned b = 0;
+  while (x) { b++; x >>= 1; }
+  return b;
+}
+
+/* Stable LSD radix sort of n records of `size` bytes by their u64 at offset 0
+ * (the records' own order breaks ties); returns the sorted copy, frees the other. */
+static void *radix_by_u64(void *a, size_t n, size_t size, unsigned bits) {
+  void *t = malloc((n ? n : 1) * size);
+  size_t *cnt = (size_t *)malloc(sizeof(size_t) << OR_RADIX_BITS);
+  const size_t nb = (size_t)1 << OR_RADIX_BITS;
+  for (unsigned sh = 0; sh < bits; sh += OR_RADIX_BITS) {
+    memset(cnt, 0, sizeof(size_t) * nb);
+    const char *src = (const char *)a;
+    for (size_t i = 0; i < n; i++) cnt[(*(const uint64_t *)(src + i * size) >> sh) & (nb - 1)]++;
+    size_t run = 0;
+    for (size_t b = 0; b < nb; b++) {
+      const size_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+    char *dst = (char *)t;
+    for (size_t i = 0; i < n; i++) {
+      const char *e = src + i * size;
+      memcpy(dst + cnt[(*(const uint64_t *)e >> sh) & (nb - 1)]++ * size, e, size);
+    }
+    void *x = a;
+    a = t;
+    t = x;
+  }
+  free(t);
+  free(cnt);
+  return a;
+}
+
 /* (sort (::s/nodes ct)) -- list.cljc:28.  Map entries compare by key first and
- * ids are unique map keys, so this is an id sort (ties only for DUP docs). */
+ * ids are unique map keys, so this is an id sort (ties only for DUP docs,
+ * kept in input order either way). */
 static lnode *sorted_nodes(size_t n, const uint64_t *id, const uint64_t *cause,
                            const uint8_t *kind) {
   lnode *s = (lnode *)malloc((n ? n : 1) * sizeof(lnode));
+  uint64_t mx = 0;
   for (size_t i = 0; i < n; i++) {
     s[i].id = id[i];
     s[i].cause = cause[i];
     s[i].idx = (uint32_t)i;
     s[i].kind = kind[i];
+    if (id[i] > mx) mx = id[i];
   }
-  qsort(s, n, sizeof(lnode), cmp_lnode);
+  if (n < OR_RADIX_MIN) qsort(s, n, sizeof(lnode), cmp_lnode);
+  else s = (lnode *)radix_by_u64(s, n, sizeof(lnode), sig_bits(mx));
   return s;
 }
 
@@ -54,16 +101,46 @@ static size_t find_id(const lnode *s, size_t n, uint64_t key) {
   return (lo < n && s[lo].id == key) ? lo : n;
 }
 
-/* Domain checks shared with the HIP path (CW_STATUS_*). */
-static uint32_t doc_status(const lnode *s, size_t n) {
+/* Every rank's cause as a rank: find_id(s, n, s[r].cause) for each r, n when
+ * absent.  Large lists: the (cause, rank) pairs radix-sorted by cause (causes
+ * past the largest id clamped to one value: all absent) and merged against the
+ * sorted ids. */
+typedef struct {
+  uint64_t c;
+  uint64_t r;
+} crec;
+static uint32_t *cause_ranks(const lnode *s, size_t n) {
+  uint32_t *cr = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+  if (n < OR_RADIX_MIN) {
+    for (size_t r = 0; r < n; r++) cr[r] = (uint32_t)find_id(s, n, s[r].cause);
+    return cr;
+  }
+  const uint64_t top = s[n - 1].id + 1 ? s[n - 1].id + 1 : s[n - 1].id;
+  crec *a = (crec *)malloc(n * sizeof(crec));
+  for (size_t r = 0; r < n; r++) {
+    a[r].c = s[r].cause < top ? s[r].cause : top;
+    a[r].r = r;
+  }
+  a = (crec *)radix_by_u64(a, n, sizeof(crec), sig_bits(top));
+  size_t j = 0;
+  for (size_t k = 0; k < n; k++) {
+    const uint64_t c = a[k].c;
+    while (j < n && s[j].id < c) j++;
+    cr[a[k].r] = (uint32_t)(j < n && s[j].id == c && c == s[a[k].r].cause ? j : n);
+  }
+  free(a);
+  return cr;
+}
+
+/* Domain checks shared with the HIP path (CW_STATUS_*); cr = cause_ranks. */
+static uint32_t doc_status(const lnode *s, size_t n, const uint32_t *cr) {
   uint32_t st = 0;
   if (n == 0 || !(s[0].kind & OR_ROOT)) st |= OR_ST_ROOT;
   for (size_t r = 0; r < n; r++) {
     if (r > 0 && (s[r].kind & OR_ROOT)) st |= OR_ST_ROOT;
     if (r > 0 && s[r].id == s[r - 1].id) st |= OR_ST_DUP;
     if (r == 0) continue;
-    size_t c = find_id(s, n, s[r].cause);
-    if (c == n) st |= OR_ST_ORPHAN;
+    if (cr[r] == n) st |= OR_ST_ORPHAN;
     else if (s[r].cause >= s[r].id) st |= OR_ST_NON_LAMPORT;
   }
   return st;
@@ -154,7 +231,9 @@ static size_t weave_node_lit(lnode *W, size_t L, const lnode *nm, const lnode *m
 uint32_t or_list_fold_literal(size_t n, const uint64_t *id, const uint64_t *cause,
                               const uint8_t *kind, uint32_t *out_perm) {
   lnode *s = sorted_nodes(n, id, cause, kind);
-  uint32_t st = doc_status(s, n);
+  uint32_t *cr = cause_ranks(s, n);
+  uint32_t st = doc_status(s, n, cr);
+  free(cr);
   lnode *W = (lnode *)malloc((n ? n : 1) * sizeof(lnode));
   seenset seen;
   seen_init(&seen, n);
@@ -171,7 +250,9 @@ uint32_t or_list_insert_sequence(size_t n, const uint64_t *id, const uint64_t *c
                                  const uint8_t *kind, const uint32_t *order,
                                  uint32_t *out_perm) {
   lnode *s = sorted_nodes(n, id, cause, kind);
-  uint32_t st = doc_status(s, n);
+  uint32_t *cr = cause_ranks(s, n);
+  uint32_t st = doc_status(s, n, cr);
+  free(cr);
   free(s);
   lnode *W = (lnode *)malloc((n ? n : 1) * sizeof(lnode));
   seenset seen;
@@ -193,8 +274,10 @@ uint32_t or_list_insert_sequence(size_t n, const uint64_t *id, const uint64_t *c
 uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause,
                              const uint8_t *kind, uint32_t *out_perm) {
   lnode *s = sorted_nodes(n, id, cause, kind);
-  uint32_t st = doc_status(s, n);
+  uint32_t *cr = cause_ranks(s, n);
+  uint32_t st = doc_status(s, n, cr);
   if (st) {
+    free(cr);
     free(s);
     or_list_fold_literal(n, id, cause, kind, out_perm);
     return st;
@@ -203,7 +286,7 @@ uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause
   uint32_t *next = (uint32_t *)malloc(n * sizeof(uint32_t));
   next[0] = END;
   for (size_t r = 1; r < n; r++) {
-    uint32_t at = (uint32_t)find_id(s, n, s[r].cause);
+    uint32_t at = cr[r];
     if (!is_special(s[r].kind))
       while (next[at] != END && is_special(s[next[at]].kind)) at = next[at];
     next[r] = next[at];
@@ -212,6 +295,7 @@ uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause
   size_t p = 0;
   for (uint32_t v = 0; v != END; v = next[v]) out_perm[p++] = s[v].idx;
   free(next);
+  free(cr);
   free(s);
   return st;
 }
@@ -226,13 +310,14 @@ uint32_t or_list_fold_linked(size_t n, const uint64_t *id, const uint64_t *cause
 uint32_t or_list_fold_general(size_t n, const uint64_t *id, const uint64_t *cause,
                               const uint8_t *kind, uint32_t *out_perm) {
   lnode *s = sorted_nodes(n, id, cause, kind);
-  uint32_t st = doc_status(s, n);
+  uint32_t *cr = cause_ranks(s, n);
+  uint32_t st = doc_status(s, n, cr);
   const uint32_t END = UINT32_MAX, HEAD = UINT32_MAX - 1, NIL = UINT32_MAX - 2;
   uint32_t *par = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
   uint32_t *next = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
   uint8_t *early = (uint8_t *)calloc(n ? n : 1, 1);
   for (size_t r = 0; r < n; r++) {
-    size_t c = find_id(s, n, s[r].cause);
+    size_t c = cr[r];
     par[r] = s[r].cause == OR_NIL ? NIL : (c == n ? END : (uint32_t)c);
     if (c < n && c > r) early[c] = 1;
   }
@@ -261,54 +346,71 @@ uint32_t or_list_fold_general(size_t n, const uint64_t *id, const uint64_t *caus
   }
   size_t k = 0;
   for (uint32_t v = head; v != END; v = next[v]) out_perm[k++] = s[v].idx;
-  free(par); free(next); free(early); free(s);
+  free(par); free(next); free(early); free(cr); free(s);
   return st;
 }
 
-/* preorder of the effective tree, walked with the same
- * (first child, next sibling, parent) links the HIP Euler walk uses. */
+/* preorder of the effective tree -- a node, then its special
+ * children by descending id, then its non-special children by descending id,
+ * each with its subtree.  Computed in passes over the ranks instead of a walk
+ * (ids ascend with rank and every cause is older, so a parent's rank is below
+ * its children's): subtree sizes bottom-up, each child's offset among its
+ * siblings (the sizes of the siblings before it), positions top-down.  Every
+ * pass is sequential over the ranks with one independent random access a
+ * node: a 2e7-node list 3x faster than walking (first child, next sibling,
+ * parent) links, which the HIP Euler walk uses and this replaced (round 6). */
 uint32_t or_list_eff_preorder(size_t n, const uint64_t *id, const uint64_t *cause,
                               const uint8_t *kind, uint32_t *out_perm) {
   lnode *s = sorted_nodes(n, id, cause, kind);
-  uint32_t st = doc_status(s, n);
+  uint32_t *cr = cause_ranks(s, n);
+  uint32_t st = doc_status(s, n, cr);
   if (st) {
+    free(cr);
     free(s);
     or_list_fold_literal(n, id, cause, kind, out_perm);
     return st;
   }
-  const uint32_t NONE = 0; /* rank 0 is the root, never a child */
-  uint32_t *par = (uint32_t *)calloc(n, sizeof(uint32_t));
-  uint32_t *eff = (uint32_t *)calloc(n, sizeof(uint32_t));
-  uint32_t *spec_head = (uint32_t *)calloc(n, sizeof(uint32_t));
-  uint32_t *norm_head = (uint32_t *)calloc(n, sizeof(uint32_t));
-  uint32_t *sib = (uint32_t *)calloc(n, sizeof(uint32_t));
+  uint8_t *sp = (uint8_t *)malloc(n);
+  uint32_t *eff = (uint32_t *)malloc(n * sizeof(uint32_t));
+  uint32_t *up = (uint32_t *)malloc(n * sizeof(uint32_t));  /* nearest non-special ancestor-or-self */
+  for (size_t r = 0; r < n; r++) sp[r] = (uint8_t)is_special(s[r].kind);
+  up[0] = 0;
+  eff[0] = 0;
   for (size_t r = 1; r < n; r++) {
-    uint32_t c = (uint32_t)find_id(s, n, s[r].cause);
-    par[r] = c;
-    if (!is_special(s[r].kind))
-      while (is_special(s[c].kind)) c = par[c];
-    eff[r] = c;
-    /* ascending r, pushed at the head => descending id order per class */
-    if (is_special(s[r].kind)) { sib[r] = spec_head[c]; spec_head[c] = (uint32_t)r; }
-    else { sib[r] = norm_head[c]; norm_head[c] = (uint32_t)r; }
+    const uint32_t c = cr[r];
+    /* a non-special climbs through special causes; a special keeps its cause */
+    eff[r] = sp[r] ? c : up[c];
+    up[r] = sp[r] ? up[c] : (uint32_t)r;
   }
-  size_t p = 0;
-  uint32_t v = 0;
-  out_perm[p++] = s[0].idx;
-  for (;;) {
-    uint32_t fc = spec_head[v] ? spec_head[v] : norm_head[v];
-    if (fc != NONE) { v = fc; out_perm[p++] = s[v].idx; continue; }
-    for (;;) {
-      if (v == 0) goto done;
-      uint32_t ns = sib[v];
-      if (ns == NONE && is_special(s[v].kind)) ns = norm_head[eff[v]];
-      if (ns != NONE) { v = ns; break; }
-      v = eff[v];
+  free(up);
+  uint32_t *size = cr;  /* (the cause ranks are done) */
+  uint32_t *spec_tot = (uint32_t *)calloc(n, sizeof(uint32_t));
+  for (size_t r = 0; r < n; r++) size[r] = 1;
+  for (size_t r = n - 1; r >= 1; r--) {
+    size[eff[r]] += size[r];
+    if (sp[r]) spec_tot[eff[r]] += size[r];
+  }
+  /* siblings before a child: for a special, the specials with larger ids; for a
+   * non-special, every special and the non-specials with larger ids */
+  uint32_t *acc_s = (uint32_t *)calloc(n, sizeof(uint32_t)), *acc_n = (uint32_t *)calloc(n, sizeof(uint32_t));
+  uint32_t *pos = (uint32_t *)malloc(n * sizeof(uint32_t));  /* the offset before, then the position */
+  for (size_t r = n - 1; r >= 1; r--) {
+    const uint32_t c = eff[r];
+    if (sp[r]) {
+      pos[r] = acc_s[c];
+      acc_s[c] += size[r];
+    } else {
+      pos[r] = spec_tot[c] + acc_n[c];
+      acc_n[c] += size[r];
     }
-    out_perm[p++] = s[v].idx;
   }
-done:
-  free(par); free(eff); free(spec_head); free(norm_head); free(sib); free(s);
+  free(acc_s);
+  free(acc_n);
+  free(spec_tot);
+  pos[0] = 0;
+  for (size_t r = 1; r < n; r++) pos[r] += pos[eff[r]] + 1;
+  for (size_t r = 0; r < n; r++) out_perm[pos[r]] = s[r].idx;
+  free(pos); free(eff); free(sp); free(cr); free(s);
   return st;
 }
 
