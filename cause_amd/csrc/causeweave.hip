@@ -941,25 +941,26 @@ __global__ __launch_bounds__(256) void k_gjoin(const uint64_t *__restrict__ skey
   gjoin_items(ck, kd, i0, n, kmax, dir, par, skind, status);
 }
 
-// k_gjoin after an id sort that carried cause | kind (OsPayload): both read in
-// rank order, as two u32 halves, instead of gathered by input index -- a
-// random line a node (round 5: 58 ms of config 5's 2e9 nodes)
+// k_gjoin after an id sort that carried cause and kind (OsPayload, kb key
+// bits): both read in rank order, lo and hi, instead of gathered by input index
+// -- a random line a node (round 5: 58 ms of config 5's 2e9 nodes)
 __global__ __launch_bounds__(256) void k_gjoin_r(const uint64_t *__restrict__ skey,
                                                  const uint32_t *__restrict__ plo,
-                                                 const uint32_t *__restrict__ phi, uint32_t n,
-                                                 const uint4 *__restrict__ dir, uint64_t E,
+                                                 const uint32_t *__restrict__ phi, uint32_t kb,
+                                                 uint32_t n, const uint4 *__restrict__ dir, uint64_t E,
                                                  uint32_t *__restrict__ par, uint8_t *__restrict__ skind,
                                                  uint32_t *__restrict__ status) {
   const uint32_t i0 = blockIdx.x * (256 * GJOIN_ITEMS) + threadIdx.x;
   const uint64_t kmax = min(skey[n - 1], E * GD_KEYS - 1);
+  const uint32_t ch = os_pl_ch(kb);
   uint64_t ck[GJOIN_ITEMS];
   uint8_t kd[GJOIN_ITEMS];
 #pragma unroll
   for (int k = 0; k < GJOIN_ITEMS; k++) {
     const uint32_t i = i0 + k * 256;
     const uint32_t lo = i < n ? plo[i] : 0u, hi = i < n ? phi[i] : 0u;
-    ck[k] = (uint64_t)(hi & 0xFFFFFFu) << 32 | lo;
-    kd[k] = (uint8_t)(hi >> 24);
+    ck[k] = (uint64_t)(hi & ((1u << ch) - 1)) << 32 | lo;  // (2^kb: no id, above kmax)
+    kd[k] = (uint8_t)(hi >> ch);
   }
   gjoin_items(ck, kd, i0, n, kmax, dir, par, skind, status);
 }
@@ -4727,14 +4728,15 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 // and (kB,vB).
 #include "onesweep.hip"
 
-// The cause | kind payload of an id sort (OsPayload): its source, two pairs of
-// u32 half buffers for the passes, and where the last pass left it (lo_out ==
-// nullptr: the sort did not carry it -- not the one-sweep path).
+// The cause / kind payload of an id sort (OsPayload): its source, two u32
+// buffers for lo in turn, one for the last pass's hi, and where the last pass
+// left lo (lo_out == nullptr: the sort did not carry it -- not the one-sweep
+// path, or more than OS_PL_MAX_BITS key bits).
 struct OsPayloadBufs {
   const uint64_t *cause;
   const uint8_t *kind;
-  uint32_t *lo[2], *hi[2];
-  uint32_t *lo_out, *hi_out;
+  uint32_t *lo[2], *hi;
+  uint32_t *lo_out;
 };
 
 // One array (one document, or rt's one list): the one-sweep passes
@@ -4825,27 +4827,36 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
     const size_t pw = (size_t)p * OS_RANGES * OS_MAX_BINS;
     // the payload: packed from its source in pass 0, then the half buffers in turn
     OsPayload pl{};
-    const bool carry = plb && sizeof(K) == 8 && shape == 2;
+    const bool carry = plb && sizeof(K) == 8 && shape == 2 && shift0 == 0 && bits <= OS_PL_MAX_BITS && ko;
     if (carry) {
       pl.cause = p == 0 ? plb->cause : nullptr;
       pl.kind = p == 0 ? plb->kind : nullptr;
       pl.lo_in = p == 0 ? nullptr : plb->lo[(p + 1) & 1];
-      pl.hi_in = p == 0 ? nullptr : plb->hi[(p + 1) & 1];
       pl.lo_out = plb->lo[p & 1];
-      pl.hi_out = plb->hi[p & 1];
+      pl.hi_out = last ? plb->hi : nullptr;
+      pl.kb = bits;
     }
     {
       Launch L(c, nm, (double)N * ((ko ? 2 : 1) * sizeof(K) + (vi ? 8 : 4) + (last && inv ? 4 : 0) +
-                                   (carry ? (p == 0 ? 9 : 8) + 8 : 0)));
+                                   (carry ? (p == 0 ? 9 : 4) + 4 + (last ? 4 : 0) : 0)));
       auto launch = [&](auto kern, uint32_t nt) {
         hipLaunchKernelGGL(kern, dim3(Tr * nr), dim3(nt), 0, c->stream, ki, vi, ko, vo,
                            last ? inv : nullptr, N, dg.shift[p], dg.bits[p], base + pw, lb, ep, c->os_exp,
                            Tr, ranged ? ticket + p * OS_RANGES : nullptr, pl);
       };
-      if (shape == 1) launch(k_os_pass<K, 512, 8>, 512);
-      else if (shape == 3) launch(k_os_pass<K, 512, 16>, 512);
-      else if (carry) launch(k_os_pass<K, 1024, 8, sizeof(K) == 8>, 1024);
-      else launch(k_os_pass<K, 1024, 8>, 1024);
+      if (shape == 1) {
+        launch(k_os_pass<K, 512, 8>, 512);
+      } else if (shape == 3) {
+        launch(k_os_pass<K, 512, 16>, 512);
+      } else if (!carry) {
+        launch(k_os_pass<K, 1024, 8>, 1024);
+      } else if constexpr (sizeof(K) == 8) {  // (the payload's role: a kernel each)
+        const int m = 1 | (p == 0 ? 2 : 0) | (last ? 4 : 0);
+        if (m == 1) launch(k_os_pass<K, 1024, 8, 1>, 1024);
+        else if (m == 3) launch(k_os_pass<K, 1024, 8, 3>, 1024);
+        else if (m == 5) launch(k_os_pass<K, 1024, 8, 5>, 1024);
+        else launch(k_os_pass<K, 1024, 8, 7>, 1024);
+      }
     }
     if (check_launch(c, nm)) return -1;
     ki = ko;
@@ -4856,9 +4867,8 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
   *kout = const_cast<K *>(ki);
   *vout = const_cast<uint32_t *>(vi);
   if (plb) {
-    const bool carried = sizeof(K) == 8 && shape == 2;
+    const bool carried = sizeof(K) == 8 && shape == 2 && shift0 == 0 && bits <= OS_PL_MAX_BITS && !vfinal;
     plb->lo_out = carried ? plb->lo[(dg.passes + 1) & 1] : nullptr;
-    plb->hi_out = carried ? plb->hi[(dg.passes + 1) & 1] : nullptr;
   }
   return 0;
 }
@@ -4875,7 +4885,7 @@ int radix_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin, K 
                uint32_t *vA, K *kB, uint32_t *vB, uint32_t bits, uint32_t shift0, uint32_t N,
                K **kout, uint32_t **vout, uint32_t *inv = nullptr, uint32_t *vfinal = nullptr,
                const RSTab *rt = nullptr, OsPayloadBufs *plb = nullptr) {
-  if (plb) plb->lo_out = plb->hi_out = nullptr;  // (carried only by the one-sweep passes)
+  if (plb) plb->lo_out = nullptr;  // (carried only by the one-sweep passes)
   auto &t = c->tab;
   const RSTab tt = rt ? *rt
                       : RSTab{t.T, (uint32_t)(t.doc_off.size() - 1), dev_tab(c, "t_tile_start"),
@@ -5638,14 +5648,13 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     const bool gd_join = is_giant(c, D, bt->doc_offsets) && c->gjoin && key_bits <= GD_MAX_BITS;
     OsPayloadBufs plb{};
     OsPayloadBufs *plp = nullptr;
-    if (gd_join && key_bits <= 55 && c->id_payload) {
+    if (gd_join && key_bits <= OS_PL_MAX_BITS && c->id_payload) {
       plb.cause = cause_key;
       plb.kind = kind;
       plb.lo[0] = scratch_t<uint32_t>(c, "g_keyA", N);
-      plb.hi[0] = scratch_t<uint32_t>(c, "g_keyB", N);
-      plb.lo[1] = scratch_t<uint32_t>(c, "g_valA", N);
-      plb.hi[1] = scratch_t<uint32_t>(c, "g_valB", N);
-      if (!plb.lo[0] || !plb.hi[0] || !plb.lo[1] || !plb.hi[1]) return fail(c, "out of device memory (id sort)");
+      plb.lo[1] = scratch_t<uint32_t>(c, "g_keyB", N);
+      plb.hi = scratch_t<uint32_t>(c, "g_valA", N);
+      if (!plb.lo[0] || !plb.lo[1] || !plb.hi) return fail(c, "out of device memory (id sort)");
       plp = &plb;
     }
     if (radix_sort<uint64_t>(c, "idsort", id_key, nullptr, skA, svA, skB, svB, key_bits, 0, N,
@@ -5671,8 +5680,8 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
           // rank and kind written -- all in rank order now
           Launch L(c, "join", (double)N * (8 + 4 + 1));
           hipLaunchKernelGGL(k_gjoin_r, dim3((N + 256 * GJOIN_ITEMS - 1) / (256 * GJOIN_ITEMS)), B256, 0,
-                             c->stream, skey, plb.lo_out, plb.hi_out, N, reinterpret_cast<const uint4 *>(gdir),
-                             E, par, skind, out->status);
+                             c->stream, skey, plb.lo_out, plb.hi, key_bits, N,
+                             reinterpret_cast<const uint4 *>(gdir), E, par, skind, out->status);
         }
         if (check_launch(c, "join")) return -1;
         // (the exact path gathers causes by input index: the carried ones go

@@ -32,6 +32,11 @@ constexpr uint32_t MIN_LOG2K = 3;                 // >= 8 nodes per splitter blo
 // in use with the caller's 21 B a node of inputs and outputs).
 constexpr uint64_t GIANT_CAP32_BYTES = 100;
 
+// An id sort's carried cause and kind (onesweep.hip OsPayload): the cause's
+// bits above 32 and the kind ride in the key's bits above kb, CH + 8 of them.
+constexpr uint32_t OS_PL_MAX_BITS = 43;  // CH + 8 <= 64 - kb
+__host__ __device__ constexpr uint32_t os_pl_ch(uint32_t kb) { return (kb > 32 ? kb : 32) - 31; }
+
 // link word (u32): low 29 bits = the node's preorder successor (SUCC_END for the
 // last node), bit 31 = the node renders, bit 30 = the node is a splitter, bit
 // 29 = the successor is thr[low bits] (a thread the giant-document tree left

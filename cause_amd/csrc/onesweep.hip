@@ -114,22 +114,26 @@ __global__ __launch_bounds__(OS_MAX_BINS) void k_os_scan(const uint32_t *__restr
   }
 }
 
-// A second value carried through the passes (PL): config 5's cause and kind,
-// packed cause | kind << 56 (causes of 2^56 and more as 2^56 - 1, above every
-// id of a sort this is used for) and kept as two u32 halves.  The first pass
-// packs it from the inputs (cause, kind by element index); the id sort then
-// leaves every rank's cause and kind in rank order, and the join reads them
-// sequentially instead of gathering them by input index (round 6).
+// A second value carried through the passes (PL): config 5's cause and kind.
+// With kb = the sort's key bits (<= OS_PL_MAX_BITS) the cause is clamped to
+// c' = min(cause, 2^kb) (2^kb: no id -- above every id of the sort), and
+//   lo = c' & 0xFFFFFFFF           a u32 array beside the values,
+//   hi = c' >> 32 | kind << CH     in the key's unused bits above kb,
+// CH = max(kb, 32) - 31; the last pass writes the bare ids and hi into its own
+// u32 array.  The first pass packs it from the inputs (cause, kind by element
+// index); the id sort then leaves every rank's cause and kind in rank order,
+// and the join reads them sequentially instead of gathering them by input
+// index (round 6).  (A u64 payload a key cost 16 B a key and pass instead of
+// 8: +6.9 ms over the passes of 2^29 keys.)  OS_PL_MAX_BITS, os_pl_ch:
+// cw_internal.h.
 struct OsPayload {
-  const uint64_t *cause;  // pass 0's source (by element index)
+  const uint64_t *cause;  // the first pass's source (by element index)
   const uint8_t *kind;
-  const uint32_t *lo_in, *hi_in;  // later passes' source
-  uint32_t *lo_out, *hi_out;
+  const uint32_t *lo_in;  // later passes' source
+  uint32_t *lo_out;
+  uint32_t *hi_out;       // the last pass: hi of every key, the keys written bare
+  uint32_t kb;
 };
-__device__ __forceinline__ uint64_t os_pack_ck(uint64_t c, uint8_t kd) {
-  constexpr uint64_t M56 = (1ull << 56) - 1;
-  return (c < M56 ? c : M56) | ((uint64_t)kd << 56);
-}
 
 // One LSD pass.  NT threads, IT keys a thread (wave-blocked: wave w holds the
 // tile's elements [w * IT * 64, (w + 1) * IT * 64)), digit = (key >> shift) &
@@ -137,15 +141,19 @@ __device__ __forceinline__ uint64_t os_pack_ck(uint64_t c, uint8_t kd) {
 // value is the element's index.  keys_out == nullptr: values only.  inv: also
 // inv[value] = the element's sorted position (the last pass of a sort whose
 // values are input indices).  PL: the payload above, staged through the key
-// buffer after the keys are out.
-template <typename K, int NT, int IT, bool PL = false>
+// buffer after the keys are out.  PLM (the payload's role in this pass, each a
+// kernel of its own so no pass carries another's code): 0 none, bit 1 carried
+// (lo in and out), bit 2 the first pass (packed from cause / kind), bit 4 the
+// last pass (bare ids, hi apart).
+template <typename K, int NT, int IT, int PLM = 0>
 __global__ __launch_bounds__(NT) void k_os_pass(
     const K *__restrict__ keys_in, const uint32_t *__restrict__ vals_in, K *__restrict__ keys_out,
     uint32_t *__restrict__ vals_out, uint32_t *__restrict__ inv, uint32_t n, uint32_t shift,
     uint32_t dbits, const uint32_t *__restrict__ base, unsigned long long *lb, uint32_t epoch,
     uint32_t exp, uint32_t tiles_per_range, uint32_t *__restrict__ ticket, OsPayload pl) {
   constexpr uint32_t TS = NT * IT, NW = NT / 64;
-  static_assert(!PL || sizeof(K) == 8, "the payload is staged in a u64 key buffer");
+  constexpr bool PL = PLM != 0, PL_FIRST = (PLM & 2) != 0, PL_LAST = (PLM & 4) != 0;
+  static_assert(!PL || sizeof(K) == 8, "hi rides in a u64 key");
   static_assert(NT >= OS_MAX_BINS, "one thread per bucket");
   const uint32_t EXPS = exp;
   __shared__ K skey[TS];
@@ -170,16 +178,20 @@ __global__ __launch_bounds__(NT) void k_os_pass(
   const uint32_t *const bx = base + (size_t)x * OS_MAX_BINS;
   K key[IT];
   uint32_t val[IT], dig[IT], pin[IT];
-  uint64_t pv[PL ? IT : 1];
+  uint32_t pv[PL ? IT : 1];
 #pragma unroll
   for (uint32_t k = 0; k < IT; k++) {
     const uint32_t j = (w * IT + k) * 64 + lane;
     const bool v = j < len;
     key[k] = v ? keys_in[s + j] : (K)0;
     val[k] = v ? (vals_in ? vals_in[s + j] : s + j) : 0u;
-    if (PL) {
-      if (pl.cause) pv[k] = v ? os_pack_ck(pl.cause[s + j], pl.kind[s + j]) : 0ull;
-      else pv[k] = v ? ((uint64_t)pl.hi_in[s + j] << 32 | pl.lo_in[s + j]) : 0ull;
+    if (PL_FIRST) {
+      const uint64_t c = v ? min(pl.cause[s + j], 1ull << pl.kb) : 0ull;
+      const uint64_t kd = v ? pl.kind[s + j] : 0u;
+      pv[k] = (uint32_t)c;
+      key[k] |= ((c >> 32) | kd << os_pl_ch(pl.kb)) << pl.kb;
+    } else if (PL) {
+      pv[k] = v ? pl.lo_in[s + j] : 0u;
     }
   }
   // rank of every key among the keys of its digit in its wave (stable: item
@@ -291,25 +303,25 @@ __global__ __launch_bounds__(NT) void k_os_pass(
     uint32_t dst = goff[(uint32_t)(kk >> shift) & dmask] + j;
     if (EXPS) dst %= n;  // (an experiment's positions are garbage: keep them in the buffer)
     if (PL) dk[k] = dst;
-    if (keys_out) keys_out[dst] = kk;
+    if (PL_LAST) {  // (bare ids, hi apart)
+      keys_out[dst] = kk & ((1ull << pl.kb) - 1);
+      pl.hi_out[dst] = (uint32_t)(kk >> pl.kb);
+    } else if (keys_out) {
+      keys_out[dst] = kk;
+    }
     const uint32_t vv = sval[j];
     vals_out[dst] = vv;
     if (inv) inv[vv] = dst;
   }
   if (PL) {
-    // the payload through the key buffer: the same positions, the same runs
-    uint64_t *const sp = reinterpret_cast<uint64_t *>(skey);
+    // lo through the value buffer: the same positions, the same runs
     __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < IT; k++)
-      if ((w * IT + k) * 64 + lane < len) sp[pin[k]] = pv[k];
+      if ((w * IT + k) * 64 + lane < len) sval[pin[k]] = pv[k];
     __syncthreads();
 #pragma unroll
-    for (uint32_t k = 0; k < IT; k++) {
-      if (dk[k] == 0xFFFFFFFFu) continue;
-      const uint64_t x = sp[tid + k * NT];
-      pl.lo_out[dk[k]] = (uint32_t)x;
-      pl.hi_out[dk[k]] = (uint32_t)(x >> 32);
-    }
+    for (uint32_t k = 0; k < IT; k++)
+      if (dk[k] != 0xFFFFFFFFu) pl.lo_out[dk[k]] = sval[tid + k * NT];
   }
 }
