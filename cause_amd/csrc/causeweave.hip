@@ -4731,12 +4731,15 @@ uint32_t *dev_tab(cw_ctx *c, const char *name) { return (uint32_t *)c->bufs[name
 // The cause / kind payload of an id sort (OsPayload): its source, two u32
 // buffers for lo in turn, one for the last pass's hi, and where the last pass
 // left lo (lo_out == nullptr: the sort did not carry it -- not the one-sweep
-// path, or more than OS_PL_MAX_BITS key bits).
+// path, or more than OS_PL_MAX_BITS key bits).  An id past the key bits sets
+// CW_STATUS_INTERNAL in *status (the keys are cut to the key bits: nothing
+// downstream reads past the directory).
 struct OsPayloadBufs {
   const uint64_t *cause;
   const uint8_t *kind;
   uint32_t *lo[2], *hi;
   uint32_t *lo_out;
+  uint32_t *status;
 };
 
 // One array (one document, or rt's one list): the one-sweep passes
@@ -4834,6 +4837,7 @@ int onesweep_sort(cw_ctx *c, const char *tag, const K *kin, const uint32_t *vin,
       pl.lo_in = p == 0 ? nullptr : plb->lo[(p + 1) & 1];
       pl.lo_out = plb->lo[p & 1];
       pl.hi_out = last ? plb->hi : nullptr;
+      pl.status = plb->status;
       pl.kb = bits;
     }
     {
@@ -5651,6 +5655,7 @@ int weave_lists_device(cw_ctx *c, const cw_list_batch *bt, const uint64_t *id_ke
     if (gd_join && key_bits <= OS_PL_MAX_BITS && c->id_payload) {
       plb.cause = cause_key;
       plb.kind = kind;
+      plb.status = out->status;
       plb.lo[0] = scratch_t<uint32_t>(c, "g_keyA", N);
       plb.lo[1] = scratch_t<uint32_t>(c, "g_keyB", N);
       plb.hi = scratch_t<uint32_t>(c, "g_valA", N);

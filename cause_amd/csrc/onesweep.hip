@@ -132,6 +132,7 @@ struct OsPayload {
   const uint32_t *lo_in;  // later passes' source
   uint32_t *lo_out;
   uint32_t *hi_out;       // the last pass: hi of every key, the keys written bare
+  uint32_t *status;       // the first pass: CW_STATUS_INTERNAL for an id past kb bits
   uint32_t kb;
 };
 
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(NT) void k_os_pass(
   K key[IT];
   uint32_t val[IT], dig[IT], pin[IT];
   uint32_t pv[PL ? IT : 1];
+  bool wide = false;  // (an id past kb bits: the caller's key_bits are wrong)
 #pragma unroll
   for (uint32_t k = 0; k < IT; k++) {
     const uint32_t j = (w * IT + k) * 64 + lane;
@@ -189,11 +191,13 @@ __global__ __launch_bounds__(NT) void k_os_pass(
       const uint64_t c = v ? min(pl.cause[s + j], 1ull << pl.kb) : 0ull;
       const uint64_t kd = v ? pl.kind[s + j] : 0u;
       pv[k] = (uint32_t)c;
-      key[k] |= ((c >> 32) | kd << os_pl_ch(pl.kb)) << pl.kb;
+      wide |= (key[k] >> pl.kb) != 0;
+      key[k] = (key[k] & ((1ull << pl.kb) - 1)) | ((c >> 32) | kd << os_pl_ch(pl.kb)) << pl.kb;
     } else if (PL) {
       pv[k] = v ? pl.lo_in[s + j] : 0u;
     }
   }
+  if (PL_FIRST && __ballot(wide) && lane == 0) atomicOr(pl.status, (uint32_t)CW_STATUS_INTERNAL);
   // rank of every key among the keys of its digit in its wave (stable: item
   // order, then lane order); the wave's LDS operations run in order, so the
   // counter row needs no barrier inside the wave
