@@ -28,6 +28,7 @@ case "$1" in
     python scripts/pmc_summary.py $O/pmc26 > $O/pmc_table_config5.txt
     python scripts/pmc_traffic.py $O/pmc26 gpurun_out/pmc_traffic.json --workload config5
     rm -rf $O/pmc26/pmc_*
+    cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json  # (the lines below read it)
     timeout -k 10 300 python bench.py --config 5 > $O/c5.json 2> $O/c5.err
     timeout -k 10 300 python bench.py --config 1 > $O/c1.json 2> $O/c1.err
     echo "scaled ok" ;;
@@ -36,7 +37,9 @@ case "$1" in
     python scripts/pmc_summary.py $O/pmcfull > $O/pmc_table_config5full.txt
     python scripts/pmc_traffic.py $O/pmcfull gpurun_out/pmc_traffic.json --workload config5full
     rm -rf $O/pmcfull/pmc_*
+    cp gpurun_out/pmc_traffic.json profiles/pmc_traffic.json  # (the lines below read it)
     timeout -k 10 600 python bench.py --config 5 --giant 2000000001 --cache /tmp/c5cache --steps 2 --warmup 1 > $O/c5full.json 2> $O/c5full.err
+    timeout -k 10 300 python bench.py --config 5 > $O/c5.json 2> $O/c5.err
     echo "full ok" ;;
   *) echo "usage: $0 scaled|full"; exit 2 ;;
 esac

@@ -14,7 +14,10 @@ def load(d):
     out = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv")):
         for row in csv.DictReader(open(f)):
-            name = row["Kernel_Name"].split("(")[0].replace("void ", "")
+            # (kernels in an anonymous namespace -- onesweep.hip's -- carry it
+            # as a prefix: without it the name is cut at its parenthesis)
+            kn = row["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+            name = kn.split("(")[0]
             out[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return out
 

@@ -72,16 +72,28 @@ def main():
             name = f"{width}_{part}"
         if name in ("gd_first", "gd_set_sorted"):  # the library's "index" stat: both kernels
             name = "index"
-        # several symbols under one library stat (the ranking's levels, the
-        # index's two kernels): their bytes per launch add up
         r = res.setdefault(name, {"kernel": [], "fetch_kib": 0.0, "write_kib": 0.0,
                                   "launches_sampled": ctr.get("launches")})
         r["kernel"].append(sym)
-        r["fetch_kib"] += ctr["FETCH_SIZE"]
-        r["write_kib"] += ctr["WRITE_SIZE"]
+        if name.startswith(("idsort_", "gsort_")):
+            # one launch a pass, a kernel per pass role (the id sort's payload):
+            # the average a launch, weighted by each symbol's launches
+            n = ctr.get("launches") or 1
+            r["_n"] = r.get("_n", 0) + n
+            r["_f"] = r.get("_f", 0.0) + ctr["FETCH_SIZE"] * n
+            r["_w"] = r.get("_w", 0.0) + ctr["WRITE_SIZE"] * n
+            r["fetch_kib"], r["write_kib"] = r["_f"] / r["_n"], r["_w"] / r["_n"]
+            r["launches_sampled"] = r["_n"]
+        else:
+            # several symbols under one library stat (the ranking's levels, the
+            # index's two kernels): their bytes per launch add up
+            r["fetch_kib"] += ctr["FETCH_SIZE"]
+            r["write_kib"] += ctr["WRITE_SIZE"]
         r["bytes"] = (2 * r["fetch_kib"] + r["write_kib"]) * 1024.0
     for r in res.values():
         r["kernel"] = " + ".join(r["kernel"])
+        for k in ("_n", "_f", "_w"):
+            r.pop(k, None)
     table = {"build_id": bid, "workloads": {}}
     if os.path.exists(a.out):
         old = json.load(open(a.out))
