@@ -8,9 +8,10 @@ and its render bits.
 VERDICT r5 weak #8: the full-size test (test_gpu_giant_full.py) stitches
 config-2 documents under one root, so no cause crosses a document; this one has
 long-range causes.  The default size, 2^25 nodes, runs in the GPU suite in
-well under a minute; CW_GIANT_OWN_N sets another (round 6 ran 5e8 nodes:
-profiles/r06_giant_own_5e8.log -- the single-document generator and the oracle
-run on one host core, ~8 minutes, progress written to gpurun_out/).
+well under a minute; CW_GIANT_OWN_N sets another (round 6 ran 5e8 nodes and
+config 5's full 2,000,000,001: profiles/r06_giant_own_5e8.log, _2e9.log -- the
+single-document generator and the oracle run on one host core, 14 minutes at
+full size, progress written to gpurun_out/).
 """
 import dataclasses
 import os
