@@ -433,6 +433,35 @@ def test_giant_path_small_documents(giant_weaver):
         check_batch(giant_weaver, b.offsets, b.id_key, b.cause_key, b.kind, b.layout)
 
 
+@pytest.mark.parametrize("target_bits", [0, 31, 32, 33, 40, 43, 44])
+def test_id_sort_carried_cause_key_widths(target_bits):
+    """The id sort's carried cause and kind (round 6, onesweep.hip OsPayload:
+    the cause's low 32 bits beside the index, its high bits and the kind above
+    the key bits) at key widths either side of 32 and up to OS_PL_MAX_BITS = 43
+    (44 takes the join that gathers by input index): one 150k-node list, ids
+    and causes shifted left into a wider tx field (order and layout kept), with
+    orphan causes (one past an id, one past the largest id) and a nil cause --
+    the exact path then reweaves it -- against the oracle's general fold."""
+    spec = dataclasses.replace(gen.CONFIG2, nodes_per_doc=150_000, seed=57)
+    off, idk, ck, kd = gen.generate(spec, 0, 1)
+    lay0 = spec.layout()
+    shift = max(0, target_bits - lay0.key_bits)
+    lay = pack.KeyLayout(lay0.ts_bits, lay0.site_bits, lay0.tx_bits + shift)
+    nil = ck == np.uint64(pack.NIL)
+    idk = idk << np.uint64(shift)
+    ck = ck << np.uint64(shift)
+    ck[nil] = np.uint64(pack.NIL)
+    rng = np.random.default_rng(target_bits)
+    some = rng.choice(np.arange(1, len(ck)), 40, replace=False)
+    ck[some[:20]] = idk[some[:20]] + np.uint64(1)           # (1 << shift > 1: not an id)
+    ck[some[20:39]] = idk.max() + np.uint64(1 << shift)      # past the largest id
+    ck[some[39]] = np.uint64(pack.NIL)
+    assert lay.key_bits == max(lay0.key_bits, target_bits)
+    with _weaver_with({"CW_GDIR": "0", "CW_GIANT_MIN": "0"}) as w:
+        res = check_batch(w, off, idk, ck, kd, lay, method=oracle.METHOD_GENERAL, yarns=False)
+    assert res.status[0] & abi.STATUS_ORPHAN
+
+
 def test_giant_join_misdeclared_key_bits():
     """ids wider than the declared key_bits on the sorted-id directory join
     (ADVICE r3): the directory is never read past its end, the list is flagged
