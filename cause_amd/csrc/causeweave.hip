@@ -3517,8 +3517,10 @@ __global__ __launch_bounds__(NT) void k_weave_doc(
 // every rank's input index (sval16).  In LDS: the site of every rank (a byte,
 // 50 KB at 50,001 nodes: two workgroups a CU); the yarn is written straight
 // from a wave-level multisplit, each wave's ranks going to 16 runs that grow a
-// chunk at a time.  9 B a node: site 1 + rank 2 + sval 2 in, yarn_perm 4 out
-// (+1 B in the fused kernel for the site byte).  Round 4 placed the yarns
+// chunk at a time; each wave's per-site counts are LDS atomics made while the
+// sites are scattered (round 6: a pass of ballots over the site bytes before,
+// yarns 1.46-1.49 -> 1.36-1.40 ms).  9 B a node: site 1 + rank 2 + sval 2 in,
+// yarn_perm 4 out (+1 B in the fused kernel for the site byte).  Round 4 placed the yarns
 // inside the fused kernel's front end: +3.9 ms on a config-2 step; round 5:
 // an LDS-staged version there, +3.8 ms; this kernel with per-thread rank
 // ranges and the yarn staged in LDS, 2.60 ms; the multisplit with no staging,
@@ -3541,6 +3543,9 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
   const uint32_t base = doc_off[d], n = doc_off[d + 1] - base;
   uint8_t *const sr = reinterpret_cast<uint8_t *>(lds_y);
   for (uint32_t w = tid; w < (n + 3) / 4; w += NT) lds_y[w] = 0xFFFFFFFFu;  // (no site: a DUP doc)
+  constexpr uint32_t NW = NT / 64;
+  const uint32_t perw = ((n + NW - 1) / NW + 63) & ~63u;  // ranks a wave places (pass B)
+  for (uint32_t w = tid; w < NW * 16; w += NT) (&wrow[0][0])[w] = 0;
   __syncthreads();
   // 1. the site of every rank (the fused kernel's front end wrote each input's
   // site byte beside its rank)
@@ -3555,7 +3560,12 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
     }
 #pragma unroll
     for (uint32_t u = 0; u < U; u++)
-      if (r[u] < n) sr[r[u]] = (uint8_t)x[u];
+      if (r[u] < n) {
+        sr[r[u]] = (uint8_t)x[u];
+        // each wave's per-site counts over the ranks it places, counted here
+        // rather than in a pass over the site bytes (round 6)
+        atomicAdd(&wrow[r[u] / perw][x[u] & 15u], 1u);
+      }
   }
   __syncthreads();
   // 2-3. a wave-level multisplit: wave wv owns a contiguous range of ranks and
@@ -3568,9 +3578,7 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
   // s's).  (Round 5 v3 gave each thread a contiguous range and sixteen 16-bit
   // counters: 2.55 ms a config-2 step, its counting and placement ALU-bound.)
   {
-    constexpr uint32_t NW = NT / 64;
     const uint32_t lane = tid & 63, wv = tid >> 6;
-    const uint32_t perw = ((n + NW - 1) / NW + 63) & ~63u;
     const uint32_t w0 = min(n, wv * perw), w1 = min(n, w0 + perw);
     // the lanes of site `st` among this chunk's ballots (st = 0xFF: none)
     auto site_mask = [&](uint32_t st, uint64_t valid, uint64_t b0, uint64_t b1, uint64_t b2,
@@ -3578,17 +3586,7 @@ __global__ __launch_bounds__(NT) void k_yarn_doc(const uint8_t *__restrict__ sit
       return valid & ((st & 1u) ? b0 : ~b0) & ((st & 2u) ? b1 : ~b1) & ((st & 4u) ? b2 : ~b2) &
              ((st & 8u) ? b3 : ~b3);
     };
-    // pass A: lane s (< 16) counts site s over the wave's range
-    uint32_t cnt = 0;
-    for (uint32_t c = w0; c < w1; c += 64) {
-      const uint32_t r = c + lane;
-      const uint32_t st = r < w1 ? sr[r] : 0xFFu;
-      const uint64_t valid = __ballot(st < 16u), b0 = __ballot(st & 1u), b1 = __ballot(st & 2u),
-                     b2 = __ballot(st & 4u), b3 = __ballot(st & 8u);
-      cnt += (uint32_t)__popcll(site_mask(lane, valid, b0, b1, b2, b3));
-    }
-    if (lane < 16) wrow[wv][lane] = cnt;
-    __syncthreads();
+    // (pass A, the per-site counts of the wave's ranks, came with the scatter)
     // lane s: the ranks of sites < s (all waves) + of site s in earlier waves
     uint32_t before = 0, tot = 0;
     if (lane < 16) {
